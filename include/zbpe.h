@@ -1,0 +1,116 @@
+/*
+ * zbpe.h -- C ABI of the MI355X BPE trainer (libzbpe.so, built from zig-bpe_amd/csrc).
+ *
+ * Drop-in boundary for the hot path of dbtreasure/zig-bpe: BasicTokenizer.train's pair
+ * count + merge loop (src/basic_tokenizer.zig:140-306) and its encode (:71-88). The Zig
+ * struct API (init/deinit/train/encode/decode/serializeMerges/deserializeMerges) stays on
+ * the host; it calls these entry points through `extern "C"` (see INTEGRATION.md for the
+ * Zig, ctypes and C++ bindings). Plain pointers and sizes only; no torch types.
+ *
+ * Ownership: inputs are borrowed for the duration of a call; outputs go to caller-allocated
+ * buffers sized from the arguments; device memory is owned by the context.
+ * Threading: one call at a time per context (the reference is single-threaded too).
+ * Errors: every entry point returns a zbpe_status; zbpe_last_error() gives the message.
+ */
+#ifndef ZBPE_H
+#define ZBPE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum zbpe_status {
+    ZBPE_OK = 0,
+    ZBPE_INVALID_VOCAB_SIZE = 1, /* TrainError.InvalidVocabSize (basic_tokenizer.zig:6-10,147-149) */
+    ZBPE_OUT_OF_MEMORY = 2,      /* TrainError.OutOfMemory (host or device allocation failed) */
+    ZBPE_DEVICE_ERROR = 3,       /* a HIP call or kernel failed; the Zig shim maps it to OutOfMemory */
+    ZBPE_COMM_ERROR = 4,         /* an RCCL collective failed */
+    ZBPE_INVALID_ARGUMENT = 5,   /* null pointer, size out of range, unsupported merge table */
+    ZBPE_INVALID_TOKEN = 6,      /* decode: token with no merge (error.InvalidToken, :101,125,135) */
+    ZBPE_INTERNAL = 7            /* an internal consistency check failed (bug) */
+} zbpe_status;
+
+typedef struct zbpe_ctx zbpe_ctx;
+
+/* Timing buckets mirror the reference's TimeStats (src/utils/time_statistics.zig:4-13) so the CPU
+ * and GPU breakdowns line up; the remaining fields are measurement counters. Times in seconds. */
+typedef struct zbpe_stats {
+    double count_pairs_s;     /* generateCodePointPairs + countCodePointPairs: initial histogram + per-merge scan */
+    double sort_pairs_s;      /* sortCodePointPairs + [0]: argmax over pair counts + Zig-order tie-break */
+    double replace_pair_s;    /* replaceTopPairWithNewToken: apply + count update + compaction */
+    double other_s;           /* upload, widen, host bookkeeping, synchronisation */
+    double total_s;           /* wall time of the call */
+    uint64_t count_pairs_calls, sort_pairs_calls, replace_pair_calls;
+    /* dominant kernel (zbpe_scan_pairs) measured with HIP events on the engine's stream */
+    uint64_t scan_launches;
+    double scan_kernel_s;     /* sum of scan kernel durations */
+    uint64_t scan_alg_bytes;  /* algorithmic bytes: 2 B per live token scanned */
+    uint64_t scan_read_bytes; /* bytes the scan actually streamed (live tokens + holes) */
+    uint64_t tie_iterations;  /* merges whose top count was shared by >1 pair */
+    uint64_t tie_fallbacks;   /* ties resolved by the exact first-occurrence emulation */
+    uint64_t compactions;
+    uint64_t self_pair_merges;
+    uint64_t final_tokens;    /* token-stream length after training (all ranks) */
+    uint64_t distinct_pairs;  /* live pairs after the last merge */
+    uint64_t pair_ids;        /* pair-table ids allocated (live + dead) */
+    uint64_t sum_tokens;      /* sum over merges of the stream length n_t */
+} zbpe_stats;
+
+/* Create a single-GPU context on HIP device `device`. */
+zbpe_status zbpe_create(int device, zbpe_ctx **out);
+
+/* Multi-GPU: one process per GPU. Rank 0 calls zbpe_comm_unique_id() and broadcasts the 128 bytes
+ * (e.g. with torch.distributed); every rank then calls zbpe_create_dist. The token stream is split
+ * into `world` contiguous shards; pair-count deltas are summed with an RCCL all-reduce each merge. */
+zbpe_status zbpe_comm_unique_id(void *out128);
+zbpe_status zbpe_create_dist(int device, int rank, int world, const void *unique_id128, zbpe_ctx **out);
+
+void zbpe_destroy(zbpe_ctx *ctx);
+const char *zbpe_last_error(const zbpe_ctx *ctx);
+
+/* BasicTokenizer.train (basic_tokenizer.zig:140-153): learn up to vocab_size-256 merges from `text`.
+ * out_triples: caller buffer of 3*(vocab_size-256) u16 {first, second, new_token} in training order.
+ * out_counts:  optional, vocab_size-256 u64 top counts ("had N occurrences", :309).
+ * verbose:     print the reference's per-merge line to stderr (:308-317).
+ * n == 0 or 1 yields zero merges ("No more pairs to merge. Stopping early.", :188-191).
+ * In a distributed context every rank passes the same full text. */
+zbpe_status zbpe_train(zbpe_ctx *ctx, const uint8_t *text, size_t n, uint16_t vocab_size, int verbose,
+                       uint16_t *out_triples, uint64_t *out_counts, size_t *out_n_merges, zbpe_stats *stats);
+
+/* Split form of zbpe_train for benchmarks: zbpe_upload stages this rank's shard of `text` in HBM;
+ * zbpe_train_resident trains from the resident bytes (inputs already in HBM when timing starts). */
+zbpe_status zbpe_upload(zbpe_ctx *ctx, const uint8_t *text, size_t n);
+zbpe_status zbpe_train_resident(zbpe_ctx *ctx, uint16_t vocab_size, int verbose, uint16_t *out_triples,
+                                uint64_t *out_counts, size_t *out_n_merges, zbpe_stats *stats);
+
+/* BasicTokenizer.encode (basic_tokenizer.zig:71-88): apply `n_merges` merges in order, left-greedy.
+ * out: caller buffer of n u16; *out_len receives the encoded length. */
+zbpe_status zbpe_encode(zbpe_ctx *ctx, const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n,
+                        uint16_t *out, size_t *out_len);
+
+/* Diagnostics used by the parity tests: recount every pair of the current token stream with the
+ * full-histogram kernel and compare with the incrementally maintained counts. Returns ZBPE_OK and
+ * *mismatches = 0 when they agree. Valid after zbpe_train*. */
+zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches);
+
+/* Tuning / test options: "debug_checks" (0/1), "exact_ties" (resolve every tie by the exact
+ * first-occurrence emulation and cross-check the GPU cluster test), "compact_den" (compact when
+ * holes > slots/den), "scan_blocks_per_cu". */
+zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
+
+/* Host-only diagnostic (no device work): the Zig 0.13 pair-map iteration order emulation used by
+ * the exact tie fallback. Given every live pair's first-occurrence position, key (first |
+ * second << 16) and count, returns the first pair in slot order whose count == top. */
+zbpe_status zbpe_zig_order_winner(const uint32_t *first_pos, const uint32_t *keys, const uint32_t *counts, size_t n,
+                                  uint32_t top, int call_after_last_insert, uint32_t *winner);
+
+/* Library version string. */
+const char *zbpe_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZBPE_H */

@@ -1,0 +1,132 @@
+"""CPU tests of the oracle (oracle/zig_ref.c) against the reference's own artefacts:
+Zig wyhash.zig known-answer vectors, merges.txt (config 1), the five inline tests of
+basic_tokenizer.zig:351-461 restated, and the committed seeded goldens."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import c1_golden, c1_merges_txt, c1_text, sha256, synth_goldens, synth_text
+
+
+def test_wyhash_known_answers():
+    assert O.selftest() == 0  # Zig 0.13 lib/std/hash/wyhash.zig test vectors
+    assert O.wyhash(0, b"") == 0x0409638EE2BDE459
+    assert O.wyhash(3, b"message digest") == 0x8619124089A3A16B
+
+
+@pytest.mark.parametrize("pair,h", [((0, 0), 0x14B83016DC460955), ((104, 101), 0xA96A3086990FD3BF),
+                                    ((101, 32), 0x544D3DA525A0DEDA), ((46, 10), 0xDA1944F769904CC9),
+                                    ((265, 101), 0x3A6CB6F333C4024E), ((256, 257), 0x61071EF1FA2190F0),
+                                    ((65535, 65535), 0x53AC8FA6824BCAD0)])
+def test_pair_hash(pair, h):
+    assert O.pair_hash(*pair) == h
+
+
+def test_c1_merges_txt_reproduced():
+    g = c1_golden()
+    text = c1_text()
+    assert sha256(text) == g["taylorswift_sha256"]
+    assert sha256(c1_merges_txt()) == g["merges_txt_sha256"] == \
+        "f1a9b78b2be24bf3c6813cb0efd4920f0e40347ac7da7a098df61bd215d5f8d0"
+    r = O.train(text, 300)
+    assert O.serialize(r.merges) == c1_merges_txt()
+    # merge 294 (line 39) is a real top-count tie decided by the Zig hash-map order
+    assert r.ties[38] == 2 and r.counts[38] == 685 and list(r.merges[38]) == [265, 101, 294]
+
+
+def test_hello_world_hello_map_order():
+    toks = list(b"hello world hello")
+    keys, slots, counts, cap = O.map_order(toks)
+    assert cap == 32  # D = 12 == max_load(16) and a getOrPut follows the 12th insertion
+    order = [bytes([k & 0xFF, k >> 16]) for k in keys]
+    assert order == [b"wo", b"d ", b" h", b"el", b"lo", b"ld", b"o ", b" w", b"ll", b"or", b"rl", b"he"]
+    r = O.train(b"hello world hello", 300)
+    assert r.merges.tolist() == [[101, 108, 256], [104, 256, 257], [257, 108, 258], [258, 111, 259], [119, 111, 260],
+                                 [32, 260, 261], [261, 114, 262], [100, 32, 263], [259, 262, 264], [264, 108, 265],
+                                 [265, 263, 266], [266, 259, 267]]
+
+
+# --- basic_tokenizer.zig:351-461 restated -------------------------------------------------------
+HW_MERGES = np.array([[ord("h"), ord("e"), 256], [256, ord("l"), 257], [ord("w"), ord("o"), 258]], dtype=np.uint16)
+
+
+def test_ref_generateInitialTokens():
+    r = O.train(b"hello world", 256)
+    assert r.tokens.tolist() == list(b"hello world")
+
+
+def test_ref_encode():
+    for literal in (True, False):
+        assert O.encode(HW_MERGES, b"hello world", literal).tolist() == [257, ord("l"), ord("o"), ord(" "), 258, ord("r"),
+                                                                         ord("l"), ord("d")]
+
+
+def test_ref_decode():
+    assert O.decode(HW_MERGES, [257, ord("l"), ord("o"), ord(" "), 258, ord("r"), ord("l"), ord("d")]) == b"hello world"
+
+
+def test_ref_train():
+    r = O.train(b"hello world hello", 300)
+    assert len(r.merges) > 0
+    enc = O.encode(r.merges, b"hello")
+    assert enc.tolist() == [259]
+    assert O.decode(r.merges, enc) == b"hello"
+
+
+def test_ref_serialize_roundtrip(tmp_path):
+    import zbpe
+
+    t = zbpe.BasicTokenizer()
+    for a, b, c in HW_MERGES:
+        t.merges.put(zbpe.CharPair(int(a), int(b)), int(c))
+    p = tmp_path / "test_merges.txt"
+    t.serializeMerges(str(p))
+    assert p.read_bytes() == O.serialize(HW_MERGES)
+    t2 = zbpe.BasicTokenizer()
+    t2.deserializeMerges(str(p))
+    assert t2.merges.merges == t.merges.merges
+
+
+def test_edge_cases():
+    with pytest.raises(ValueError):
+        O.train(b"abc", 255)
+    for text in (b"", b"a"):
+        assert len(O.train(text, 300).merges) == 0
+    r = O.train(b"ab", 300)
+    assert r.merges.tolist() == [[97, 98, 256]]
+    r = O.train(b"aaaa", 300)  # self pairs: overlapping count 3, left-greedy merge -> 256 256
+    assert r.counts[0] == 3 and r.merges[1].tolist() == [256, 256, 257]
+
+
+def test_encode_literal_equals_linear():
+    rng = np.random.default_rng(1)
+    text = bytes(rng.integers(97, 100, 3000, dtype=np.uint8))
+    r = O.train(text, 400)
+    assert np.array_equal(O.encode(r.merges, text, True), O.encode(r.merges, text, False))
+    assert np.array_equal(O.encode(r.merges, text), r.tokens)
+
+
+@pytest.mark.parametrize("g", synth_goldens(), ids=lambda g: g["name"])
+def test_synth_goldens(g):
+    text = synth_text(g)
+    r = O.train(text, g["vocab_size"])
+    assert r.merges.tolist() == g["merges"]
+    assert r.counts.tolist() == g["counts"]
+    assert sha256(r.tokens.tobytes()) == g["final_tokens_sha256"]
+
+
+def test_incremental_model_matches_oracle(tmp_path):
+    """The CPU design model of the engine's incremental algorithm (tests/model/inc_model.cpp)."""
+    src = os.path.join(os.path.dirname(__file__), "model", "inc_model.cpp")
+    exe = tmp_path / "inc_model"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src], check=True)
+    for g in synth_goldens():
+        if g["n"] > (1 << 18):
+            continue
+        p = tmp_path / "c.bin"
+        p.write_bytes(synth_text(g))
+        out = subprocess.run([str(exe), str(p), str(g["vocab_size"])], capture_output=True, check=True).stdout
+        assert out == O.serialize(np.array(g["merges"], dtype=np.uint16)), g["name"]

@@ -1,0 +1,106 @@
+// extern "C" entry points declared in include/zbpe.h.
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "engine.hpp"
+#include "zig_order.hpp"
+#include <vector>
+#include <string>
+
+struct zbpe_ctx {
+    zbpe::Engine eng;
+};
+
+static const char *env_or(const char *k) { const char *v = getenv(k); return v && *v ? v : nullptr; }
+
+extern "C" {
+
+const char *zbpe_version(void) { return "zbpe-mi355x 0.1 (gfx950)"; }
+
+zbpe_status zbpe_create(int device, zbpe_ctx **out) {
+    if (!out) return ZBPE_INVALID_ARGUMENT;
+    *out = nullptr;
+    zbpe_ctx *c = new (std::nothrow) zbpe_ctx();
+    if (!c) return ZBPE_OUT_OF_MEMORY;
+    zbpe_status s = c->eng.init(device);
+    if (s != ZBPE_OK) {
+        *out = c;  // keep it so zbpe_last_error() can report; caller destroys
+        return s;
+    }
+    if (env_or("ZBPE_DEBUG")) c->eng.debug_checks = true;
+    if (env_or("ZBPE_EXACT_TIES")) c->eng.force_exact_ties = true;
+    if (const char *v = env_or("ZBPE_COMPACT_DEN")) c->eng.compact_den = strtoull(v, nullptr, 10);
+    if (const char *v = env_or("ZBPE_SCAN_BLOCKS_PER_CU")) c->eng.scan_blocks_per_cu = atoi(v);
+    *out = c;
+    return ZBPE_OK;
+}
+
+zbpe_status zbpe_comm_unique_id(void *out128) {
+    (void)out128;
+    return ZBPE_COMM_ERROR;
+}
+zbpe_status zbpe_create_dist(int device, int rank, int world, const void *unique_id128, zbpe_ctx **out) {
+    (void)unique_id128;
+    if (world == 1 && rank == 0) return zbpe_create(device, out);
+    return ZBPE_COMM_ERROR;
+}
+
+void zbpe_destroy(zbpe_ctx *ctx) { delete ctx; }
+
+const char *zbpe_last_error(const zbpe_ctx *ctx) { return ctx ? ctx->eng.err.c_str() : "null context"; }
+
+zbpe_status zbpe_upload(zbpe_ctx *ctx, const uint8_t *text, size_t n) {
+    if (!ctx || (!text && n)) return ZBPE_INVALID_ARGUMENT;
+    return ctx->eng.upload(text, n);
+}
+
+zbpe_status zbpe_train_resident(zbpe_ctx *ctx, uint16_t vocab_size, int verbose, uint16_t *out_triples,
+                                uint64_t *out_counts, size_t *out_n_merges, zbpe_stats *stats) {
+    if (!ctx || !out_n_merges || (!out_triples && vocab_size > 256)) return ZBPE_INVALID_ARGUMENT;
+    return ctx->eng.train(vocab_size, verbose, out_triples, out_counts, out_n_merges, stats);
+}
+
+zbpe_status zbpe_train(zbpe_ctx *ctx, const uint8_t *text, size_t n, uint16_t vocab_size, int verbose,
+                       uint16_t *out_triples, uint64_t *out_counts, size_t *out_n_merges, zbpe_stats *stats) {
+    if (!ctx || !out_n_merges || (!text && n)) return ZBPE_INVALID_ARGUMENT;
+    *out_n_merges = 0;
+    if (vocab_size < 256) return ctx->eng.fail(ZBPE_INVALID_VOCAB_SIZE, "vocabSize %u < 256", vocab_size);
+    zbpe_status s = ctx->eng.upload(text, n);
+    if (s != ZBPE_OK) return s;
+    return zbpe_train_resident(ctx, vocab_size, verbose, out_triples, out_counts, out_n_merges, stats);
+}
+
+zbpe_status zbpe_encode(zbpe_ctx *ctx, const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n,
+                        uint16_t *out, size_t *out_len) {
+    if (!ctx || !out_len || (!text && n) || (!triples && n_merges) || (!out && n)) return ZBPE_INVALID_ARGUMENT;
+    return ctx->eng.encode(triples, n_merges, text, n, out, out_len);
+}
+
+zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches) {
+    if (!ctx || !mismatches) return ZBPE_INVALID_ARGUMENT;
+    return ctx->eng.verify_counts(mismatches);
+}
+
+zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
+    if (!ctx || !name) return ZBPE_INVALID_ARGUMENT;
+    std::string k(name);
+    zbpe::Engine &e = ctx->eng;
+    if (k == "debug_checks") e.debug_checks = value != 0;
+    else if (k == "exact_ties") e.force_exact_ties = value != 0;
+    else if (k == "compact_den" && value > 0) e.compact_den = (uint64_t)value;
+    else if (k == "scan_blocks_per_cu" && value > 0) e.scan_blocks_per_cu = (int)value;
+    else return e.fail(ZBPE_INVALID_ARGUMENT, "unknown option %s", name);
+    return ZBPE_OK;
+}
+
+zbpe_status zbpe_zig_order_winner(const uint32_t *first_pos, const uint32_t *keys, const uint32_t *counts, size_t n,
+                                  uint32_t top, int call_after_last_insert, uint32_t *winner) {
+    if ((!first_pos || !keys || !counts) && n) return ZBPE_INVALID_ARGUMENT;
+    if (!winner) return ZBPE_INVALID_ARGUMENT;
+    std::vector<zbpe::ZigOrderInput> in(n);
+    for (size_t i = 0; i < n; i++) in[i] = zbpe::ZigOrderInput{first_pos[i], keys[i], counts[i]};
+    return zbpe::zig_order_winner(std::move(in), top, call_after_last_insert != 0, winner) ? ZBPE_OK : ZBPE_INTERNAL;
+}
+
+}  // extern "C"

@@ -1,0 +1,510 @@
+// Host orchestration of the MI355X BPE trainer: device buffers, the per-merge launch sequence,
+// Zig-order tie resolution, compaction, encode. One Engine per process and GPU.
+//
+// Per merge (BasicTokenizer.expandVocabulary loop, basic_tokenizer.zig:183-204):
+//   [argmax of the previous update is already on the host]
+//   tie? -> zbpe_lastpair, zbpe_tie_occupy, zbpe_tie_resolve (+ exact emulation if undecided)
+//   zbpe_scan_pairs | (compact, zbpe_self_tiles, zbpe_self_carry, zbpe_scan_self) for (a, a)
+//   zbpe_apply, zbpe_update, zbpe_reset_merge, zbpe_argmax_partial/final -> one D2H + sync
+#include "engine.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "kernels.hpp"
+#include "zig_order.hpp"
+
+namespace zbpe {
+
+#define HIP_OK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) return fail(ZBPE_DEVICE_ERROR, "%s: %s (%s:%d)", #expr,     \
+                                          hipGetErrorString(e_), __FILE__, __LINE__);      \
+    } while (0)
+#define LAUNCH_OK() HIP_OK(hipGetLastError())
+#define CHECK(expr)                       \
+    do {                                  \
+        zbpe_status s_ = (expr);          \
+        if (s_ != ZBPE_OK) return s_;     \
+    } while (0)
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+
+zbpe_status Engine::fail(zbpe_status s, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    err = buf;
+    return s;
+}
+
+Engine::~Engine() { release(); }
+
+void Engine::release() {
+    auto f = [](void *p) { if (p) (void)hipFree(p); };
+    f(d_text); f(d_tok[0]); f(d_tok[1]);
+    f(T.ht_key); f(T.ht_id); f(T.id_key); f(T.id_cnt);
+    f(d_left); f(d_right); f(d_st); f(d_rec); f(d_partial); f(d_hist);
+    f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
+    f(d_first); f(d_gather); f(d_recount);
+    if (h_st) (void)hipHostFree(h_st);
+    for (auto &e : ev) if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+    d_text = nullptr; d_tok[0] = d_tok[1] = nullptr; T = Tables{};
+    d_left = d_right = nullptr; d_st = nullptr; d_rec = nullptr; d_partial = nullptr; d_hist = nullptr;
+    d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr;
+    d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
+    for (auto &e : ev) e = nullptr;
+}
+
+zbpe_status Engine::init(int dev) {
+    device = dev;
+    int ndev = 0;
+    HIP_OK(hipGetDeviceCount(&ndev));
+    if (dev < 0 || dev >= ndev) return fail(ZBPE_INVALID_ARGUMENT, "device %d out of range (%d devices)", dev, ndev);
+    HIP_OK(hipSetDevice(dev));
+    HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HIP_OK(hipHostMalloc((void **)&h_st, sizeof(DevState), hipHostMallocDefault));
+    HIP_OK(hipMalloc(&d_st, sizeof(DevState)));
+    HIP_OK(hipMalloc(&d_left, 65536 * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_right, 65536 * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
+    for (auto &e : ev) HIP_OK(hipEventCreate(&e));
+    // the initial byte-pair histogram keeps 128 KiB of bins in LDS
+    HIP_OK(hipFuncSetAttribute((const void *)zbpe_count_byte_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4));
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, dev));
+    num_cus = prop.multiProcessorCount;
+    return ZBPE_OK;
+}
+
+template <typename T_>
+zbpe_status Engine::ensure(T_ **p, size_t &cap, size_t need, const char *what) {
+    if (*p && cap >= need) return ZBPE_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    size_t c = std::max(need, cap * 2);
+    if (hipMalloc((void **)p, c * sizeof(T_)) != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        cap = 0;
+        return fail(ZBPE_OUT_OF_MEMORY, "device allocation of %zu x %zu B for %s failed", c, sizeof(T_), what);
+    }
+    cap = c;
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::upload(const uint8_t *text, size_t n) {
+    if (n > (size_t)0xFFFFFFF0u) return fail(ZBPE_INVALID_ARGUMENT, "shard of %zu bytes exceeds 2^32 tokens", n);
+    HIP_OK(hipSetDevice(device));
+    CHECK(ensure(&d_text, text_cap, round_up(n + 64, 64), "corpus"));
+    if (n) HIP_OK(hipMemcpyAsync(d_text, text, n, hipMemcpyHostToDevice, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    n_text = n;
+    uploaded = true;
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::sync_state() {
+    HIP_OK(hipMemcpyAsync(h_st, d_st, sizeof(DevState), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    if (h_st->error)
+        return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow)",
+                    h_st->error);
+    return ZBPE_OK;
+}
+
+// tables sized for `need_ids`; rebuild keeps live ids only
+zbpe_status Engine::alloc_tables(size_t id_cap_new) {
+    size_t ht_cap_new = 1;
+    while (ht_cap_new < 2 * id_cap_new) ht_cap_new <<= 1;
+    Tables N{};
+    N.id_cap = (uint32_t)id_cap_new;
+    N.ht_mask = (uint32_t)(ht_cap_new - 1);
+    if (hipMalloc(&N.ht_key, ht_cap_new * 4) != hipSuccess || hipMalloc(&N.ht_id, ht_cap_new * 4) != hipSuccess ||
+        hipMalloc(&N.id_key, id_cap_new * 4) != hipSuccess || hipMalloc(&N.id_cnt, id_cap_new * 4) != hipSuccess) {
+        (void)hipGetLastError();
+        for (void *p : {(void *)N.ht_key, (void *)N.ht_id, (void *)N.id_key, (void *)N.id_cnt}) if (p) (void)hipFree(p);
+        return fail(ZBPE_OUT_OF_MEMORY, "pair table allocation (%zu ids) failed", id_cap_new);
+    }
+    HIP_OK(hipMemsetAsync(N.ht_key, 0xFF, ht_cap_new * 4, stream));
+    if (T.id_key) {  // rebuild from the old tables
+        uint32_t old_n = h_st->num_ids;
+        HIP_OK(hipMemsetAsync(&d_st->num_ids, 0, 4, stream));
+        zbpe_rebuild<<<std::min<uint32_t>(2048, (old_n + 255) / 256 + 1), 256, 0, stream>>>(T.id_key, T.id_cnt, old_n, N, d_st);
+        LAUNCH_OK();
+        HIP_OK(hipStreamSynchronize(stream));
+        (void)hipFree(T.ht_key); (void)hipFree(T.ht_id); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt);
+        stats_rebuilds++;
+    }
+    T = N;
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::maybe_grow_tables(uint32_t X) {
+    const uint64_t need = (uint64_t)h_st->num_ids + 2ull * X + 8;
+    const uint64_t live = (uint64_t)std::max(h_st->live, 0);
+    const uint64_t dead = h_st->num_ids - live;
+    if (need <= T.id_cap && !(dead > std::max<uint64_t>(live, 1u << 20))) return ZBPE_OK;
+    uint64_t cap = T.id_cap;
+    while (live + 2ull * X + 8 > cap / 2) cap *= 2;
+    CHECK(alloc_tables(cap));
+    return sync_state();
+}
+
+zbpe_status Engine::compact() {
+    const int64_t ntiles = (n_slots + COMPACT_TILE - 1) / COMPACT_TILE;
+    if (ntiles == 0) return ZBPE_OK;
+    CHECK(ensure(&d_tile_cnt, tile_cnt_cap, ntiles, "compaction tiles"));
+    CHECK(ensure(&d_tile_off, tile_off_cap, ntiles + 1, "compaction offsets"));
+    uint16_t *src = d_tok[cur], *dst = d_tok[cur ^ 1];
+    zbpe_compact_count<<<ntiles, 256, 0, stream>>>(src, n_slots, d_tile_cnt);
+    LAUNCH_OK();
+    zbpe_scan_u32<<<1, 1024, 0, stream>>>(d_tile_cnt, ntiles, d_tile_off, d_tile_off + ntiles);
+    LAUNCH_OK();
+    zbpe_compact_scatter<<<ntiles, 256, 0, stream>>>(src, n_slots, d_tile_off, dst);
+    LAUNCH_OK();
+    const int64_t pad_end = (int64_t)round_up(n_live + 1, 64) + 64;
+    zbpe_fill_u16<<<64, 256, 0, stream>>>(dst, n_live, pad_end, HOLE);
+    LAUNCH_OK();
+    cur ^= 1;
+    n_slots = n_live;
+    stats.compactions++;
+    if (debug_checks) {
+        uint64_t total = 0;
+        HIP_OK(hipMemcpyAsync(&total, d_tile_off + ntiles, 8, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        if ((int64_t)total != n_live) return fail(ZBPE_INTERNAL, "compaction kept %llu tokens, expected %lld",
+                                                  (unsigned long long)total, (long long)n_live);
+    }
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::launch_argmax() {
+    const uint32_t nid = std::max<uint32_t>(h_st->num_ids + 2 * 65536u, 1);  // upper bound after this merge
+    int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, (nid / 4 + ARGMAX_THREADS - 1) / ARGMAX_THREADS + 1);
+    zbpe_argmax_partial<<<blocks, ARGMAX_THREADS, 0, stream>>>(T.id_cnt, T.id_cap, d_st, d_partial);
+    LAUNCH_OK();
+    zbpe_argmax_final<<<1, 256, 0, stream>>>(d_partial, blocks, T.id_key, d_st);
+    LAUNCH_OK();
+    return ZBPE_OK;
+}
+
+// Zig-order winner among the pairs sharing the top count
+zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
+    stats.tie_iterations++;
+    zbpe_lastpair<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, T, d_st);
+    LAUNCH_OK();
+    CHECK(sync_state());
+    const uint64_t D = (uint64_t)h_st->live;
+    const bool call_after = h_st->lastpair_count >= 2;
+    const uint64_t cap = zig_final_capacity(D, call_after);
+    if (cap > (1ull << 31)) return fail(ZBPE_INTERNAL, "Zig map capacity %llu out of range", (unsigned long long)cap);
+    CHECK(ensure(&d_bitmap, bitmap_cap, cap / 32 + 1, "tie bitmap"));
+    CHECK(ensure(&d_tie_list, tie_list_cap, ties, "tie list"));
+    HIP_OK(hipMemsetAsync(d_bitmap, 0, (cap / 32 + 1) * 4, stream));
+    HIP_OK(hipMemsetAsync(&d_st->tie_len, 0, 4, stream));
+    const uint32_t nid = h_st->num_ids;
+    zbpe_tie_occupy<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_st, (uint32_t)(cap - 1), top, d_bitmap,
+                                                                                 d_tie_list, (uint32_t)tie_list_cap);
+    LAUNCH_OK();
+    zbpe_tie_resolve<<<1, 256, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, d_bitmap, (uint32_t)(cap - 1));
+    LAUNCH_OK();
+    CHECK(sync_state());
+    if (h_st->tie_len != ties)
+        return fail(ZBPE_INTERNAL, "tie collection found %u pairs at count %u, argmax said %u", h_st->tie_len, top, ties);
+    if (h_st->tie_verdict == 0 && !force_exact_ties) {
+        *winner = h_st->tie_winner;
+        return ZBPE_OK;
+    }
+    // exact emulation from first-occurrence order
+    stats.tie_fallbacks++;
+    CHECK(ensure(&d_first, first_cap, nid, "first occurrences"));
+    CHECK(ensure(&d_gather, gather_cap, (size_t)D, "live pairs"));
+    HIP_OK(hipMemsetAsync(d_first, 0xFF, (size_t)nid * 4, stream));
+    HIP_OK(hipMemsetAsync(&d_st->gather_len, 0, 4, stream));
+    zbpe_first_occ<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, T, d_first, d_st);
+    LAUNCH_OK();
+    zbpe_gather_live<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_first, d_st, d_gather, (uint32_t)gather_cap);
+    LAUNCH_OK();
+    CHECK(sync_state());
+    const uint32_t g = h_st->gather_len;
+    if (g != D || g > gather_cap) return fail(ZBPE_INTERNAL, "gathered %u live pairs, expected %llu", g, (unsigned long long)D);
+    std::vector<LiveRec> recs(g);
+    HIP_OK(hipMemcpy(recs.data(), d_gather, (size_t)g * sizeof(LiveRec), hipMemcpyDeviceToHost));
+    std::vector<ZigOrderInput> in(g);
+    for (uint32_t i = 0; i < g; i++) in[i] = ZigOrderInput{recs[i].first_pos, recs[i].key, recs[i].count};
+    if (!zig_order_winner(std::move(in), top, call_after, winner))
+        return fail(ZBPE_INTERNAL, "exact tie emulation found no pair with count %u", top);
+    if (h_st->tie_verdict == 0 && *winner != h_st->tie_winner)
+        return fail(ZBPE_INTERNAL, "tie fast path chose 0x%08x, exact emulation 0x%08x", h_st->tie_winner, *winner);
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::alloc_stream(size_t n) {
+    const size_t need = round_up(n + 1, 64) + 64;
+    CHECK(ensure(&d_tok[0], tok_cap0, need, "token stream"));
+    CHECK(ensure(&d_tok[1], tok_cap1, need, "token stream (compaction buffer)"));
+    cur = 0;
+    zbpe_fill_u16<<<256, 256, 0, stream>>>(d_tok[0], 0, (int64_t)need, HOLE);
+    LAUNCH_OK();
+    const uint64_t n_pad16 = round_up(n, 16);
+    if (n) {
+        zbpe_widen<<<(int)std::min<uint64_t>(4096, n_pad16 / 16 / 256 + 1), 256, 0, stream>>>(d_text, d_tok[0], n, n_pad16);
+        LAUNCH_OK();
+    }
+    n_slots = (int64_t)n;
+    n_live = (int64_t)n;
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triples, uint64_t *out_counts,
+                          size_t *out_n_merges, zbpe_stats *out_stats) {
+    const double t_start = now_s();
+    stats = zbpe_stats{};
+    *out_n_merges = 0;
+    if (vocab_size < 256) return fail(ZBPE_INVALID_VOCAB_SIZE, "vocabSize %u < 256", vocab_size);
+    if (!uploaded) return fail(ZBPE_INVALID_ARGUMENT, "no corpus uploaded");
+    HIP_OK(hipSetDevice(device));
+    const size_t n = n_text;
+    double ev_count = 0, ev_select = 0, ev_replace = 0;
+
+    // ---- generateInitialTokens + initial histogram ------------------------------------------------
+    CHECK(alloc_stream(n));
+    if (!T.id_key || T.id_cap < (1u << 20)) {
+        if (T.id_key) { (void)hipFree(T.ht_key); (void)hipFree(T.ht_id); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt); T = Tables{}; }
+        CHECK(alloc_tables(1u << 20));
+    } else {
+        HIP_OK(hipMemsetAsync(T.ht_key, 0xFF, ((size_t)T.ht_mask + 1) * 4, stream));
+    }
+    HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
+    HIP_OK(hipMemsetAsync(d_left, 0, 65536 * 4, stream));
+    HIP_OK(hipMemsetAsync(d_right, 0, 65536 * 4, stream));
+    HIP_OK(hipMemsetAsync(d_hist, 0, 65536 * 4, stream));
+    HIP_OK(hipEventRecord(ev[0], stream));
+    if (n >= 2) {
+        const int hb = std::max(1, num_cus);
+        for (uint32_t lo : {0u, 128u}) {
+            zbpe_count_byte_pairs<<<hb, HIST_THREADS, 32768 * 4, stream>>>(d_text, n, -1, lo, d_hist);
+            LAUNCH_OK();
+        }
+        zbpe_hist_to_table<<<256, 256, 0, stream>>>(d_hist, T, d_st);
+        LAUNCH_OK();
+    }
+    HIP_OK(hipEventRecord(ev[1], stream));
+    h_st->num_ids = 0;
+    CHECK(launch_argmax());
+    HIP_OK(hipEventRecord(ev[2], stream));
+    CHECK(sync_state());
+    {
+        float ms;
+        HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1])); ev_count += ms * 1e-3;
+        HIP_OK(hipEventElapsedTime(&ms, ev[1], ev[2])); ev_select += ms * 1e-3;
+        stats.count_pairs_calls++;
+    }
+    uint64_t holes = 0;
+    size_t merges = 0;
+    for (uint32_t X = 256; X < vocab_size; X++) {
+        if (h_st->live <= 0) {  // sortedCodePointPairs.len == 0 (basic_tokenizer.zig:188-191)
+            fprintf(stderr, "No more pairs to merge. Stopping early.\n");
+            break;
+        }
+        const uint32_t top = h_st->top_count, ties = h_st->tie_count;
+        uint32_t key = h_st->top_key;
+        const double t_sel = now_s();
+        if (ties > 1) CHECK(resolve_tie(top, ties, &key));
+        stats.sort_pairs_calls++;
+        if (ties > 1) ev_select += now_s() - t_sel;
+        const uint32_t a = key & 0xFFFF, b = key >> 16;
+        if (verbose)
+            fprintf(stderr, "merge %u/%u: (%u,%u) -> %u had %u occurrences\n", X - 256 + 1, vocab_size - 256u, a, b, X, top);
+        out_triples[3 * merges + 0] = (uint16_t)a;
+        out_triples[3 * merges + 1] = (uint16_t)b;
+        out_triples[3 * merges + 2] = (uint16_t)X;
+        if (out_counts) out_counts[merges] = top;
+        merges++;
+        stats.sum_tokens += (uint64_t)n_live;
+
+        CHECK(maybe_grow_tables(X));
+        CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(top, 1), "occurrence records"));
+        const bool self = a == b;
+        if (self && holes) {
+            HIP_OK(hipEventRecord(ev[3], stream));
+            CHECK(compact());
+            holes = 0;
+            HIP_OK(hipEventRecord(ev[4], stream));
+            HIP_OK(hipEventSynchronize(ev[4]));
+            float ms;
+            HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
+            ev_replace += ms * 1e-3;
+        }
+        // ---- count: scan the stream for (a, b) -----------------------------------------------------
+        ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 1};
+        HIP_OK(hipEventRecord(ev[0], stream));
+        if (!self) {
+            const int64_t ntiles = (n_slots + SCAN_TILE - 1) / SCAN_TILE;
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)num_cus * scan_blocks_per_cu));
+            zbpe_scan_pairs<<<grid, SCAN_THREADS, 0, stream>>>(A);
+            LAUNCH_OK();
+            stats.scan_launches++;
+        } else {
+            stats.self_pair_merges++;
+            const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);
+            CHECK(ensure(&d_tile_fn, tile_fn_cap, ntiles, "self tiles"));
+            CHECK(ensure(&d_carry, carry_cap, ntiles, "self carry"));
+            zbpe_self_tiles<<<ntiles, SELF_THREADS, 0, stream>>>(d_tok[cur], n_slots, a, d_tile_fn);
+            LAUNCH_OK();
+            zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry);
+            LAUNCH_OK();
+            zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
+            LAUNCH_OK();
+        }
+        HIP_OK(hipEventRecord(ev[1], stream));
+        // ---- replace: apply + count update ---------------------------------------------------------
+        zbpe_apply<<<(int)std::min<uint64_t>(2048, top / 256 + 1), 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, d_st, X);
+        LAUNCH_OK();
+        zbpe_update<<<(X + 255) / 256, 256, 0, stream>>>(T, d_st, d_left, d_right, a, b, X, key);
+        LAUNCH_OK();
+        zbpe_reset_merge<<<1, 1, 0, stream>>>(d_st);
+        LAUNCH_OK();
+        HIP_OK(hipEventRecord(ev[2], stream));
+        // ---- select for the next merge -------------------------------------------------------------
+        CHECK(launch_argmax());
+        HIP_OK(hipEventRecord(ev[3], stream));
+        CHECK(sync_state());
+        {
+            float ms;
+            HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1])); ev_count += ms * 1e-3;
+            if (!self) {
+                stats.scan_kernel_s += ms * 1e-3;
+                stats.scan_alg_bytes += 2ull * (uint64_t)n_live;
+                stats.scan_read_bytes += 2ull * (uint64_t)n_slots;
+            }
+            HIP_OK(hipEventElapsedTime(&ms, ev[1], ev[2])); ev_replace += ms * 1e-3;
+            HIP_OK(hipEventElapsedTime(&ms, ev[2], ev[3])); ev_select += ms * 1e-3;
+            stats.count_pairs_calls++;
+            stats.replace_pair_calls++;
+        }
+        const uint32_t occ = h_st->last_occ;
+        if (!self && occ != top)
+            return fail(ZBPE_INTERNAL, "merge %u: scan found %u occurrences of (%u,%u), count was %u", X, occ, a, b, top);
+        n_live -= occ;
+        holes += occ;
+        if (holes * compact_den > (uint64_t)n_slots) {
+            HIP_OK(hipEventRecord(ev[0], stream));
+            CHECK(compact());
+            holes = 0;
+            HIP_OK(hipEventRecord(ev[1], stream));
+            HIP_OK(hipEventSynchronize(ev[1]));
+            float ms;
+            HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+            ev_replace += ms * 1e-3;
+        }
+    }
+    HIP_OK(hipStreamSynchronize(stream));
+    *out_n_merges = merges;
+    stats.count_pairs_s = ev_count;
+    stats.sort_pairs_s = ev_select;
+    stats.replace_pair_s = ev_replace;
+    stats.total_s = now_s() - t_start;
+    stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
+    stats.final_tokens = (uint64_t)n_live;
+    stats.distinct_pairs = (uint64_t)std::max(h_st->live, 0);
+    stats.pair_ids = h_st->num_ids;
+    trained = true;
+    if (out_stats) *out_stats = stats;
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::verify_counts(uint64_t *mismatches) {
+    if (!trained) return fail(ZBPE_INVALID_ARGUMENT, "verify_counts needs a trained context");
+    HIP_OK(hipSetDevice(device));
+    CHECK(sync_state());
+    const uint32_t nid = h_st->num_ids;
+    CHECK(ensure(&d_recount, recount_cap, std::max<uint32_t>(nid, 1), "recount"));
+    HIP_OK(hipMemsetAsync(d_recount, 0, (size_t)std::max<uint32_t>(nid, 1) * 4, stream));
+    HIP_OK(hipMemsetAsync(&d_st->mismatches, 0, 4, stream));
+    zbpe_recount<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, T, d_recount, d_st);
+    LAUNCH_OK();
+    zbpe_recount_compare<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_recount, d_st);
+    LAUNCH_OK();
+    CHECK(sync_state());
+    *mismatches = h_st->mismatches;
+    return ZBPE_OK;
+}
+
+// encode (basic_tokenizer.zig:71-88): replay merges in rank order on the device
+zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n, uint16_t *out,
+                           size_t *out_len) {
+    for (size_t k = 0; k < n_merges; k++) {
+        if (triples[3 * k + 2] == triples[3 * k])
+            return fail(ZBPE_INVALID_ARGUMENT, "merge %zu: new_token == first (%u) is not supported by the device encoder", k,
+                        triples[3 * k]);
+        if (triples[3 * k + 2] == HOLE || triples[3 * k] == HOLE || triples[3 * k + 1] == HOLE)
+            return fail(ZBPE_INVALID_ARGUMENT, "merge %zu uses token 65535", k);
+    }
+    CHECK(upload(text, n));
+    trained = false;
+    CHECK(alloc_stream(n));
+    HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
+    CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(n / 2 + 1, 1), "occurrence records"));
+    uint64_t holes = 0;
+    for (size_t k = 0; k < n_merges; k++) {
+        const uint32_t a = triples[3 * k], b = triples[3 * k + 1], X = triples[3 * k + 2];
+        if (a == b) {
+            CHECK(sync_state());
+            holes += h_st->total_occ;
+            HIP_OK(hipMemsetAsync(&d_st->total_occ, 0, 4, stream));
+            n_live -= h_st->total_occ;
+            if (holes) { CHECK(compact()); holes = 0; }
+        }
+        ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 0};
+        if (a != b) {
+            const int64_t ntiles = (n_slots + SCAN_TILE - 1) / SCAN_TILE;
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)num_cus * scan_blocks_per_cu));
+            zbpe_scan_pairs<<<grid, SCAN_THREADS, 0, stream>>>(A);
+            LAUNCH_OK();
+        } else {
+            const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);
+            CHECK(ensure(&d_tile_fn, tile_fn_cap, ntiles, "self tiles"));
+            CHECK(ensure(&d_carry, carry_cap, ntiles, "self carry"));
+            zbpe_self_tiles<<<ntiles, SELF_THREADS, 0, stream>>>(d_tok[cur], n_slots, a, d_tile_fn);
+            LAUNCH_OK();
+            zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry);
+            LAUNCH_OK();
+            zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
+            LAUNCH_OK();
+        }
+        zbpe_apply<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, d_st, X);
+        LAUNCH_OK();
+        zbpe_reset_merge<<<1, 1, 0, stream>>>(d_st);
+        LAUNCH_OK();
+        if ((k & 63) == 63) {
+            CHECK(sync_state());
+            holes += h_st->total_occ;
+            n_live -= h_st->total_occ;
+            HIP_OK(hipMemsetAsync(&d_st->total_occ, 0, 4, stream));
+            if (holes * compact_den > (uint64_t)n_slots) { CHECK(compact()); holes = 0; }
+        }
+    }
+    CHECK(sync_state());
+    n_live -= h_st->total_occ;
+    HIP_OK(hipMemsetAsync(&d_st->total_occ, 0, 4, stream));
+    CHECK(compact());
+    if (n_live) HIP_OK(hipMemcpy(out, d_tok[cur], (size_t)n_live * 2, hipMemcpyDeviceToHost));
+    *out_len = (size_t)n_live;
+    return ZBPE_OK;
+}
+
+}  // namespace zbpe

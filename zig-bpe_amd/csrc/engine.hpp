@@ -1,0 +1,88 @@
+// Engine: one MI355X, one process. See engine.hip for the per-merge launch sequence.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/zbpe.h"
+#include "types.hpp"
+
+namespace zbpe {
+
+constexpr int ARGMAX_MAX_BLOCKS = 1024;
+
+struct Engine {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // corpus (this rank's shard) and token stream
+    uint8_t *d_text = nullptr;
+    size_t text_cap = 0, n_text = 0;
+    bool uploaded = false, trained = false;
+    uint16_t *d_tok[2] = {nullptr, nullptr};
+    size_t tok_cap0 = 0, tok_cap1 = 0;
+    int cur = 0;
+    int64_t n_slots = 0;  // live tokens + holes
+    int64_t n_live = 0;
+
+    // pair table and per-merge scratch
+    Tables T{};
+    uint32_t *d_left = nullptr, *d_right = nullptr, *d_hist = nullptr;
+    DevState *d_st = nullptr, *h_st = nullptr;
+    uint32_t *d_rec = nullptr;
+    size_t rec_cap = 0;
+    MaxRec *d_partial = nullptr;
+    uint32_t *d_tile_cnt = nullptr;
+    size_t tile_cnt_cap = 0;
+    uint64_t *d_tile_off = nullptr;
+    size_t tile_off_cap = 0;
+    uint8_t *d_tile_fn = nullptr, *d_carry = nullptr;
+    size_t tile_fn_cap = 0, carry_cap = 0;
+    uint32_t *d_bitmap = nullptr;
+    size_t bitmap_cap = 0;
+    uint64_t *d_tie_list = nullptr;
+    size_t tie_list_cap = 0;
+    uint32_t *d_first = nullptr;
+    size_t first_cap = 0;
+    LiveRec *d_gather = nullptr;
+    size_t gather_cap = 0;
+    uint32_t *d_recount = nullptr;
+    size_t recount_cap = 0;
+    hipEvent_t ev[6] = {};
+
+    // policy knobs
+    uint64_t compact_den = 8;     // compact when holes > slots / compact_den
+    int scan_blocks_per_cu = 8;
+    bool debug_checks = false;    // extra syncs + consistency checks
+    bool force_exact_ties = false;  // resolve every tie by the exact emulation and cross-check the fast path
+
+    zbpe_stats stats{};
+    uint64_t stats_rebuilds = 0;
+
+    ~Engine();
+    zbpe_status init(int device);
+    void release();
+    zbpe_status fail(zbpe_status s, const char *fmt, ...);
+    template <typename T_>
+    zbpe_status ensure(T_ **p, size_t &cap, size_t need, const char *what);
+    zbpe_status upload(const uint8_t *text, size_t n);
+    zbpe_status train(uint16_t vocab_size, int verbose, uint16_t *out_triples, uint64_t *out_counts,
+                      size_t *out_n_merges, zbpe_stats *out_stats);
+    zbpe_status encode(const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n, uint16_t *out,
+                       size_t *out_len);
+    zbpe_status verify_counts(uint64_t *mismatches);
+
+   private:
+    zbpe_status sync_state();
+    zbpe_status alloc_tables(size_t id_cap);
+    zbpe_status maybe_grow_tables(uint32_t X);
+    zbpe_status alloc_stream(size_t n);
+    zbpe_status compact();
+    zbpe_status launch_argmax();
+    zbpe_status resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner);
+};
+
+}  // namespace zbpe

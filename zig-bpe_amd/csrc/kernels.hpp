@@ -1,0 +1,833 @@
+// Device code of the MI355X (gfx950) BPE trainer. Included by engine.hip only.
+//
+// Token stream: u16 per token in HBM, HOLE (0xFFFF) marks a slot freed by a merge; holes are
+// squeezed out by zbpe_compact_* when they exceed a fraction of the stream. Real tokens are
+// < 0xFFFF because vocabSize is a u16 (basic_tokenizer.zig:140) so new tokens stop at 0xFFFE.
+//
+// Pair table: open addressing on u32 key = first | second << 16 -> dense id; per id a count
+// (u32) and its key. Once a pair's count reaches 0 it never returns: a merge only creates pairs
+// that contain the brand-new token, so table entries are never revived.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "types.hpp"
+
+namespace zbpe {
+// ------------------------------------------------------------------------------------------
+// Zig 0.13 std.hash.Wyhash(seed 0) of the 4-byte key
+// ------------------------------------------------------------------------------------------
+constexpr uint64_t WY_S0 = 0xa0761d6478bd642fULL, WY_S1 = 0xe7037ed1a0b428dbULL;
+__host__ __device__ constexpr inline uint64_t mulhi64(uint64_t a, uint64_t b) {
+    uint64_t al = a & 0xffffffffu, ah = a >> 32, bl = b & 0xffffffffu, bh = b >> 32;
+    uint64_t ll = al * bl, lh = al * bh, hl = ah * bl, hh = ah * bh;
+    uint64_t mid = (ll >> 32) + (lh & 0xffffffffu) + (hl & 0xffffffffu);
+    return hh + (lh >> 32) + (hl >> 32) + (mid >> 32);
+}
+__host__ __device__ constexpr inline uint64_t wy_mix(uint64_t a, uint64_t b) { return (a * b) ^ mulhi64(a, b); }
+constexpr uint64_t WY_SEED0 = 0 ^ wy_mix(0 ^ WY_S0, WY_S1);  // Wyhash.init(0).state[0]
+
+__device__ inline uint64_t zig_pair_hash(uint32_t w) {
+    uint64_t a = ((uint64_t)w << 32) | w;
+    uint64_t b = a;
+    a ^= WY_S1;
+    b ^= WY_SEED0;
+    uint64_t lo = a * b, hi = __umul64hi(a, b);
+    return wy_mix(lo ^ WY_S0 ^ 4ull, hi ^ WY_S1);
+}
+
+// ------------------------------------------------------------------------------------------
+// pair table
+// ------------------------------------------------------------------------------------------
+
+__device__ inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+__device__ inline uint32_t ht_find(const Tables &T, uint32_t key) {
+    uint32_t s = fmix32(key) & T.ht_mask;
+    for (uint32_t probes = 0; probes <= T.ht_mask; ++probes) {
+        uint32_t k = T.ht_key[s];
+        if (k == key) return T.ht_id[s];
+        if (k == EMPTY_KEY) return NO_ID;
+        s = (s + 1) & T.ht_mask;
+    }
+    return NO_ID;
+}
+// Insert a key known to be absent (callers guarantee uniqueness within a launch).
+__device__ inline void ht_insert_new(const Tables &T, uint32_t key, uint32_t id) {
+    uint32_t s = fmix32(key) & T.ht_mask;
+    for (;;) {
+        uint32_t prev = atomicCAS(&T.ht_key[s], EMPTY_KEY, key);
+        if (prev == EMPTY_KEY) { T.ht_id[s] = id; return; }
+        s = (s + 1) & T.ht_mask;
+    }
+}
+__device__ inline void pair_new(const Tables &T, DevState *st, uint32_t key, uint32_t count) {
+    uint32_t id = atomicAdd(&st->num_ids, 1u);
+    if (id >= T.id_cap) { atomicOr(&st->error, 1u); return; }
+    T.id_key[id] = key;
+    T.id_cnt[id] = count;
+    ht_insert_new(T, key, id);
+    atomicAdd(&st->live, 1);
+}
+__device__ inline void pair_dec(const Tables &T, DevState *st, uint32_t key, uint32_t d) {
+    uint32_t id = ht_find(T, key);
+    if (id == NO_ID) { atomicOr(&st->error, 4u); return; }
+    uint32_t old = atomicSub(&T.id_cnt[id], d);
+    if (old < d) atomicOr(&st->error, 2u);
+    if (old == d) atomicSub(&st->live, 1);
+}
+
+// ------------------------------------------------------------------------------------------
+// generateInitialTokens (basic_tokenizer.zig:155-170): u8 -> u16, 16 bytes per thread
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) zbpe_widen(const uint8_t *__restrict__ text, uint16_t *__restrict__ tok,
+                                                  uint64_t n, uint64_t n_pad) {
+    uint64_t nv = n_pad / 16;
+    for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t base = v * 16;
+        uint32_t w[8];
+        if (base + 16 <= n) {
+            uint4 x = *reinterpret_cast<const uint4 *>(text + base);
+            uint32_t in[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                w[2 * i] = (in[i] & 0xffu) | ((in[i] & 0xff00u) << 8);
+                w[2 * i + 1] = ((in[i] >> 16) & 0xffu) | ((in[i] >> 8) & 0xff0000u);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                uint32_t lo = base + 2 * i < n ? text[base + 2 * i] : HOLE;
+                uint32_t hi = base + 2 * i + 1 < n ? text[base + 2 * i + 1] : HOLE;
+                w[i] = lo | (hi << 16);
+            }
+        }
+        uint4 *o = reinterpret_cast<uint4 *>(tok + base);
+        o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Initial pair histogram over the byte stream (countCodePointPairs at t = 0): 65,536 possible
+// byte pairs; one launch per half of the first byte so the 32,768 u32 bins fit in LDS (128 KiB).
+// Pair i = (text[i], text[i+1]); pairs with i >= n-1 are absent. `next_byte` extends the shard by
+// one byte (the first byte of the next shard) or is < 0 when there is none.
+// ------------------------------------------------------------------------------------------
+constexpr int HIST_THREADS = 1024;
+__global__ void __launch_bounds__(HIST_THREADS) zbpe_count_byte_pairs(const uint8_t *__restrict__ text, uint64_t n,
+                                                                      int next_byte, uint32_t lo,
+                                                                      uint32_t *__restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // 32768
+    for (int i = threadIdx.x; i < 32768; i += HIST_THREADS) h[i] = 0;
+    __syncthreads();
+    const uint64_t npairs = next_byte >= 0 ? n : (n ? n - 1 : 0);  // pair starts [0, npairs)
+    const uint64_t per_block = ((npairs + gridDim.x - 1) / gridDim.x + 15) & ~15ull;
+    const uint64_t beg = blockIdx.x * per_block;
+    const uint64_t end = min(npairs, beg + per_block);
+    for (uint64_t base = beg + 16ull * threadIdx.x; base < end; base += 16ull * HIST_THREADS) {
+        uint8_t b[17];
+        if (base + 17 <= n) {
+            uint4 x = *reinterpret_cast<const uint4 *>(text + base);
+            uint32_t in[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int i = 0; i < 16; i++) b[i] = (uint8_t)(in[i >> 2] >> (8 * (i & 3)));
+            b[16] = text[base + 16];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 17; i++) {
+                uint64_t p = base + i;
+                b[i] = p < n ? text[p] : (uint8_t)(next_byte >= 0 ? next_byte : 0);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            if (base + i < end) {
+                uint32_t f = (uint32_t)b[i] - lo;
+                if (f < 128) atomicAdd(&h[(f << 8) | b[i + 1]], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 32768; i += HIST_THREADS) {
+        uint32_t c = h[i];
+        if (c) atomicAdd(&hist[(lo << 8) + i], c);
+    }
+}
+
+// hist[first*256+second] -> pair table entries
+__global__ void zbpe_hist_to_table(const uint32_t *__restrict__ hist, Tables T, DevState *st) {
+    uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= 65536) return;
+    uint32_t c = hist[k];
+    if (c) pair_new(T, st, pair_key(k >> 8, k & 0xff), c);
+}
+
+// ------------------------------------------------------------------------------------------
+// argmax over pair counts (sortCodePointPairs + sorted[0], basic_tokenizer.zig:280-306,:193):
+// the max count, how many pairs share it, and the smallest id holding it.
+// ------------------------------------------------------------------------------------------
+__device__ inline MaxRec max_combine(MaxRec x, MaxRec y) {
+    if (x.cnt > y.cnt) return x;
+    if (y.cnt > x.cnt) return y;
+    return MaxRec{x.cnt, x.ties + y.ties, min(x.id, y.id)};
+}
+__device__ inline MaxRec wave_max(MaxRec r) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        MaxRec o{(uint32_t)__shfl_xor((int)r.cnt, off), (uint32_t)__shfl_xor((int)r.ties, off),
+                 (uint32_t)__shfl_xor((int)r.id, off)};
+        r = max_combine(r, o);
+    }
+    return r;
+}
+constexpr int ARGMAX_THREADS = 256;
+__global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_argmax_partial(const uint32_t *__restrict__ cnt, uint32_t id_cap,
+                                                                      const DevState *st, MaxRec *__restrict__ partial) {
+    const uint32_t n = min(st->num_ids, id_cap);
+    MaxRec r{0, 0, NO_ID};
+    const uint32_t nv = n / 4;
+    for (uint32_t v = blockIdx.x * ARGMAX_THREADS + threadIdx.x; v < nv; v += gridDim.x * ARGMAX_THREADS) {
+        uint4 c = reinterpret_cast<const uint4 *>(cnt)[v];
+        uint32_t cc[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) r = max_combine(r, MaxRec{cc[i], cc[i] ? 1u : 0u, cc[i] ? 4 * v + i : NO_ID});
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        uint32_t i = nv * 4 + threadIdx.x, c = cnt[i];
+        r = max_combine(r, MaxRec{c, c ? 1u : 0u, c ? i : NO_ID});
+    }
+    r = wave_max(r);
+    __shared__ MaxRec sm[ARGMAX_THREADS / WAVE];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = r;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < ARGMAX_THREADS / WAVE; w++) r = max_combine(r, sm[w]);
+        partial[blockIdx.x] = r;
+    }
+}
+__global__ void __launch_bounds__(256) zbpe_argmax_final(const MaxRec *__restrict__ partial, int np,
+                                                         const uint32_t *__restrict__ id_key, DevState *st) {
+    MaxRec r{0, 0, NO_ID};
+    for (int i = threadIdx.x; i < np; i += 256) r = max_combine(r, partial[i]);
+    r = wave_max(r);
+    __shared__ MaxRec sm[4];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = r;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) r = max_combine(r, sm[w]);
+        st->top_count = r.cnt;
+        st->tie_count = r.cnt ? r.ties : 0;
+        st->top_id = r.id;
+        st->top_key = r.id != NO_ID ? id_key[r.id] : EMPTY_KEY;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Stream helpers (hole skipping). Positions are signed 64-bit; -1 = none.
+// ------------------------------------------------------------------------------------------
+__device__ inline int64_t next_live(const uint16_t *tok, int64_t n, int64_t i) {
+    for (int64_t k = i + 1; k < n; ++k)
+        if (tok[k] != HOLE) return k;
+    return -1;
+}
+__device__ inline int64_t prev_live(const uint16_t *tok, int64_t i) {
+    for (int64_t k = i - 1; k >= 0; --k)
+        if (tok[k] != HOLE) return k;
+    return -1;
+}
+
+// LDS-privatised neighbour histograms: tokens < LDS_BINS in LDS, the rest straight to HBM.
+struct NeighbourHist {
+    uint32_t *lds_left, *lds_right;
+    uint32_t *g_left, *g_right;
+    __device__ inline void left(uint16_t t) {
+        if (t < LDS_BINS) atomicAdd(&lds_left[t], 1u);
+        else atomicAdd(&g_left[t], 1u);
+    }
+    __device__ inline void right(uint16_t t) {
+        if (t < LDS_BINS) atomicAdd(&lds_right[t], 1u);
+        else atomicAdd(&g_right[t], 1u);
+    }
+};
+
+struct ScanArgs {
+    const uint16_t *tok;
+    int64_t n;           // slots in the stream (live + holes); tok is padded with HOLE to a multiple of 8
+    uint32_t a, b;       // top pair (a != b for zbpe_scan_pairs)
+    uint32_t *left;      // [65536] count of (L, a) pairs destroyed == (L, X) pairs created
+    uint32_t *right;     // [65536] count of (b, R) destroyed == (X, R) created
+    DevState *st;
+    uint32_t *rec;       // occurrence start positions
+    uint32_t rec_cap;
+    int count_deltas;    // 0: encode mode (records only)
+};
+
+// General occurrence handler (any holes, any position). Returns 1 if (p, next_live(p)) == (a, b).
+__device__ inline int occ_slow(const ScanArgs &A, NeighbourHist &H, int64_t p, uint32_t &xx) {
+    const uint16_t *tok = A.tok;
+    int64_t q = next_live(tok, A.n, p);
+    if (q < 0 || tok[q] != A.b) return 0;
+    if (A.count_deltas) {
+        int64_t l = prev_live(tok, p);
+        if (l >= 0) {
+            uint16_t tl = tok[l];
+            bool merged_end = false;
+            if (tl == A.b) {
+                int64_t pl = prev_live(tok, l);
+                merged_end = pl >= 0 && tok[pl] == A.a;
+            }
+            if (!merged_end) H.left(tl);
+        }
+        int64_t r = next_live(tok, A.n, q);
+        if (r >= 0) {
+            uint16_t tr = tok[r];
+            bool r_occ = false;
+            if (tr == A.a) {
+                int64_t rn = next_live(tok, A.n, r);
+                r_occ = rn >= 0 && tok[rn] == A.b;
+            }
+            if (r_occ) xx++;
+            else H.right(tr);
+        }
+    }
+    return 1;
+}
+
+__device__ inline uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x += (uint32_t)__shfl_xor((int)x, off);
+    return x;
+}
+__device__ inline uint32_t tok_at(uint4 v, int k) {
+    uint32_t w = k < 2 ? v.x : k < 4 ? v.y : k < 6 ? v.z : v.w;
+    return (k & 1) ? (w >> 16) : (w & 0xffffu);
+}
+__device__ inline uint32_t match8(uint4 v, uint32_t a) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) m |= (tok_at(v, k) == a ? 1u : 0u) << k;
+    return m;
+}
+
+// ------------------------------------------------------------------------------------------
+// THE HOT KERNEL (one launch per merge): stream the token stream once, find every occurrence
+// of the top pair (a, b), a != b (every occurrence is merged: non-overlapping by construction),
+// and emit the pair-count deltas of replaceTopPairWithNewToken (basic_tokenizer.zig:207-232):
+//   left[L]  : pair (L, a) destroyed and (L, X) created, unless L ends the previous occurrence
+//   right[R] : pair (b, R) destroyed and (X, R) created, unless R starts the next occurrence
+//   xx       : adjacent occurrences: (b, a) destroyed and (X, X) created
+// plus the occurrence start positions. Each lane holds 8 consecutive tokens (16-B loads); a
+// wave covers 1 KiB contiguous; neighbours across a lane boundary come from DPP/ds shuffles.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs(ScanArgs A) {
+    __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
+    __shared__ uint32_t s_rec[SCAN_REC_CAP];
+    __shared__ uint32_t s_nrec, s_base, s_any;
+    for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
+    if (threadIdx.x == 0) { s_nrec = 0; s_any = 0; }
+    __syncthreads();
+    NeighbourHist H{s_left, s_right, A.left, A.right};
+    const uint16_t *tok = A.tok;
+    const int64_t n = A.n;
+    const int64_t nvec = (n + 7) / 8;
+    const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const int lane = threadIdx.x & 63;
+    uint32_t xx = 0;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t vbase = tile * (SCAN_TILE / 8);
+        uint4 v[SCAN_UNROLL];
+#pragma unroll
+        for (int u = 0; u < SCAN_UNROLL; u++) {
+            int64_t vi = vbase + u * SCAN_THREADS + threadIdx.x;
+            v[u] = vi < nvec ? reinterpret_cast<const uint4 *>(tok)[vi] : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+        }
+#pragma unroll
+        for (int u = 0; u < SCAN_UNROLL; u++) {
+            const int64_t vi = vbase + u * SCAN_THREADS + threadIdx.x;
+            uint32_t m = match8(v[u], A.a);
+            if (__ballot(m != 0) == 0) continue;  // wave-uniform: no `a` in this KiB
+            // neighbours: next vector's first 4 tokens, previous vector's last 2 tokens
+            uint32_t nx = __shfl_down((int)v[u].x, 1), ny = __shfl_down((int)v[u].y, 1);
+            uint32_t pw = __shfl_up((int)v[u].w, 1);
+            if (m) {
+                if (lane == 63) {
+                    if (vi + 1 < nvec) {
+                        uint2 t = reinterpret_cast<const uint2 *>(tok)[2 * (vi + 1)];
+                        nx = t.x; ny = t.y;
+                    } else { nx = 0xffffffffu; ny = 0xffffffffu; }
+                }
+                if (lane == 0) pw = vi > 0 ? reinterpret_cast<const uint32_t *>(tok)[4 * vi - 1] : 0xffffffffu;
+                // window of 14 tokens tok[p0-2 .. p0+11], p0 = 8*vi, kept in four u64 (no scratch)
+                const uint64_t W0 = (uint64_t)pw | ((uint64_t)v[u].x << 32);
+                const uint64_t W1 = (uint64_t)v[u].y | ((uint64_t)v[u].z << 32);
+                const uint64_t W2 = (uint64_t)v[u].w | ((uint64_t)nx << 32);
+                const uint64_t W3 = (uint64_t)ny;
+                auto win = [&](int i) -> uint32_t {
+                    uint64_t q = i < 4 ? W0 : i < 8 ? W1 : i < 12 ? W2 : W3;
+                    return (uint32_t)(q >> ((i & 3) * 16)) & 0xffffu;
+                };
+                while (m) {
+                    const int k = __ffs(m) - 1;
+                    m &= m - 1;
+                    const int64_t p = vi * 8 + k;
+                    const uint32_t t0 = win(k), t1 = win(k + 1), t3 = win(k + 3), t4 = win(k + 4), t5 = win(k + 5);
+                    // fast path: tok[p-2 .. p+3] all live and inside the stream
+                    const bool fast = p >= 2 && p + 3 < n && t0 != HOLE && t1 != HOLE && t3 != HOLE && t4 != HOLE &&
+                                      t5 != HOLE;
+                    int hit;
+                    if (fast) {
+                        hit = t3 == A.b;
+                        if (hit && A.count_deltas) {
+                            const bool merged_end = (t1 == A.b) && (t0 == A.a);
+                            if (!merged_end) H.left((uint16_t)t1);
+                            const bool r_occ = (t4 == A.a) && (t5 == A.b);
+                            if (r_occ) xx++;
+                            else H.right((uint16_t)t4);
+                        }
+                    } else {
+                        hit = occ_slow(A, H, p, xx);
+                    }
+                    if (hit) {
+                        uint32_t slot = atomicAdd(&s_nrec, 1u);
+                        s_rec[slot] = (uint32_t)p;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t nrec = s_nrec;
+        if (nrec) {
+            if (threadIdx.x == 0) {
+                s_base = atomicAdd(&A.st->rec_count, nrec);
+                s_any = 1;
+            }
+            __syncthreads();
+            const uint32_t base = s_base;
+            for (uint32_t i = threadIdx.x; i < nrec; i += SCAN_THREADS)
+                if (base + i < A.rec_cap) A.rec[base + i] = s_rec[i];
+            if (threadIdx.x == 0 && base + nrec > A.rec_cap) atomicOr(&A.st->error, 8u);
+            __syncthreads();
+            if (threadIdx.x == 0) s_nrec = 0;
+            __syncthreads();
+        }
+    }
+    // flush LDS neighbour histograms and the xx count
+    xx = wave_sum(xx);
+    if (lane == 0 && xx) atomicAdd(&A.st->xx, xx);
+    __syncthreads();
+    if (s_any) {
+        for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) {
+            uint32_t l = s_left[i], r = s_right[i];
+            if (l) atomicAdd(&A.left[i], l);
+            if (r) atomicAdd(&A.right[i], r);
+        }
+    }
+}
+
+// apply: tok[p] = X, next live slot after p (the `b`) becomes a hole. Occurrences are disjoint.
+__global__ void __launch_bounds__(256) zbpe_apply(uint16_t *tok, int64_t n, const uint32_t *__restrict__ rec,
+                                                  const DevState *st, uint32_t X) {
+    const uint32_t cnt = st->rec_count;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
+        int64_t p = rec[i];
+        tok[p] = (uint16_t)X;
+        int64_t q = next_live(tok, n, p);
+        if (q >= 0) tok[q] = HOLE;
+    }
+}
+
+// count update after merge X = (a, b): one thread per neighbour token t < X.
+__global__ void __launch_bounds__(256) zbpe_update(Tables T, DevState *st, uint32_t *left, uint32_t *right, uint32_t a,
+                                                   uint32_t b, uint32_t X, uint32_t top_key) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t < X) {
+        uint32_t l = left[t];
+        if (l) {
+            left[t] = 0;
+            pair_dec(T, st, pair_key(t, a), l);
+            pair_new(T, st, pair_key(t, X), l);
+        }
+        uint32_t r = right[t];
+        if (r) {
+            right[t] = 0;
+            pair_dec(T, st, pair_key(b, t), r);
+            pair_new(T, st, pair_key(X, t), r);
+        }
+    }
+    if (t == 0) {
+        const uint32_t occ = st->rec_count, xx = st->xx;
+        if (xx) {
+            pair_dec(T, st, pair_key(b, a), xx);
+            pair_new(T, st, pair_key(X, X), xx);
+        }
+        const uint32_t top_id = ht_find(T, top_key);
+        if (top_id == NO_ID) { atomicOr(&st->error, 4u); return; }
+        uint32_t old = atomicSub(&T.id_cnt[top_id], occ);
+        if (old < occ) atomicOr(&st->error, 2u);
+        if (old == occ) atomicSub(&st->live, 1);
+    }
+}
+
+// zeroes the per-merge scratch counters (kept separate so the update kernel can read them)
+__global__ void zbpe_reset_merge(DevState *st) {
+    st->last_occ = st->rec_count;
+    st->total_occ += st->rec_count;
+    st->rec_count = 0;
+    st->xx = 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Self pair (a, a): left-greedy over runs needs each position's offset parity inside its run
+// of a's (basic_tokenizer.zig:217-226 consumes a run of L a's as floor(L/2) merges). The stream
+// is compacted (no holes) before these kernels run. Per tile: all_a flag + trailing-run parity;
+// a scan composes them into the parity of the run entering each tile.
+// ------------------------------------------------------------------------------------------
+constexpr int SELF_THREADS = 256;
+constexpr int SELF_PER_THREAD = 32;
+constexpr int SELF_TILE = SELF_THREADS * SELF_PER_THREAD;  // 8192
+__global__ void __launch_bounds__(SELF_THREADS) zbpe_self_tiles(const uint16_t *__restrict__ tok, int64_t n, uint32_t a,
+                                                                uint8_t *__restrict__ tile_fn) {
+    // tile_fn bit0: tile is all a; bit1: parity of the trailing a-run (if not all a)
+    const int64_t beg = blockIdx.x * (int64_t)SELF_TILE;
+    const int64_t end = min(n, beg + SELF_TILE);
+    __shared__ int32_t s_last[SELF_THREADS];
+    int32_t last = -1;  // last index (tile-relative) holding a non-a
+    for (int i = 0; i < SELF_PER_THREAD; i++) {
+        int64_t p = beg + threadIdx.x * SELF_PER_THREAD + i;
+        if (p < end && tok[p] != a) last = threadIdx.x * SELF_PER_THREAD + i;
+    }
+    s_last[threadIdx.x] = last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t L = -1;
+        for (int t = 0; t < SELF_THREADS; t++) L = max(L, s_last[t]);
+        int64_t len = end - beg;
+        uint8_t f;
+        if (L < 0) f = 1 | (uint8_t)((len & 1) << 1);  // all a: carry parity += len
+        else f = (uint8_t)(((len - 1 - L) & 1) << 1);
+        tile_fn[blockIdx.x] = f;
+    }
+}
+// carry_in[t] = parity of the a-run entering tile t. One block; each thread composes a segment.
+__global__ void __launch_bounds__(1024) zbpe_self_carry(const uint8_t *__restrict__ tile_fn, int64_t ntiles,
+                                                        uint8_t *__restrict__ carry_in) {
+    // function of a tile: x -> all_a ? x ^ p : p   (x, p parities)
+    __shared__ uint8_t s_all[1024], s_par[1024];
+    const int64_t per = (ntiles + 1023) / 1024;
+    const int64_t b0 = threadIdx.x * per, b1 = min(ntiles, b0 + per);
+    uint8_t all = 1, par = 0;  // identity
+    for (int64_t t = b0; t < b1; t++) {
+        uint8_t f = tile_fn[t], fa = f & 1, fp = (f >> 1) & 1;
+        if (fa) par ^= fp;   // compose: g(x) = f(cur(x))
+        else { all = 0; par = fp; }
+    }
+    s_all[threadIdx.x] = all;
+    s_par[threadIdx.x] = par;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // sequential exclusive composition over 1024 segments
+        uint8_t x = 0;
+        for (int t = 0; t < 1024; t++) {
+            uint8_t nx = s_all[t] ? (x ^ s_par[t]) : s_par[t];
+            s_par[t] = x;  // carry into segment t
+            x = nx;
+        }
+    }
+    __syncthreads();
+    uint8_t x = s_par[threadIdx.x];
+    for (int64_t t = b0; t < b1; t++) {
+        carry_in[t] = x;
+        uint8_t f = tile_fn[t], fa = f & 1, fp = (f >> 1) & 1;
+        x = fa ? (x ^ fp) : fp;
+    }
+}
+__global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A, const uint8_t *__restrict__ carry_in) {
+    __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
+    __shared__ uint32_t s_rec[SELF_TILE / 2];
+    __shared__ int32_t s_last[SELF_THREADS];
+    __shared__ uint32_t s_nrec, s_base;
+    for (int i = threadIdx.x; i < LDS_BINS; i += SELF_THREADS) { s_left[i] = 0; s_right[i] = 0; }
+    if (threadIdx.x == 0) s_nrec = 0;
+    __syncthreads();
+    NeighbourHist H{s_left, s_right, A.left, A.right};
+    const uint16_t *tok = A.tok;
+    const int64_t n = A.n;
+    const uint32_t a = A.a;
+    const int64_t beg = blockIdx.x * (int64_t)SELF_TILE;
+    const int64_t end = min(n, beg + SELF_TILE);
+    const int64_t t0 = beg + threadIdx.x * SELF_PER_THREAD;
+    int32_t last = -1;
+    for (int i = 0; i < SELF_PER_THREAD; i++) {
+        int64_t p = t0 + i;
+        if (p < end && tok[p] != a) last = (int32_t)(threadIdx.x * SELF_PER_THREAD + i);
+    }
+    s_last[threadIdx.x] = last;
+    __syncthreads();
+    // exclusive max over threads before me (sequential: 256 entries, cheap relative to the tile)
+    int32_t prev = -1;
+    for (int t = 0; t < (int)threadIdx.x; t++) prev = max(prev, s_last[t]);
+    const uint32_t carry = carry_in[blockIdx.x] & 1;
+    uint32_t xx = 0;
+    int32_t lastna = prev;  // tile-relative index of the last non-a before the current position
+    for (int i = 0; i < SELF_PER_THREAD; i++) {
+        const int64_t p = t0 + i;
+        if (p >= end) break;
+        const int32_t rel = (int32_t)(threadIdx.x * SELF_PER_THREAD + i);
+        if (tok[p] != a) { lastna = rel; continue; }
+        uint32_t off_par = lastna >= 0 ? (uint32_t)((rel - lastna - 1) & 1) : ((carry + (uint32_t)rel) & 1);
+        if (off_par) continue;
+        if (p + 1 >= n || tok[p + 1] != a) continue;
+        // occurrence at p
+        if (A.count_deltas) {
+            // offset 0 in the run: the left neighbour is not the end of a previous occurrence
+            const bool run_start = lastna >= 0 ? (rel - lastna - 1 == 0) : (rel == 0 && (p == 0 || tok[p - 1] != a));
+            if (run_start && p > 0) H.left(tok[p - 1]);
+            if (p + 2 < n) {
+                uint16_t tr = tok[p + 2];
+                bool r_occ = (tr == a) && (p + 3 < n) && (tok[p + 3] == a);
+                if (r_occ) xx++;
+                else H.right(tr);
+            }
+        }
+        uint32_t slot = atomicAdd(&s_nrec, 1u);
+        s_rec[slot] = (uint32_t)p;
+    }
+    __syncthreads();
+    const uint32_t nrec = s_nrec;
+    if (nrec) {
+        if (threadIdx.x == 0) s_base = atomicAdd(&A.st->rec_count, nrec);
+        __syncthreads();
+        const uint32_t base = s_base;
+        for (uint32_t i = threadIdx.x; i < nrec; i += SELF_THREADS)
+            if (base + i < A.rec_cap) A.rec[base + i] = s_rec[i];
+        if (threadIdx.x == 0 && base + nrec > A.rec_cap) atomicOr(&A.st->error, 8u);
+    }
+    xx = wave_sum(xx);
+    if ((threadIdx.x & 63) == 0 && xx) atomicAdd(&A.st->xx, xx);
+    if (nrec) {
+        for (int i = threadIdx.x; i < LDS_BINS; i += SELF_THREADS) {
+            uint32_t l = s_left[i], r = s_right[i];
+            if (l) atomicAdd(&A.left[i], l);
+            if (r) atomicAdd(&A.right[i], r);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Compaction (squeeze holes): tile counts -> exclusive scan -> scatter
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) zbpe_compact_count(const uint16_t *__restrict__ tok, int64_t n,
+                                                          uint32_t *__restrict__ tile_cnt) {
+    const int64_t beg = blockIdx.x * (int64_t)COMPACT_TILE;
+    uint32_t c = 0;
+    for (int i = threadIdx.x; i < COMPACT_TILE / 8; i += 256) {
+        int64_t p = beg + 8 * i;
+        if (p >= n) break;
+        uint4 v = *reinterpret_cast<const uint4 *>(tok + p);
+#pragma unroll
+        for (int k = 0; k < 8; k++) c += (tok_at(v, k) != HOLE) && (p + k < n);
+    }
+    c = wave_sum(c);
+    __shared__ uint32_t s[4];
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+// exclusive scan of tile counts (one block, 1024 threads, sequential segments)
+__global__ void __launch_bounds__(1024) zbpe_scan_u32(const uint32_t *__restrict__ in, int64_t m,
+                                                      uint64_t *__restrict__ out, uint64_t *total) {
+    __shared__ uint64_t s[1024];
+    const int64_t per = (m + 1023) / 1024;
+    const int64_t b0 = threadIdx.x * per, b1 = min(m, b0 + per);
+    uint64_t sum = 0;
+    for (int64_t i = b0; i < b1; i++) sum += in[i];
+    s[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        uint64_t v = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
+        __syncthreads();
+        s[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t run = s[threadIdx.x] - sum;
+    for (int64_t i = b0; i < b1; i++) { out[i] = run; run += in[i]; }
+    if (threadIdx.x == 1023) *total = s[1023];
+}
+__global__ void __launch_bounds__(256) zbpe_compact_scatter(const uint16_t *__restrict__ tok, int64_t n,
+                                                            const uint64_t *__restrict__ tile_off, uint16_t *__restrict__ out) {
+    // each thread owns 32 consecutive tokens of the tile
+    const int64_t beg = blockIdx.x * (int64_t)COMPACT_TILE + threadIdx.x * 32;
+    uint16_t t[32];
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        int64_t p = beg + 8 * q;
+        uint4 v = p < n ? *reinterpret_cast<const uint4 *>(tok + p) : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            uint32_t x = (p + k < n) ? tok_at(v, k) : HOLE;
+            t[8 * q + k] = (uint16_t)x;
+            c += x != HOLE;
+        }
+    }
+    // block exclusive scan of c
+    __shared__ uint32_t s[256];
+    s[threadIdx.x] = c;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        uint32_t v = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
+        __syncthreads();
+        s[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t o = tile_off[blockIdx.x] + s[threadIdx.x] - c;
+#pragma unroll
+    for (int k = 0; k < 32; k++)
+        if (t[k] != HOLE) out[o++] = t[k];
+}
+__global__ void zbpe_fill_u16(uint16_t *p, int64_t beg, int64_t end, uint16_t v) {
+    for (int64_t i = beg + blockIdx.x * 256 + threadIdx.x; i < end; i += (int64_t)gridDim.x * 256) p[i] = v;
+}
+
+// ------------------------------------------------------------------------------------------
+// Zig-order tie-break. The Zig map of iteration t has capacity C_f; its set
+// of occupied slots depends only on the multiset of home slots hash & (C_f-1), so a parallel
+// linear-probing insert of every live key reproduces it exactly. Tied keys sit in the run that
+// holds their home; the tied key with the smallest home wins unless the second-smallest home is
+// in the same run or a tied key could have wrapped past slot C_f-1 (then: exact emulation).
+// ------------------------------------------------------------------------------------------
+__global__ void zbpe_lastpair(const uint16_t *tok, int64_t n, Tables T, DevState *st) {
+    if (threadIdx.x || blockIdx.x) return;
+    int64_t j = n - 1;
+    while (j >= 0 && tok[j] == HOLE) j--;
+    int64_t i = j - 1;
+    while (i >= 0 && tok[i] == HOLE) i--;
+    uint32_t c = 0;
+    if (i >= 0) {
+        uint32_t id = ht_find(T, pair_key(tok[i], tok[j]));
+        c = id == NO_ID ? 0 : T.id_cnt[id];
+    }
+    st->lastpair_count = c;
+}
+__global__ void __launch_bounds__(256) zbpe_tie_occupy(Tables T, DevState *st, uint32_t cap_mask, uint32_t top,
+                                                       uint32_t *__restrict__ bitmap, uint64_t *__restrict__ tie_list,
+                                                       uint32_t tie_cap) {
+    const uint32_t n = min(st->num_ids, T.id_cap);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        uint32_t c = T.id_cnt[i];
+        if (!c) continue;
+        uint32_t key = T.id_key[i];
+        uint32_t h = (uint32_t)(zig_pair_hash(key) & cap_mask), s = h;
+        for (;;) {
+            uint32_t bit = 1u << (s & 31);
+            uint32_t old = atomicOr(&bitmap[s >> 5], bit);
+            if (!(old & bit)) break;
+            s = (s + 1) & cap_mask;
+        }
+        if (c == top) {
+            uint32_t j = atomicAdd(&st->tie_len, 1u);
+            if (j < tie_cap) tie_list[j] = ((uint64_t)h << 32) | key;
+        }
+    }
+}
+__device__ inline bool occ_bit(const uint32_t *bm, uint32_t s) { return (bm[s >> 5] >> (s & 31)) & 1u; }
+__global__ void __launch_bounds__(256) zbpe_tie_resolve(DevState *st, const uint64_t *__restrict__ tie_list, uint32_t tie_cap,
+                                                        const uint32_t *__restrict__ bitmap, uint32_t cap_mask) {
+    const uint32_t len = min(st->tie_len, tie_cap);
+    // smallest (home, key), second smallest home, largest home
+    uint64_t m1 = ~0ull, m2 = ~0ull;
+    uint32_t hmax = 0;
+    for (uint32_t i = threadIdx.x; i < len; i += 256) {
+        uint64_t e = tie_list[i];
+        if (e < m1) { m2 = m1; m1 = e; } else if (e < m2) m2 = e;
+        hmax = max(hmax, (uint32_t)(e >> 32));
+    }
+    __shared__ uint64_t s1[256], s2[256];
+    __shared__ uint32_t sh[256];
+    s1[threadIdx.x] = m1; s2[threadIdx.x] = m2; sh[threadIdx.x] = hmax;
+    __syncthreads();
+    if (threadIdx.x) return;
+    for (int t = 1; t < 256; t++) {  // second smallest of {m1, m2, s1[t], s2[t]}
+        const uint64_t b1 = s1[t], b2 = s2[t];
+        m2 = min(max(m1, b1), min(m2, b2));
+        m1 = min(m1, b1);
+        hmax = max(hmax, sh[t]);
+    }
+    const uint32_t cap = cap_mask + 1;
+    const uint32_t h1 = (uint32_t)(m1 >> 32);
+    uint32_t verdict = 0;
+    if (st->tie_len > tie_cap) verdict = 1;
+    // first free slot at or after h1
+    uint32_t f = h1;
+    while (f < cap && occ_bit(bitmap, f)) f++;
+    if (f == cap) verdict = 1;  // h1's run reaches the wrap
+    if (m2 != ~0ull && f > (uint32_t)(m2 >> 32)) verdict = 1;  // second tied key in the same run
+    if (occ_bit(bitmap, cap - 1) && occ_bit(bitmap, 0)) {
+        uint32_t sw = cap - 1;
+        while (sw > 0 && occ_bit(bitmap, sw - 1)) sw--;
+        if (hmax >= sw) verdict = 1;  // a tied key in the wrapping run
+    }
+    st->tie_verdict = verdict;
+    st->tie_winner = (uint32_t)m1;
+}
+
+// exact fallback: first occurrence position of every live pair in the current stream
+__global__ void __launch_bounds__(256) zbpe_first_occ(const uint16_t *__restrict__ tok, int64_t n, Tables T, uint32_t *first,
+                                                      DevState *st) {
+    for (int64_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        uint16_t x = tok[p];
+        if (x == HOLE) continue;
+        int64_t q = next_live(tok, n, p);
+        if (q < 0) continue;
+        uint32_t id = ht_find(T, pair_key(x, tok[q]));
+        if (id == NO_ID) { atomicOr(&st->error, 4u); continue; }
+        atomicMin(&first[id], (uint32_t)p);
+    }
+}
+__global__ void __launch_bounds__(256) zbpe_gather_live(Tables T, const uint32_t *__restrict__ first, DevState *st,
+                                                        LiveRec *__restrict__ out, uint32_t out_cap) {
+    const uint32_t n = min(st->num_ids, T.id_cap);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        uint32_t c = T.id_cnt[i];
+        if (!c) continue;
+        uint32_t j = atomicAdd(&st->gather_len, 1u);
+        if (j < out_cap) out[j] = LiveRec{first[i], T.id_key[i], c, 0};
+    }
+}
+
+// verification: recount every live pair of the stream and compare with the maintained counts
+__global__ void __launch_bounds__(256) zbpe_recount(const uint16_t *__restrict__ tok, int64_t n, Tables T, uint32_t *recount,
+                                                    DevState *st) {
+    for (int64_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+        uint16_t x = tok[p];
+        if (x == HOLE) continue;
+        int64_t q = next_live(tok, n, p);
+        if (q < 0) continue;
+        uint32_t id = ht_find(T, pair_key(x, tok[q]));
+        if (id == NO_ID) { atomicAdd(&st->mismatches, 1u); continue; }
+        atomicAdd(&recount[id], 1u);
+    }
+}
+__global__ void __launch_bounds__(256) zbpe_recount_compare(Tables T, const uint32_t *recount, DevState *st) {
+    const uint32_t n = min(st->num_ids, T.id_cap);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+        if (recount[i] != T.id_cnt[i]) atomicAdd(&st->mismatches, 1u);
+}
+
+// rebuild: keep live ids only (drops dead pairs so the argmax pass stays short)
+__global__ void __launch_bounds__(256) zbpe_rebuild(const uint32_t *__restrict__ old_key, const uint32_t *__restrict__ old_cnt,
+                                                    uint32_t old_n, Tables T, DevState *st) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < old_n; i += gridDim.x * 256) {
+        uint32_t c = old_cnt[i];
+        if (!c) continue;
+        uint32_t id = atomicAdd(&st->num_ids, 1u);
+        if (id >= T.id_cap) { atomicOr(&st->error, 1u); continue; }
+        T.id_key[id] = old_key[i];
+        T.id_cnt[id] = c;
+        ht_insert_new(T, old_key[i], id);
+    }
+}
+
+}  // namespace zbpe

@@ -1,0 +1,55 @@
+// Types and constants shared by the device code (kernels.hpp) and the host engine.
+#pragma once
+#include <stdint.h>
+
+namespace zbpe {
+
+
+constexpr uint16_t HOLE = 0xFFFF;
+constexpr uint32_t EMPTY_KEY = 0xFFFFFFFFu;  // (0xFFFF, 0xFFFF) is never a real pair
+constexpr uint32_t NO_ID = 0xFFFFFFFFu;
+constexpr int WAVE = 64;
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_UNROLL = 4;                                       // 16-B vectors per thread per tile
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_UNROLL * 8;            // tokens per tile (8192)
+constexpr int SCAN_REC_CAP = SCAN_TILE / 2;                          // occurrences per tile (non-overlapping)
+constexpr int LDS_BINS = 1024;                                       // neighbour tokens counted in LDS
+constexpr int COMPACT_TILE = 8192;                                   // tokens per compaction tile
+
+__host__ __device__ constexpr inline uint32_t pair_key(uint32_t first, uint32_t second) { return first | (second << 16); }
+
+// Device-resident state. Host reads a copy after each merge (one small D2H per merge).
+struct DevState {
+    uint32_t num_ids;        // pair ids allocated
+    int32_t live;            // D_t: pairs with count > 0
+    uint32_t rec_count;      // occurrences recorded by the last scan
+    uint32_t xx;             // adjacent occurrences: (b,a) -> (X,X)
+    uint32_t top_count;      // argmax result
+    uint32_t tie_count;
+    uint32_t top_id;
+    uint32_t top_key;
+    uint32_t lastpair_count; // count of the stream's last pair (decides the Zig map's final grow)
+    uint32_t tie_len;        // tied keys collected by the tie kernel
+    uint32_t tie_verdict;    // 0 = winner found by the cluster test, 1 = needs the exact emulation
+    uint32_t tie_winner;
+    uint32_t error;          // bit flags: 1 id overflow, 2 count underflow, 4 key missing, 8 record overflow
+    uint32_t gather_len;
+    uint32_t mismatches;
+    uint32_t last_occ;       // occurrences merged by the last merge (copied by zbpe_reset_merge)
+    uint32_t total_occ;      // running sum of last_occ (encode bookkeeping)
+    uint32_t pad[2];
+};
+
+struct Tables {
+    uint32_t *ht_key;   // [ht_cap]
+    uint32_t *ht_id;    // [ht_cap]
+    uint32_t ht_mask;
+    uint32_t *id_key;   // [id_cap]
+    uint32_t *id_cnt;   // [id_cap]
+    uint32_t id_cap;
+};
+
+struct MaxRec { uint32_t cnt, ties, id; };
+struct LiveRec { uint32_t first_pos, key, count, pad; };
+
+}  // namespace zbpe
