@@ -98,6 +98,19 @@ def test_random_corpora_vs_oracle(engine, kind, n, vocab, seed):
     assert engine.verify_counts() == 0
 
 
+@pytest.mark.parametrize("kind,n,vocab,seed", [("words_utf8", 2 << 20, 1500, 51), ("uniform", 1 << 16, 700, 52)])
+def test_debug_checks_hot_list_and_compaction(kind, n, vocab, seed):
+    """debug_checks: every merge cross-checks the hot-list argmax against a full argmax over all ids."""
+    text = zbpe.synth_corpus(kind, seed, n)
+    e = zbpe.Engine(0)
+    e.set_option("debug_checks", 1)
+    m, c, st = e.train(text, vocab)
+    r = O.train(text, vocab, max_merges=300 if n > (1 << 20) else 0)
+    assert m[: len(r.merges)].tolist() == r.merges.tolist()
+    assert e.verify_counts() == 0
+    e.close()
+
+
 def test_compaction_policies_agree(engine):
     text = zbpe.synth_corpus("words_utf8", 31, 300000)
     r = O.train(text, 700)

@@ -3,9 +3,9 @@
 //
 // Per merge (BasicTokenizer.expandVocabulary loop, basic_tokenizer.zig:183-204):
 //   [argmax of the previous update is already on the host]
-//   tie? -> zbpe_lastpair, zbpe_tie_occupy, zbpe_tie_resolve (+ exact emulation if undecided)
+//   tie? -> zbpe_tie_occupy, zbpe_tie_resolve (+ exact emulation if undecided)
 //   zbpe_scan_pairs | (compact, zbpe_self_tiles, zbpe_self_carry, zbpe_scan_self) for (a, a)
-//   zbpe_apply, zbpe_update, zbpe_reset_merge, zbpe_argmax_partial/final -> one D2H + sync
+//   zbpe_apply, zbpe_update, zbpe_reset_merge, zbpe_argmax_hot/final -> one D2H + sync
 #include "engine.hpp"
 
 #include <algorithm>
@@ -56,14 +56,16 @@ void Engine::release() {
     f(T.ht_key); f(T.ht_id); f(T.id_key); f(T.id_cnt);
     f(d_left); f(d_right); f(d_st); f(d_rec); f(d_partial); f(d_hist);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist);
     if (h_st) (void)hipHostFree(h_st);
+    if (h_count_hist) (void)hipHostFree(h_count_hist);
     for (auto &e : ev) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
     d_text = nullptr; d_tok[0] = d_tok[1] = nullptr; T = Tables{};
     d_left = d_right = nullptr; d_st = nullptr; d_rec = nullptr; d_partial = nullptr; d_hist = nullptr;
     d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr;
     d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
+    d_summ = nullptr; d_count_hist = nullptr; h_count_hist = nullptr; hot_cap_alloc = home_words_cap = 0; home_slots = 0;
     for (auto &e : ev) e = nullptr;
 }
 
@@ -80,6 +82,8 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipMalloc(&d_right, 65536 * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
+    HIP_OK(hipMalloc(&d_count_hist, COUNT_BINS * sizeof(uint32_t)));
+    HIP_OK(hipHostMalloc((void **)&h_count_hist, COUNT_BINS * sizeof(uint32_t), hipHostMallocDefault));
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
     // the initial byte-pair histogram keeps 128 KiB of bins in LDS
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_count_byte_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4));
@@ -130,6 +134,7 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     size_t ht_cap_new = 1;
     while (ht_cap_new < 2 * id_cap_new) ht_cap_new <<= 1;
     Tables N{};
+    N.hot = T.hot; N.hot_cap = T.hot_cap; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
     if (hipMalloc(&N.ht_key, ht_cap_new * 4) != hipSuccess || hipMalloc(&N.ht_id, ht_cap_new * 4) != hipSuccess ||
@@ -149,6 +154,7 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
         stats_rebuilds++;
     }
     T = N;
+    hot_stale = true;  // ids were renumbered
     return ZBPE_OK;
 }
 
@@ -191,35 +197,138 @@ zbpe_status Engine::compact() {
     return ZBPE_OK;
 }
 
+static uint32_t count_bin_lo(int b) {
+    if (b < 64) return (uint32_t)b;
+    const int e = (b - 64) / 32 + 6, m = (b - 64) % 32;
+    return (uint32_t)(32 + m) << (e - 5);
+}
+
+// Hot list rebuild: choose theta so that about hot_target live ids have count >= theta.
+zbpe_status Engine::rebuild_hot() {
+    const uint32_t nid = h_st->num_ids;
+    HIP_OK(hipMemsetAsync(d_count_hist, 0, COUNT_BINS * 4, stream));
+    zbpe_count_hist<<<std::min<uint32_t>(2048, nid / 256 + 1), 256, 0, stream>>>(T, d_st, d_count_hist);
+    LAUNCH_OK();
+    HIP_OK(hipMemcpyAsync(h_count_hist, d_count_hist, COUNT_BINS * 4, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    uint64_t cum = 0;
+    uint32_t theta = 1;
+    for (int b = COUNT_BINS - 1; b >= 1; b--) {
+        const uint64_t h = h_count_hist[b];
+        if (!h) continue;
+        if (cum > 0 && cum + h > hot_target) break;
+        cum += h;
+        theta = count_bin_lo(b);
+    }
+    const size_t need = std::max<size_t>(4 * hot_target, 2 * cum + 4096);
+    if (!T.hot || hot_cap_alloc < need) {
+        if (T.hot) (void)hipFree(T.hot);
+        T.hot = nullptr;
+        if (hipMalloc(&T.hot, need * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            hot_cap_alloc = 0;
+            return fail(ZBPE_OUT_OF_MEMORY, "hot list allocation (%zu ids) failed", need);
+        }
+        hot_cap_alloc = need;
+    }
+    T.hot_cap = (uint32_t)hot_cap_alloc;
+    uint32_t th[2] = {theta, 0};  // DevState.theta, DevState.hot_len
+    HIP_OK(hipMemcpyAsync(&d_st->theta, th, 8, hipMemcpyHostToDevice, stream));
+    zbpe_hot_build<<<std::min<uint32_t>(2048, nid / 256 + 1), 256, 0, stream>>>(T, d_st);
+    LAUNCH_OK();
+    HIP_OK(hipStreamSynchronize(stream));
+    hot_stale = false;
+    hot_rebuilds++;
+    return ZBPE_OK;
+}
+
 zbpe_status Engine::launch_argmax() {
-    const uint32_t nid = std::max<uint32_t>(h_st->num_ids + 2 * 65536u, 1);  // upper bound after this merge
-    int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, (nid / 4 + ARGMAX_THREADS - 1) / ARGMAX_THREADS + 1);
-    zbpe_argmax_partial<<<blocks, ARGMAX_THREADS, 0, stream>>>(T.id_cnt, T.id_cap, d_st, d_partial);
+    if (hot_stale) CHECK(rebuild_hot());
+    const uint32_t cap = T.hot_cap;
+    int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, (cap + 4 * ARGMAX_THREADS - 1) / (4 * ARGMAX_THREADS));
+    blocks = std::max(blocks, 1);
+    zbpe_argmax_hot<<<blocks, ARGMAX_THREADS, 0, stream>>>(T, d_st, d_partial);
     LAUNCH_OK();
-    zbpe_argmax_final<<<1, 256, 0, stream>>>(d_partial, blocks, T.id_key, d_st);
+    zbpe_argmax_final<<<1, 256, 0, stream>>>(d_partial, blocks, T, d_tok[cur], n_slots, d_st);
     LAUNCH_OK();
+    return ZBPE_OK;
+}
+
+// After an argmax + sync: if the hot list overflowed or no listed id still reaches theta, the
+// result is not the global max: rebuild the list (lower theta) and select again.
+zbpe_status Engine::select_ready() {
+    for (int tries = 0; tries < 4; tries++) {
+        const bool overflow = h_st->hot_len > T.hot_cap;
+        const bool exhausted = h_st->live > 0 && h_st->top_count == 0;
+        if (!overflow && !exhausted) {
+            if (debug_checks) {  // cross-check the hot list against a full argmax over every id
+                DevState *dbg = nullptr;
+                HIP_OK(hipMalloc(&dbg, sizeof(DevState)));
+                HIP_OK(hipMemcpyAsync(dbg, d_st, sizeof(DevState), hipMemcpyDeviceToDevice, stream));
+                const uint32_t nid = h_st->num_ids;
+                const int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, nid / (4 * ARGMAX_THREADS) + 1);
+                zbpe_argmax_partial<<<blocks, ARGMAX_THREADS, 0, stream>>>(T.id_cnt, T.id_cap, dbg, d_partial);
+                zbpe_argmax_final<<<1, 256, 0, stream>>>(d_partial, blocks, T, d_tok[cur], n_slots, dbg);
+                DevState h{};
+                HIP_OK(hipMemcpyAsync(&h, dbg, sizeof(DevState), hipMemcpyDeviceToHost, stream));
+                HIP_OK(hipStreamSynchronize(stream));
+                (void)hipFree(dbg);
+                if (h.top_count != h_st->top_count || h.tie_count != h_st->tie_count)
+                    return fail(ZBPE_INTERNAL, "hot-list argmax (%u x%u) != full argmax (%u x%u)", h_st->top_count,
+                                h_st->tie_count, h.top_count, h.tie_count);
+            }
+            return ZBPE_OK;
+        }
+        hot_stale = true;
+        CHECK(launch_argmax());
+        CHECK(sync_state());
+    }
+    return fail(ZBPE_INTERNAL, "hot list rebuild did not converge (live %d, hot_len %u, theta %u)", h_st->live, h_st->hot_len,
+                h_st->theta);
+}
+
+zbpe_status Engine::rebuild_home(uint64_t cap) {
+    const size_t words = cap / 4 + 1;
+    if (!T.home_cnt || home_words_cap < words) {
+        if (T.home_cnt) (void)hipFree(T.home_cnt);
+        T.home_cnt = nullptr;
+        if (hipMalloc(&T.home_cnt, words * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            home_words_cap = 0;
+            home_slots = 0;
+            return fail(ZBPE_OUT_OF_MEMORY, "home histogram allocation (%llu slots) failed", (unsigned long long)cap);
+        }
+        home_words_cap = words;
+    }
+    HIP_OK(hipMemsetAsync(T.home_cnt, 0, words * 4, stream));
+    T.home_mask = (uint32_t)(cap - 1);
+    const uint32_t nid = h_st->num_ids;
+    zbpe_home_build<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_st);
+    LAUNCH_OK();
+    home_slots = cap;
+    home_rebuilds++;
     return ZBPE_OK;
 }
 
 // Zig-order winner among the pairs sharing the top count
 zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     stats.tie_iterations++;
-    zbpe_lastpair<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, T, d_st);
-    LAUNCH_OK();
-    CHECK(sync_state());
     const uint64_t D = (uint64_t)h_st->live;
     const bool call_after = h_st->lastpair_count >= 2;
     const uint64_t cap = zig_final_capacity(D, call_after);
     if (cap > (1ull << 31)) return fail(ZBPE_INTERNAL, "Zig map capacity %llu out of range", (unsigned long long)cap);
-    CHECK(ensure(&d_bitmap, bitmap_cap, cap / 32 + 1, "tie bitmap"));
+    if (cap != home_slots) CHECK(rebuild_home(cap));
+    const size_t nb = (cap + SUMM_SLOTS - 1) / SUMM_SLOTS;
+    CHECK(ensure(&d_summ, summ_cap, nb, "home summaries"));
     CHECK(ensure(&d_tie_list, tie_list_cap, ties, "tie list"));
-    HIP_OK(hipMemsetAsync(d_bitmap, 0, (cap / 32 + 1) * 4, stream));
     HIP_OK(hipMemsetAsync(&d_st->tie_len, 0, 4, stream));
-    const uint32_t nid = h_st->num_ids;
-    zbpe_tie_occupy<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_st, (uint32_t)(cap - 1), top, d_bitmap,
-                                                                                 d_tie_list, (uint32_t)tie_list_cap);
+    const uint32_t hl = std::min<uint32_t>(h_st->hot_len, T.hot_cap);
+    zbpe_tie_collect<<<std::min<uint32_t>(1024, hl / 256 + 1), 256, 0, stream>>>(T, d_st, top, (uint32_t)(cap - 1), d_tie_list,
+                                                                                  (uint32_t)tie_list_cap);
     LAUNCH_OK();
-    zbpe_tie_resolve<<<1, 256, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, d_bitmap, (uint32_t)(cap - 1));
+    zbpe_home_summary<<<(unsigned)nb, 256, 0, stream>>>(T.home_cnt, (uint32_t)cap, d_summ);
+    LAUNCH_OK();
+    zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, T.home_cnt, d_summ, (uint32_t)cap);
     LAUNCH_OK();
     CHECK(sync_state());
     if (h_st->tie_len != ties)
@@ -228,6 +337,7 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
         *winner = h_st->tie_winner;
         return ZBPE_OK;
     }
+    const uint32_t nid = h_st->num_ids;
     // exact emulation from first-occurrence order
     stats.tie_fallbacks++;
     CHECK(ensure(&d_first, first_cap, nid, "first occurrences"));
@@ -242,7 +352,8 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     const uint32_t g = h_st->gather_len;
     if (g != D || g > gather_cap) return fail(ZBPE_INTERNAL, "gathered %u live pairs, expected %llu", g, (unsigned long long)D);
     std::vector<LiveRec> recs(g);
-    HIP_OK(hipMemcpy(recs.data(), d_gather, (size_t)g * sizeof(LiveRec), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpyAsync(recs.data(), d_gather, (size_t)g * sizeof(LiveRec), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
     std::vector<ZigOrderInput> in(g);
     for (uint32_t i = 0; i < g; i++) in[i] = ZigOrderInput{recs[i].first_pos, recs[i].key, recs[i].count};
     if (!zig_order_winner(std::move(in), top, call_after, winner))
@@ -289,6 +400,10 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         HIP_OK(hipMemsetAsync(T.ht_key, 0xFF, ((size_t)T.ht_mask + 1) * 4, stream));
     }
     HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
+    home_slots = 0;
+    T.home_mask = 0;
+    if (T.home_cnt) { (void)hipFree(T.home_cnt); T.home_cnt = nullptr; home_words_cap = 0; }
+    hot_stale = true;
     HIP_OK(hipMemsetAsync(d_left, 0, 65536 * 4, stream));
     HIP_OK(hipMemsetAsync(d_right, 0, 65536 * 4, stream));
     HIP_OK(hipMemsetAsync(d_hist, 0, 65536 * 4, stream));
@@ -303,10 +418,11 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         LAUNCH_OK();
     }
     HIP_OK(hipEventRecord(ev[1], stream));
-    h_st->num_ids = 0;
+    CHECK(sync_state());
     CHECK(launch_argmax());
     HIP_OK(hipEventRecord(ev[2], stream));
     CHECK(sync_state());
+    CHECK(select_ready());
     {
         float ms;
         HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1])); ev_count += ms * 1e-3;
@@ -383,6 +499,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         CHECK(launch_argmax());
         HIP_OK(hipEventRecord(ev[3], stream));
         CHECK(sync_state());
+        CHECK(select_ready());
         {
             float ms;
             HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1])); ev_count += ms * 1e-3;
@@ -502,7 +619,9 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
     n_live -= h_st->total_occ;
     HIP_OK(hipMemsetAsync(&d_st->total_occ, 0, 4, stream));
     CHECK(compact());
-    if (n_live) HIP_OK(hipMemcpy(out, d_tok[cur], (size_t)n_live * 2, hipMemcpyDeviceToHost));
+    // the engine stream is non-blocking: copy on it (a null-stream hipMemcpy would not wait for compact())
+    if (n_live) HIP_OK(hipMemcpyAsync(out, d_tok[cur], (size_t)n_live * 2, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
     *out_len = (size_t)n_live;
     return ZBPE_OK;
 }

@@ -51,6 +51,15 @@ struct Engine {
     size_t gather_cap = 0;
     uint32_t *d_recount = nullptr;
     size_t recount_cap = 0;
+    uint32_t *d_count_hist = nullptr, *h_count_hist = nullptr;
+    size_t hot_cap_alloc = 0;
+    size_t home_words_cap = 0;
+    uint64_t home_slots = 0;    // Zig capacity the home histogram is kept for (0: none)
+    Summ *d_summ = nullptr;
+    size_t summ_cap = 0;
+    bool hot_stale = true;
+    uint64_t hot_target = 1u << 16;  // ids the hot list aims to hold after a rebuild
+    uint64_t hot_rebuilds = 0, home_rebuilds = 0;
     hipEvent_t ev[6] = {};
 
     // policy knobs
@@ -82,6 +91,9 @@ struct Engine {
     zbpe_status alloc_stream(size_t n);
     zbpe_status compact();
     zbpe_status launch_argmax();
+    zbpe_status rebuild_hot();
+    zbpe_status rebuild_home(uint64_t cap);
+    zbpe_status select_ready();
     zbpe_status resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner);
 };
 

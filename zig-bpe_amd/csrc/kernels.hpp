@@ -55,6 +55,10 @@ __device__ inline uint32_t ht_find(const Tables &T, uint32_t key) {
     return NO_ID;
 }
 // Insert a key known to be absent (callers guarantee uniqueness within a launch).
+__device__ inline uint32_t ht_find_count(const Tables &T, uint32_t key) {
+    uint32_t id = ht_find(T, key);
+    return id == NO_ID ? 0 : T.id_cnt[id];
+}
 __device__ inline void ht_insert_new(const Tables &T, uint32_t key, uint32_t id) {
     uint32_t s = fmix32(key) & T.ht_mask;
     for (;;) {
@@ -63,6 +67,26 @@ __device__ inline void ht_insert_new(const Tables &T, uint32_t key, uint32_t id)
         s = (s + 1) & T.ht_mask;
     }
 }
+// Live keys per home slot of the Zig map: kept incrementally once a tie
+// has asked for it, so later ties need no pass over every key.
+__device__ inline void home_add(const Tables &T, DevState *st, uint32_t key, bool add) {
+    if (!T.home_cnt) return;
+    const uint32_t s = (uint32_t)(zig_pair_hash(key) & T.home_mask), sh = 8 * (s & 3);
+    const uint32_t old = add ? atomicAdd(&T.home_cnt[s >> 2], 1u << sh) : atomicSub(&T.home_cnt[s >> 2], 1u << sh);
+    if (((old >> sh) & 0xffu) == (add ? 0xffu : 0u)) atomicOr(&st->error, 16u);
+}
+// Wave-aggregated append: one atomic per wave. Every lane of the wave must call it.
+__device__ inline uint32_t wave_append(uint32_t *counter, bool flag) {
+    const uint64_t m = __ballot(flag);
+    if (!m) return ~0u;
+    const uint32_t lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    const uint64_t below = m & ((1ull << lane) - 1ull);
+    return flag ? base + (uint32_t)__popcll(below) : ~0u;
+}
 __device__ inline void pair_new(const Tables &T, DevState *st, uint32_t key, uint32_t count) {
     uint32_t id = atomicAdd(&st->num_ids, 1u);
     if (id >= T.id_cap) { atomicOr(&st->error, 1u); return; }
@@ -70,13 +94,21 @@ __device__ inline void pair_new(const Tables &T, DevState *st, uint32_t key, uin
     T.id_cnt[id] = count;
     ht_insert_new(T, key, id);
     atomicAdd(&st->live, 1);
+    home_add(T, st, key, true);
+    if (count >= st->theta) {
+        uint32_t j = atomicAdd(&st->hot_len, 1u);
+        if (j < T.hot_cap) T.hot[j] = id;
+    }
 }
 __device__ inline void pair_dec(const Tables &T, DevState *st, uint32_t key, uint32_t d) {
     uint32_t id = ht_find(T, key);
     if (id == NO_ID) { atomicOr(&st->error, 4u); return; }
     uint32_t old = atomicSub(&T.id_cnt[id], d);
     if (old < d) atomicOr(&st->error, 2u);
-    if (old == d) atomicSub(&st->live, 1);
+    if (old == d) {
+        atomicSub(&st->live, 1);
+        home_add(T, st, key, false);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -208,8 +240,10 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_argmax_partial(const uint
         partial[blockIdx.x] = r;
     }
 }
-__global__ void __launch_bounds__(256) zbpe_argmax_final(const MaxRec *__restrict__ partial, int np,
-                                                         const uint32_t *__restrict__ id_key, DevState *st) {
+// Final reduction + the count of the stream's last pair (it decides whether the Zig map grows once
+// more after its last insertion) so a tie needs no extra round trip.
+__global__ void __launch_bounds__(256) zbpe_argmax_final(const MaxRec *__restrict__ partial, int np, Tables T,
+                                                         const uint16_t *__restrict__ tok, int64_t n, DevState *st) {
     MaxRec r{0, 0, NO_ID};
     for (int i = threadIdx.x; i < np; i += 256) r = max_combine(r, partial[i]);
     r = wave_max(r);
@@ -221,7 +255,14 @@ __global__ void __launch_bounds__(256) zbpe_argmax_final(const MaxRec *__restric
         st->top_count = r.cnt;
         st->tie_count = r.cnt ? r.ties : 0;
         st->top_id = r.id;
-        st->top_key = r.id != NO_ID ? id_key[r.id] : EMPTY_KEY;
+        st->top_key = r.id != NO_ID ? T.id_key[r.id] : EMPTY_KEY;
+        if (r.ties > 1) {
+            int64_t j = n - 1;
+            while (j >= 0 && tok[j] == HOLE) j--;
+            int64_t i = j - 1;
+            while (i >= 0 && tok[i] == HOLE) i--;
+            st->lastpair_count = i >= 0 ? ht_find_count(T, pair_key(tok[i], tok[j])) : 0;
+        }
     }
 }
 
@@ -467,7 +508,10 @@ __global__ void __launch_bounds__(256) zbpe_update(Tables T, DevState *st, uint3
         if (top_id == NO_ID) { atomicOr(&st->error, 4u); return; }
         uint32_t old = atomicSub(&T.id_cnt[top_id], occ);
         if (old < occ) atomicOr(&st->error, 2u);
-        if (old == occ) atomicSub(&st->live, 1);
+        if (old == occ) {
+            atomicSub(&st->live, 1);
+            home_add(T, st, top_key, false);
+        }
     }
 }
 
@@ -698,79 +742,221 @@ __global__ void zbpe_fill_u16(uint16_t *p, int64_t beg, int64_t end, uint16_t v)
 // holds their home; the tied key with the smallest home wins unless the second-smallest home is
 // in the same run or a tied key could have wrapped past slot C_f-1 (then: exact emulation).
 // ------------------------------------------------------------------------------------------
-__global__ void zbpe_lastpair(const uint16_t *tok, int64_t n, Tables T, DevState *st) {
-    if (threadIdx.x || blockIdx.x) return;
-    int64_t j = n - 1;
-    while (j >= 0 && tok[j] == HOLE) j--;
-    int64_t i = j - 1;
-    while (i >= 0 && tok[i] == HOLE) i--;
-    uint32_t c = 0;
-    if (i >= 0) {
-        uint32_t id = ht_find(T, pair_key(tok[i], tok[j]));
-        c = id == NO_ID ? 0 : T.id_cnt[id];
-    }
-    st->lastpair_count = c;
+// ------------------------------------------------------------------------------------------
+// Hot list: argmax over the ids whose count was >= theta when they entered the list. Counts of
+// existing pairs only fall and a new pair's count never exceeds the current top, so every id with
+// count >= theta is in the list; if none of them still has count >= theta the host rebuilds the
+// list with a lower theta (zbpe_count_hist -> choose theta -> zbpe_hot_build).
+// ------------------------------------------------------------------------------------------
+__device__ inline uint32_t count_bin(uint32_t c) {
+    if (c < 64) return c;
+    const uint32_t e = 31 - __clz(c);
+    return 64 + (e - 6) * 32 + ((c >> (e - 5)) & 31);
 }
-__global__ void __launch_bounds__(256) zbpe_tie_occupy(Tables T, DevState *st, uint32_t cap_mask, uint32_t top,
-                                                       uint32_t *__restrict__ bitmap, uint64_t *__restrict__ tie_list,
-                                                       uint32_t tie_cap) {
+__global__ void __launch_bounds__(256) zbpe_count_hist(Tables T, const DevState *st, uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[COUNT_BINS];
+    for (int i = threadIdx.x; i < COUNT_BINS; i += 256) h[i] = 0;
+    __syncthreads();
     const uint32_t n = min(st->num_ids, T.id_cap);
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        uint32_t c = T.id_cnt[i];
-        if (!c) continue;
-        uint32_t key = T.id_key[i];
-        uint32_t h = (uint32_t)(zig_pair_hash(key) & cap_mask), s = h;
-        for (;;) {
-            uint32_t bit = 1u << (s & 31);
-            uint32_t old = atomicOr(&bitmap[s >> 5], bit);
-            if (!(old & bit)) break;
-            s = (s + 1) & cap_mask;
+        const uint32_t c = T.id_cnt[i];
+        if (c) atomicAdd(&h[count_bin(c)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < COUNT_BINS; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+__global__ void __launch_bounds__(256) zbpe_hot_build(Tables T, DevState *st) {
+    const uint32_t n = min(st->num_ids, T.id_cap), theta = st->theta;
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~63u); i0 < n; i0 += stride) {  // wave-uniform trip count
+        const uint32_t i = i0 + (threadIdx.x & 63);
+        const bool take = i < n && T.id_cnt[i] >= theta;
+        const uint32_t j = wave_append(&st->hot_len, take);
+        if (take && j < T.hot_cap) T.hot[j] = i;
+    }
+}
+__global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_argmax_hot(Tables T, const DevState *st, MaxRec *__restrict__ partial) {
+    const uint32_t n = min(st->hot_len, T.hot_cap), theta = st->theta;
+    MaxRec r{0, 0, NO_ID};
+    for (uint32_t i = blockIdx.x * ARGMAX_THREADS + threadIdx.x; i < n; i += gridDim.x * ARGMAX_THREADS) {
+        const uint32_t id = T.hot[i], c = T.id_cnt[id];
+        if (c >= theta && c) r = max_combine(r, MaxRec{c, 1u, id});
+    }
+    r = wave_max(r);
+    __shared__ MaxRec sm[ARGMAX_THREADS / WAVE];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = r;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < ARGMAX_THREADS / WAVE; w++) r = max_combine(r, sm[w]);
+        partial[blockIdx.x] = r;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Zig-order tie-break. The Zig map of this merge has capacity C; its set of
+// occupied slots depends only on the multiset of home slots hash & (C-1) of the live pairs, kept
+// in T.home_cnt. Scanning slots in order, the carry c (keys displaced past slot s) obeys
+// c(s+1) = max(0, c(s) + cnt[s] - 1), and slot s is occupied iff c(s) + cnt[s] >= 1. A run of
+// slots acts on the carry as c -> max(m, c + q); runs compose associatively, so the carry into any
+// slot is one ordered reduction over the other C-1 slots. The tied pair with the smallest home
+// wins unless the second-smallest home lies in the same occupied run, or a tied pair sits in a
+// run that wraps past slot C-1 (both rare): then the exact first-occurrence emulation decides.
+// ------------------------------------------------------------------------------------------
+__device__ inline Summ summ_cat(Summ a, Summ b) { return Summ{a.q + b.q, max(b.m, a.m + b.q)}; }
+__device__ inline Summ summ_slot(uint32_t k) {
+    const int64_t q = (int64_t)k - 1;
+    return Summ{q, q > 0 ? q : 0};
+}
+__device__ inline uint32_t home_at(const uint32_t *hc, uint32_t s) { return (hc[s >> 2] >> (8 * (s & 3))) & 0xffu; }
+
+__global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, uint32_t top, uint32_t cap_mask,
+                                                        uint64_t *__restrict__ tie_list, uint32_t tie_cap) {
+    const uint32_t n = min(st->hot_len, T.hot_cap);
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
+        const uint32_t i = i0 + (threadIdx.x & 63);
+        uint32_t id = NO_ID;
+        bool tied = false;
+        if (i < n) {
+            id = T.hot[i];
+            tied = T.id_cnt[id] == top;
         }
-        if (c == top) {
-            uint32_t j = atomicAdd(&st->tie_len, 1u);
-            if (j < tie_cap) tie_list[j] = ((uint64_t)h << 32) | key;
+        const uint32_t j = wave_append(&st->tie_len, tied);
+        if (tied && j < tie_cap) {
+            const uint32_t key = T.id_key[id];
+            tie_list[j] = ((uint64_t)(zig_pair_hash(key) & cap_mask) << 32) | key;
         }
     }
 }
-__device__ inline bool occ_bit(const uint32_t *bm, uint32_t s) { return (bm[s >> 5] >> (s & 31)) & 1u; }
-__global__ void __launch_bounds__(256) zbpe_tie_resolve(DevState *st, const uint64_t *__restrict__ tie_list, uint32_t tie_cap,
-                                                        const uint32_t *__restrict__ bitmap, uint32_t cap_mask) {
+// block summaries of the home histogram: block b covers slots [b*SUMM_SLOTS, ...)
+__global__ void __launch_bounds__(256) zbpe_home_summary(const uint32_t *__restrict__ hc, uint32_t nslots, Summ *__restrict__ out) {
+    constexpr int PER = SUMM_SLOTS / 256;  // 64 slots = 16 words per thread
+    const uint32_t beg = blockIdx.x * SUMM_SLOTS + threadIdx.x * PER;
+    Summ acc{0, 0};
+    if (beg < nslots) {
+        const uint32_t end = min(nslots, beg + PER);
+        for (uint32_t w = beg; w < end; w += 4) {
+            const uint32_t word = hc[w >> 2];
+            for (int k = 0; k < 4 && w + k < end; k++) acc = summ_cat(acc, summ_slot((word >> (8 * k)) & 0xffu));
+        }
+    }
+    __shared__ Summ sm[256];
+    sm[threadIdx.x] = acc;
+    __syncthreads();
+    for (int st = 1; st < 256; st <<= 1) {
+        if ((threadIdx.x & (2 * st - 1)) == 0) sm[threadIdx.x] = summ_cat(sm[threadIdx.x], sm[threadIdx.x + st]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = sm[0];
+}
+constexpr int DECIDE_THREADS = 1024;
+// ordered block-wide composition over raw slots [lo, hi) (no wrap)
+__device__ Summ block_compose_slots(const uint32_t *hc, uint32_t lo, uint32_t hi, Summ *sm) {
+    Summ acc{0, 0};
+    if (hi > lo) {
+        const uint32_t len = hi - lo, per = (len + DECIDE_THREADS - 1) / DECIDE_THREADS;
+        const uint32_t b = lo + threadIdx.x * per, e = min(hi, b + per);
+        for (uint32_t s = b; s < e; s++) acc = summ_cat(acc, summ_slot(home_at(hc, s)));
+    }
+    sm[threadIdx.x] = acc;
+    __syncthreads();
+    for (int st = 1; st < DECIDE_THREADS; st <<= 1) {
+        if ((threadIdx.x & (2 * st - 1)) == 0) sm[threadIdx.x] = summ_cat(sm[threadIdx.x], sm[threadIdx.x + st]);
+        __syncthreads();
+    }
+    Summ r = sm[0];
+    __syncthreads();
+    return r;
+}
+__device__ Summ block_compose_blocks(const Summ *summ, uint32_t b0, uint32_t b1, Summ *sm) {
+    Summ acc{0, 0};
+    if (b1 > b0) {
+        const uint32_t len = b1 - b0, per = (len + DECIDE_THREADS - 1) / DECIDE_THREADS;
+        const uint32_t b = b0 + threadIdx.x * per, e = min(b1, b + per);
+        for (uint32_t i = b; i < e; i++) acc = summ_cat(acc, summ[i]);
+    }
+    sm[threadIdx.x] = acc;
+    __syncthreads();
+    for (int st = 1; st < DECIDE_THREADS; st <<= 1) {
+        if ((threadIdx.x & (2 * st - 1)) == 0) sm[threadIdx.x] = summ_cat(sm[threadIdx.x], sm[threadIdx.x + st]);
+        __syncthreads();
+    }
+    Summ r = sm[0];
+    __syncthreads();
+    return r;
+}
+// carry into slot s = m of the composition over slots s+1 .. s-1 (circular)
+__device__ int64_t block_carry_into(const uint32_t *hc, const Summ *summ, uint32_t C, uint32_t s, Summ *sm) {
+    const uint32_t nb = (C + SUMM_SLOTS - 1) / SUMM_SLOTS, b = s / SUMM_SLOTS;
+    Summ a = block_compose_slots(hc, s + 1, min(C, (b + 1) * SUMM_SLOTS), sm);
+    Summ x = block_compose_blocks(summ, b + 1, nb, sm);
+    Summ y = block_compose_blocks(summ, 0, b, sm);
+    Summ z = block_compose_slots(hc, b * SUMM_SLOTS, s, sm);
+    return summ_cat(summ_cat(summ_cat(a, x), y), z).m;
+}
+__global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, const uint64_t *__restrict__ tie_list,
+                                                                  uint32_t tie_cap, const uint32_t *__restrict__ hc,
+                                                                  const Summ *__restrict__ summ, uint32_t C) {
+    __shared__ Summ sm[DECIDE_THREADS];
+    __shared__ uint64_t s1[DECIDE_THREADS], s2[DECIDE_THREADS];
+    __shared__ uint32_t sh[DECIDE_THREADS];
     const uint32_t len = min(st->tie_len, tie_cap);
-    // smallest (home, key), second smallest home, largest home
     uint64_t m1 = ~0ull, m2 = ~0ull;
     uint32_t hmax = 0;
-    for (uint32_t i = threadIdx.x; i < len; i += 256) {
-        uint64_t e = tie_list[i];
+    for (uint32_t i = threadIdx.x; i < len; i += DECIDE_THREADS) {
+        const uint64_t e = tie_list[i];
         if (e < m1) { m2 = m1; m1 = e; } else if (e < m2) m2 = e;
         hmax = max(hmax, (uint32_t)(e >> 32));
     }
-    __shared__ uint64_t s1[256], s2[256];
-    __shared__ uint32_t sh[256];
     s1[threadIdx.x] = m1; s2[threadIdx.x] = m2; sh[threadIdx.x] = hmax;
     __syncthreads();
-    if (threadIdx.x) return;
-    for (int t = 1; t < 256; t++) {  // second smallest of {m1, m2, s1[t], s2[t]}
-        const uint64_t b1 = s1[t], b2 = s2[t];
-        m2 = min(max(m1, b1), min(m2, b2));
-        m1 = min(m1, b1);
-        hmax = max(hmax, sh[t]);
+    for (int stp = 1; stp < DECIDE_THREADS; stp <<= 1) {
+        if ((threadIdx.x & (2 * stp - 1)) == 0) {
+            const uint64_t a1 = s1[threadIdx.x], a2 = s2[threadIdx.x], b1 = s1[threadIdx.x + stp], b2 = s2[threadIdx.x + stp];
+            s1[threadIdx.x] = min(a1, b1);
+            s2[threadIdx.x] = min(max(a1, b1), min(a2, b2));
+            sh[threadIdx.x] = max(sh[threadIdx.x], sh[threadIdx.x + stp]);
+        }
+        __syncthreads();
     }
-    const uint32_t cap = cap_mask + 1;
+    m1 = s1[0]; m2 = s2[0]; hmax = sh[0];
+    __syncthreads();
     const uint32_t h1 = (uint32_t)(m1 >> 32);
-    uint32_t verdict = 0;
-    if (st->tie_len > tie_cap) verdict = 1;
+    const int64_t c1 = block_carry_into(hc, summ, C, h1, sm);
+    const int64_t c0 = block_carry_into(hc, summ, C, 0, sm);
+    const uint32_t W = min(C, 65536u), ws = C - W;
+    const int64_t cw = (c0 > 0 && ws > 0) ? block_carry_into(hc, summ, C, ws, sm) : 0;
+    if (threadIdx.x) return;
+    uint32_t verdict = st->tie_len > tie_cap ? 1u : 0u;
     // first free slot at or after h1
-    uint32_t f = h1;
-    while (f < cap && occ_bit(bitmap, f)) f++;
-    if (f == cap) verdict = 1;  // h1's run reaches the wrap
-    if (m2 != ~0ull && f > (uint32_t)(m2 >> 32)) verdict = 1;  // second tied key in the same run
-    if (occ_bit(bitmap, cap - 1) && occ_bit(bitmap, 0)) {
-        uint32_t sw = cap - 1;
-        while (sw > 0 && occ_bit(bitmap, sw - 1)) sw--;
-        if (hmax >= sw) verdict = 1;  // a tied key in the wrapping run
+    int64_t c = c1;
+    uint32_t s = h1;
+    for (;; s++) {
+        if (s >= C) { verdict = 1; break; }  // the run of h1 wraps
+        const int64_t k = home_at(hc, s);
+        if (c + k == 0) break;
+        c = c + k - 1;
+    }
+    if (m2 != ~0ull && s > (uint32_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
+    if (c0 > 0) {  // a run wraps past C-1: find where it starts
+        int64_t cc = ws > 0 ? cw : c0;
+        int64_t last_free = -1;
+        for (uint32_t t = ws; t < C; t++) {
+            const int64_t k = home_at(hc, t);
+            if (cc + k == 0) last_free = t;
+            else cc = cc + k - 1;
+        }
+        if (last_free < 0 || (int64_t)hmax >= last_free + 1) verdict = 1;
     }
     st->tie_verdict = verdict;
     st->tie_winner = (uint32_t)m1;
+}
+// rebuild the home histogram for a new Zig capacity
+__global__ void __launch_bounds__(256) zbpe_home_build(Tables T, DevState *st) {
+    const uint32_t n = min(st->num_ids, T.id_cap);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+        if (T.id_cnt[i]) home_add(T, st, T.id_key[i], true);
 }
 
 // exact fallback: first occurrence position of every live pair in the current stream

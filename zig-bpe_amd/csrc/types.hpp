@@ -37,6 +37,8 @@ struct DevState {
     uint32_t mismatches;
     uint32_t last_occ;       // occurrences merged by the last merge (copied by zbpe_reset_merge)
     uint32_t total_occ;      // running sum of last_occ (encode bookkeeping)
+    uint32_t theta;          // hot-list threshold: every live id with count >= theta is in the hot list
+    uint32_t hot_len;        // ids appended to the hot list (may exceed its capacity -> rebuild)
     uint32_t pad[2];
 };
 
@@ -47,7 +49,15 @@ struct Tables {
     uint32_t *id_key;   // [id_cap]
     uint32_t *id_cnt;   // [id_cap]
     uint32_t id_cap;
+    uint32_t *hot;      // candidate ids for the argmax (count >= theta when appended)
+    uint32_t hot_cap;
+    uint32_t *home_cnt; // u8 x 4 per word: live keys per home slot of the Zig map (nullptr: not kept)
+    uint32_t home_mask; // Zig map capacity - 1 the histogram is kept for
 };
+
+constexpr int COUNT_BINS = 64 + 26 * 32;  // count histogram for choosing theta: exact < 64, then 32 per octave
+constexpr int SUMM_SLOTS = 16384;         // home-histogram slots per max-plus block summary
+struct Summ { int64_t q, m; };            // carry function c -> max(m, c + q) of a run of slots
 
 struct MaxRec { uint32_t cnt, ties, id; };
 struct LiveRec { uint32_t first_pos, key, count, pad; };
