@@ -56,7 +56,7 @@ void Engine::release() {
     f(T.ht_key); f(T.ht_id); f(T.id_key); f(T.id_cnt);
     f(d_left); f(d_right); f(d_st); f(d_rec); f(d_partial); f(d_hist);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list);
     if (h_st) (void)hipHostFree(h_st);
     if (h_count_hist) (void)hipHostFree(h_count_hist);
     for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -66,6 +66,7 @@ void Engine::release() {
     d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr;
     d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
     d_summ = nullptr; d_count_hist = nullptr; h_count_hist = nullptr; hot_cap_alloc = home_words_cap = 0; home_slots = 0;
+    dirty_list_cap = dirty_bits_cap = 0;
     for (auto &e : ev) e = nullptr;
 }
 
@@ -87,6 +88,11 @@ zbpe_status Engine::init(int dev) {
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
     // the initial byte-pair histogram keeps 128 KiB of bins in LDS
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_count_byte_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4));
+    {
+        int nb = 0;
+        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)zbpe_scan_pairs, SCAN_THREADS, 0));
+        scan_blocks_per_cu = std::max(1, nb);
+    }
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dev));
     num_cus = prop.multiProcessorCount;
@@ -135,6 +141,7 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     while (ht_cap_new < 2 * id_cap_new) ht_cap_new <<= 1;
     Tables N{};
     N.hot = T.hot; N.hot_cap = T.hot_cap; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
+    N.home_dirty = T.home_dirty; N.dirty_list = T.dirty_list;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
     if (hipMalloc(&N.ht_key, ht_cap_new * 4) != hipSuccess || hipMalloc(&N.ht_id, ht_cap_new * 4) != hipSuccess ||
@@ -300,10 +307,19 @@ zbpe_status Engine::rebuild_home(uint64_t cap) {
         }
         home_words_cap = words;
     }
+    const size_t nb = (cap + SUMM_SLOTS - 1) / SUMM_SLOTS;
+    CHECK(ensure(&d_summ, summ_cap, nb, "home summaries"));
+    CHECK(ensure(&T.dirty_list, dirty_list_cap, nb, "home dirty list"));
+    CHECK(ensure(&T.home_dirty, dirty_bits_cap, nb / 32 + 1, "home dirty bits"));
     HIP_OK(hipMemsetAsync(T.home_cnt, 0, words * 4, stream));
+    HIP_OK(hipMemsetAsync(T.home_dirty, 0, (nb / 32 + 1) * 4, stream));
     T.home_mask = (uint32_t)(cap - 1);
     const uint32_t nid = h_st->num_ids;
     zbpe_home_build<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_st);
+    LAUNCH_OK();
+    HIP_OK(hipMemsetAsync(T.home_dirty, 0, (nb / 32 + 1) * 4, stream));
+    HIP_OK(hipMemsetAsync(&d_st->dirty_len, 0, 4, stream));
+    zbpe_home_summary<<<(unsigned)std::min<size_t>(nb, 4096), 256, 0, stream>>>(T, d_st, (uint32_t)cap, (uint32_t)nb, d_summ);
     LAUNCH_OK();
     home_slots = cap;
     home_rebuilds++;
@@ -318,15 +334,13 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     const uint64_t cap = zig_final_capacity(D, call_after);
     if (cap > (1ull << 31)) return fail(ZBPE_INTERNAL, "Zig map capacity %llu out of range", (unsigned long long)cap);
     if (cap != home_slots) CHECK(rebuild_home(cap));
-    const size_t nb = (cap + SUMM_SLOTS - 1) / SUMM_SLOTS;
-    CHECK(ensure(&d_summ, summ_cap, nb, "home summaries"));
     CHECK(ensure(&d_tie_list, tie_list_cap, ties, "tie list"));
     HIP_OK(hipMemsetAsync(&d_st->tie_len, 0, 4, stream));
     const uint32_t hl = std::min<uint32_t>(h_st->hot_len, T.hot_cap);
     zbpe_tie_collect<<<std::min<uint32_t>(1024, hl / 256 + 1), 256, 0, stream>>>(T, d_st, top, (uint32_t)(cap - 1), d_tie_list,
                                                                                   (uint32_t)tie_list_cap);
     LAUNCH_OK();
-    zbpe_home_summary<<<(unsigned)nb, 256, 0, stream>>>(T.home_cnt, (uint32_t)cap, d_summ);
+    zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)cap, 0, d_summ);
     LAUNCH_OK();
     zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, T.home_cnt, d_summ, (uint32_t)cap);
     LAUNCH_OK();
@@ -361,6 +375,13 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     if (h_st->tie_verdict == 0 && *winner != h_st->tie_winner)
         return fail(ZBPE_INTERNAL, "tie fast path chose 0x%08x, exact emulation 0x%08x", h_st->tie_winner, *winner);
     return ZBPE_OK;
+}
+
+// persistent grid: as many blocks as are resident at once, fewer for short streams
+int Engine::scan_grid(int64_t slots) const {
+    const int64_t wave_tiles = (slots / 8 + 64 * SCAN_UNROLL - 1) / (64 * SCAN_UNROLL);
+    const int64_t blocks = (wave_tiles + SCAN_THREADS / 64 - 1) / (SCAN_THREADS / 64);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)num_cus * scan_blocks_per_cu));
 }
 
 zbpe_status Engine::alloc_stream(size_t n) {
@@ -403,6 +424,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     home_slots = 0;
     T.home_mask = 0;
     if (T.home_cnt) { (void)hipFree(T.home_cnt); T.home_cnt = nullptr; home_words_cap = 0; }
+    if (T.home_dirty) { (void)hipFree(T.home_dirty); T.home_dirty = nullptr; dirty_bits_cap = 0; }
+    if (T.dirty_list) { (void)hipFree(T.dirty_list); T.dirty_list = nullptr; dirty_list_cap = 0; }
     hot_stale = true;
     HIP_OK(hipMemsetAsync(d_left, 0, 65536 * 4, stream));
     HIP_OK(hipMemsetAsync(d_right, 0, 65536 * 4, stream));
@@ -469,9 +492,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 1};
         HIP_OK(hipEventRecord(ev[0], stream));
         if (!self) {
-            const int64_t ntiles = (n_slots + SCAN_TILE - 1) / SCAN_TILE;
-            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)num_cus * scan_blocks_per_cu));
-            zbpe_scan_pairs<<<grid, SCAN_THREADS, 0, stream>>>(A);
+            zbpe_scan_pairs<<<scan_grid(n_slots), SCAN_THREADS, 0, stream>>>(A);
             LAUNCH_OK();
             stats.scan_launches++;
         } else {
@@ -490,9 +511,9 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         // ---- replace: apply + count update ---------------------------------------------------------
         zbpe_apply<<<(int)std::min<uint64_t>(2048, top / 256 + 1), 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, d_st, X);
         LAUNCH_OK();
-        zbpe_update<<<(X + 255) / 256, 256, 0, stream>>>(T, d_st, d_left, d_right, a, b, X, key);
+        zbpe_update<<<update_blocks(X), 256, 0, stream>>>(T, d_st, d_left, d_right, a, b, X, key);
         LAUNCH_OK();
-        zbpe_reset_merge<<<1, 1, 0, stream>>>(d_st);
+        zbpe_reset_merge<<<(X + 255) / 256, 256, 0, stream>>>(d_st, d_left, d_right, X);
         LAUNCH_OK();
         HIP_OK(hipEventRecord(ev[2], stream));
         // ---- select for the next merge -------------------------------------------------------------
@@ -588,9 +609,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
         }
         ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 0};
         if (a != b) {
-            const int64_t ntiles = (n_slots + SCAN_TILE - 1) / SCAN_TILE;
-            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)num_cus * scan_blocks_per_cu));
-            zbpe_scan_pairs<<<grid, SCAN_THREADS, 0, stream>>>(A);
+            zbpe_scan_pairs<<<scan_grid(n_slots), SCAN_THREADS, 0, stream>>>(A);
             LAUNCH_OK();
         } else {
             const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);
@@ -605,7 +624,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
         }
         zbpe_apply<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, d_st, X);
         LAUNCH_OK();
-        zbpe_reset_merge<<<1, 1, 0, stream>>>(d_st);
+        zbpe_reset_merge<<<1, 256, 0, stream>>>(d_st, d_left, d_right, 0);
         LAUNCH_OK();
         if ((k & 63) == 63) {
             CHECK(sync_state());

@@ -53,7 +53,7 @@ struct Engine {
     size_t recount_cap = 0;
     uint32_t *d_count_hist = nullptr, *h_count_hist = nullptr;
     size_t hot_cap_alloc = 0;
-    size_t home_words_cap = 0;
+    size_t home_words_cap = 0, dirty_list_cap = 0, dirty_bits_cap = 0;
     uint64_t home_slots = 0;    // Zig capacity the home histogram is kept for (0: none)
     Summ *d_summ = nullptr;
     size_t summ_cap = 0;
@@ -91,6 +91,7 @@ struct Engine {
     zbpe_status alloc_stream(size_t n);
     zbpe_status compact();
     zbpe_status launch_argmax();
+    int scan_grid(int64_t slots) const;
     zbpe_status rebuild_hot();
     zbpe_status rebuild_home(uint64_t cap);
     zbpe_status select_ready();

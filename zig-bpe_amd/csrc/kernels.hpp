@@ -74,6 +74,8 @@ __device__ inline void home_add(const Tables &T, DevState *st, uint32_t key, boo
     const uint32_t s = (uint32_t)(zig_pair_hash(key) & T.home_mask), sh = 8 * (s & 3);
     const uint32_t old = add ? atomicAdd(&T.home_cnt[s >> 2], 1u << sh) : atomicSub(&T.home_cnt[s >> 2], 1u << sh);
     if (((old >> sh) & 0xffu) == (add ? 0xffu : 0u)) atomicOr(&st->error, 16u);
+    const uint32_t blk = s / SUMM_SLOTS, bit = 1u << (blk & 31);
+    if (!(atomicOr(&T.home_dirty[blk >> 5], bit) & bit)) T.dirty_list[atomicAdd(&st->dirty_len, 1u)] = blk;
 }
 // Wave-aggregated append: one atomic per wave. Every lane of the wave must call it.
 __device__ inline uint32_t wave_append(uint32_t *counter, bool flag) {
@@ -360,34 +362,68 @@ __device__ inline uint32_t match8(uint4 v, uint32_t a) {
 //   left[L]  : pair (L, a) destroyed and (L, X) created, unless L ends the previous occurrence
 //   right[R] : pair (b, R) destroyed and (X, R) created, unless R starts the next occurrence
 //   xx       : adjacent occurrences: (b, a) destroyed and (X, X) created
-// plus the occurrence start positions. Each lane holds 8 consecutive tokens (16-B loads); a
-// wave covers 1 KiB contiguous; neighbours across a lane boundary come from DPP/ds shuffles.
+// plus the occurrence start positions.
+// Layout: a wave owns wave-tiles of 64 lanes x SCAN_UNROLL 16-B vectors (2048 tokens, 4 KiB)
+// and grid-strides over them with no block barrier in the loop; lanes hold 8 consecutive tokens,
+// neighbours across lanes come from shuffles. Occurrence starts are staged per wave in LDS and
+// flushed with one global atomic per ~WAVE_REC tokens of records.
 // ------------------------------------------------------------------------------------------
+constexpr int WAVE_REC = 1024;  // LDS record slots per wave
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ inline uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = (uint32_t)__shfl_up((int)x, off);
+        if (lane >= off) x += y;
+    }
+    return x;
+}
+// copy the wave's staged records to the global list (one atomic)
+__device__ inline void wave_flush_records(const ScanArgs &A, const uint32_t *rec, uint32_t n) {
+    const int lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&A.st->rec_count, n);
+    base = (uint32_t)__shfl((int)base, 0);
+    for (uint32_t i = lane; i < n; i += 64)
+        if (base + i < A.rec_cap) A.rec[base + i] = rec[i];
+    if (lane == 0 && base + n > A.rec_cap) atomicOr(&A.st->error, 8u);
+}
+
 __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs(ScanArgs A) {
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
-    __shared__ uint32_t s_rec[SCAN_REC_CAP];
-    __shared__ uint32_t s_nrec, s_base, s_any;
+    __shared__ uint32_t s_rec[SCAN_THREADS / 64][WAVE_REC];
+    __shared__ uint32_t s_any;
     for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
-    if (threadIdx.x == 0) { s_nrec = 0; s_any = 0; }
+    if (threadIdx.x == 0) s_any = 0;
     __syncthreads();
     NeighbourHist H{s_left, s_right, A.left, A.right};
     const uint16_t *tok = A.tok;
     const int64_t n = A.n;
     const int64_t nvec = (n + 7) / 8;
-    const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-    const int lane = threadIdx.x & 63;
-    uint32_t xx = 0;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t vbase = tile * (SCAN_TILE / 8);
+    constexpr int WT_VEC = 64 * SCAN_UNROLL;  // vectors per wave-tile
+    const int64_t nwt = (nvec + WT_VEC - 1) / WT_VEC;
+    const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+    const int64_t wstride = (int64_t)gridDim.x * (SCAN_THREADS / 64);
+    uint32_t *wrec = s_rec[wib];
+    uint32_t nbuf = 0;  // wave-uniform: records staged in wrec
+    uint32_t xx = 0, any = 0;
+    for (int64_t wt = (int64_t)blockIdx.x * (SCAN_THREADS / 64) + wib; wt < nwt; wt += wstride) {
+        const int64_t vbase = wt * WT_VEC;
         uint4 v[SCAN_UNROLL];
 #pragma unroll
         for (int u = 0; u < SCAN_UNROLL; u++) {
-            int64_t vi = vbase + u * SCAN_THREADS + threadIdx.x;
+            const int64_t vi = vbase + u * 64 + lane;
             v[u] = vi < nvec ? reinterpret_cast<const uint4 *>(tok)[vi] : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
         }
+        uint32_t occ = 0;  // bit 8u+k: occurrence starts at token k of vector u
 #pragma unroll
         for (int u = 0; u < SCAN_UNROLL; u++) {
-            const int64_t vi = vbase + u * SCAN_THREADS + threadIdx.x;
+            const int64_t vi = vbase + u * 64 + lane;
             uint32_t m = match8(v[u], A.a);
             if (__ballot(m != 0) == 0) continue;  // wave-uniform: no `a` in this KiB
             // neighbours: next vector's first 4 tokens, previous vector's last 2 tokens
@@ -431,33 +467,38 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs(ScanArgs A) {
                     } else {
                         hit = occ_slow(A, H, p, xx);
                     }
-                    if (hit) {
-                        uint32_t slot = atomicAdd(&s_nrec, 1u);
-                        s_rec[slot] = (uint32_t)p;
-                    }
+                    if (hit) occ |= 1u << (8 * u + k);
                 }
             }
         }
-        __syncthreads();
-        const uint32_t nrec = s_nrec;
-        if (nrec) {
-            if (threadIdx.x == 0) {
-                s_base = atomicAdd(&A.st->rec_count, nrec);
-                s_any = 1;
-            }
-            __syncthreads();
-            const uint32_t base = s_base;
-            for (uint32_t i = threadIdx.x; i < nrec; i += SCAN_THREADS)
-                if (base + i < A.rec_cap) A.rec[base + i] = s_rec[i];
-            if (threadIdx.x == 0 && base + nrec > A.rec_cap) atomicOr(&A.st->error, 8u);
-            __syncthreads();
-            if (threadIdx.x == 0) s_nrec = 0;
-            __syncthreads();
+        // stage this wave-tile's occurrence starts (order is irrelevant to zbpe_apply)
+        const uint32_t c = __popc(occ);
+        const uint32_t incl = wave_incl_scan(c);
+        const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+        if (total == 0) continue;
+        any = 1;
+        if (nbuf + total > WAVE_REC) {
+            wave_lds_sync();
+            wave_flush_records(A, wrec, nbuf);
+            nbuf = 0;
+            wave_lds_sync();
         }
+        uint32_t o = nbuf + incl - c;
+        while (occ) {
+            const int bit = __ffs(occ) - 1;
+            occ &= occ - 1;
+            wrec[o++] = (uint32_t)((vbase + (bit >> 3) * 64 + lane) * 8 + (bit & 7));
+        }
+        nbuf += total;
+    }
+    if (nbuf) {
+        wave_lds_sync();
+        wave_flush_records(A, wrec, nbuf);
     }
     // flush LDS neighbour histograms and the xx count
     xx = wave_sum(xx);
     if (lane == 0 && xx) atomicAdd(&A.st->xx, xx);
+    if (lane == 0 && any) s_any = 1;
     __syncthreads();
     if (s_any) {
         for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) {
@@ -480,47 +521,79 @@ __global__ void __launch_bounds__(256) zbpe_apply(uint16_t *tok, int64_t n, cons
     }
 }
 
-// count update after merge X = (a, b): one thread per neighbour token t < X.
-__global__ void __launch_bounds__(256) zbpe_update(Tables T, DevState *st, uint32_t *left, uint32_t *right, uint32_t a,
-                                                   uint32_t b, uint32_t X, uint32_t top_key) {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t < X) {
-        uint32_t l = left[t];
-        if (l) {
-            left[t] = 0;
-            pair_dec(T, st, pair_key(t, a), l);
-            pair_new(T, st, pair_key(t, X), l);
+// Count update after merge X = (a, b). Four independent chains per neighbour token t < X so
+// each thread waits on one hash-table walk: group 0 decrements (t, a) by left[t], group 1 creates
+// (t, X) = left[t], group 2 decrements (b, t) by right[t], group 3 creates (X, t) = right[t];
+// one extra thread handles (b, a) -> (X, X) and the merged pair itself. Groups are padded to whole
+// waves so the wave-aggregated id / hot-list appends see uniform control flow.
+__global__ void __launch_bounds__(256) zbpe_update(Tables T, DevState *st, const uint32_t *__restrict__ left,
+                                                   const uint32_t *__restrict__ right, uint32_t a, uint32_t b, uint32_t X,
+                                                   uint32_t top_key) {
+    const uint32_t nX = (X + 63) & ~63u;
+    const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t g = gid / nX, t = gid - g * nX;
+    int live_delta = 0;
+    if (g == 0 || g == 2) {
+        const uint32_t c = t < X ? (g == 0 ? left[t] : right[t]) : 0;
+        if (c) {
+            const uint32_t key = g == 0 ? pair_key(t, a) : pair_key(b, t);
+            const uint32_t id = ht_find(T, key);
+            if (id == NO_ID) atomicOr(&st->error, 4u);
+            else {
+                const uint32_t old = atomicSub(&T.id_cnt[id], c);
+                if (old < c) atomicOr(&st->error, 2u);
+                if (old == c) { live_delta--; home_add(T, st, key, false); }
+            }
         }
-        uint32_t r = right[t];
-        if (r) {
-            right[t] = 0;
-            pair_dec(T, st, pair_key(b, t), r);
-            pair_new(T, st, pair_key(X, t), r);
+    } else if (g == 1 || g == 3) {
+        const uint32_t c = t < X ? (g == 1 ? left[t] : right[t]) : 0;
+        const uint32_t id = wave_append(&st->num_ids, c != 0);
+        const bool ok = c != 0 && id < T.id_cap;
+        if (c != 0 && !ok) atomicOr(&st->error, 1u);
+        const uint32_t key = g == 1 ? pair_key(t, X) : pair_key(X, t);
+        if (ok) {
+            T.id_key[id] = key;
+            T.id_cnt[id] = c;
+            ht_insert_new(T, key, id);
+            home_add(T, st, key, true);
+            live_delta++;
         }
-    }
-    if (t == 0) {
+        const bool hot = ok && c >= st->theta;
+        const uint32_t j = wave_append(&st->hot_len, hot);
+        if (hot && j < T.hot_cap) T.hot[j] = id;
+    } else if (gid == 4 * nX) {
         const uint32_t occ = st->rec_count, xx = st->xx;
         if (xx) {
             pair_dec(T, st, pair_key(b, a), xx);
             pair_new(T, st, pair_key(X, X), xx);
         }
         const uint32_t top_id = ht_find(T, top_key);
-        if (top_id == NO_ID) { atomicOr(&st->error, 4u); return; }
-        uint32_t old = atomicSub(&T.id_cnt[top_id], occ);
-        if (old < occ) atomicOr(&st->error, 2u);
-        if (old == occ) {
-            atomicSub(&st->live, 1);
-            home_add(T, st, top_key, false);
+        if (top_id == NO_ID) atomicOr(&st->error, 4u);
+        else {
+            const uint32_t old = atomicSub(&T.id_cnt[top_id], occ);
+            if (old < occ) atomicOr(&st->error, 2u);
+            if (old == occ) { live_delta--; home_add(T, st, top_key, false); }
         }
     }
+    if (g < 4) {
+        const uint32_t sum = wave_sum((uint32_t)live_delta);
+        if ((threadIdx.x & 63) == 0 && sum) atomicAdd((uint32_t *)&st->live, sum);
+    } else if (live_delta) {
+        atomicAdd(&st->live, live_delta);
+    }
 }
+__host__ __device__ inline uint32_t update_blocks(uint32_t X) { return (4 * ((X + 63) & ~63u) + 64 + 255) / 256; }
 
-// zeroes the per-merge scratch counters (kept separate so the update kernel can read them)
-__global__ void zbpe_reset_merge(DevState *st) {
-    st->last_occ = st->rec_count;
-    st->total_occ += st->rec_count;
-    st->rec_count = 0;
-    st->xx = 0;
+// end of merge: clear the neighbour histograms [0, X) and roll the per-merge counters
+__global__ void __launch_bounds__(256) zbpe_reset_merge(DevState *st, uint32_t *left, uint32_t *right, uint32_t X) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t < X) { left[t] = 0; right[t] = 0; }
+    if (t == 0) {
+        st->last_occ = st->rec_count;
+        st->total_occ += st->rec_count;
+        st->rec_count = 0;
+        st->xx = 0;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -829,26 +902,36 @@ __global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, 
         }
     }
 }
-// block summaries of the home histogram: block b covers slots [b*SUMM_SLOTS, ...)
-__global__ void __launch_bounds__(256) zbpe_home_summary(const uint32_t *__restrict__ hc, uint32_t nslots, Summ *__restrict__ out) {
-    constexpr int PER = SUMM_SLOTS / 256;  // 64 slots = 16 words per thread
-    const uint32_t beg = blockIdx.x * SUMM_SLOTS + threadIdx.x * PER;
-    Summ acc{0, 0};
-    if (beg < nslots) {
-        const uint32_t end = min(nslots, beg + PER);
-        for (uint32_t w = beg; w < end; w += 4) {
-            const uint32_t word = hc[w >> 2];
-            for (int k = 0; k < 4 && w + k < end; k++) acc = summ_cat(acc, summ_slot((word >> (8 * k)) & 0xffu));
-        }
-    }
+// block summaries of the home histogram (block b covers slots [b*SUMM_SLOTS, ...)): every block
+// when all_nb > 0 (after a rebuild), otherwise only the blocks listed dirty since the last tie
+__global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st, uint32_t nslots, uint32_t all_nb,
+                                                         Summ *__restrict__ out) {
+    constexpr int PER = SUMM_SLOTS / 256;  // 16 slots = 4 words per thread
     __shared__ Summ sm[256];
-    sm[threadIdx.x] = acc;
-    __syncthreads();
-    for (int st = 1; st < 256; st <<= 1) {
-        if ((threadIdx.x & (2 * st - 1)) == 0) sm[threadIdx.x] = summ_cat(sm[threadIdx.x], sm[threadIdx.x + st]);
+    const uint32_t nwork = all_nb ? all_nb : st->dirty_len;
+    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+        const uint32_t blk = all_nb ? w : T.dirty_list[w];
+        const uint32_t beg = blk * SUMM_SLOTS + threadIdx.x * PER;
+        Summ acc{0, 0};
+        if (beg < nslots) {
+            const uint32_t end = min(nslots, beg + PER);
+            for (uint32_t s = beg; s < end; s += 4) {
+                const uint32_t word = T.home_cnt[s >> 2];
+                for (int k = 0; k < 4 && s + k < end; k++) acc = summ_cat(acc, summ_slot((word >> (8 * k)) & 0xffu));
+            }
+        }
+        sm[threadIdx.x] = acc;
+        __syncthreads();
+        for (int sp = 1; sp < 256; sp <<= 1) {
+            if ((threadIdx.x & (2 * sp - 1)) == 0) sm[threadIdx.x] = summ_cat(sm[threadIdx.x], sm[threadIdx.x + sp]);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            out[blk] = sm[0];
+            atomicAnd(&T.home_dirty[blk >> 5], ~(1u << (blk & 31)));
+        }
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[blockIdx.x] = sm[0];
 }
 constexpr int DECIDE_THREADS = 1024;
 // ordered block-wide composition over raw slots [lo, hi) (no wrap)
@@ -895,6 +978,40 @@ __device__ int64_t block_carry_into(const uint32_t *hc, const Summ *summ, uint32
     Summ z = block_compose_slots(hc, b * SUMM_SLOTS, s, sm);
     return summ_cat(summ_cat(summ_cat(a, x), y), z).m;
 }
+// last free slot in [lo, hi) given the carry into lo (-1 if none): ordered scan of chunk functions
+__device__ int64_t block_last_free(const uint32_t *hc, uint32_t lo, uint32_t hi, int64_t carry_in, Summ *sm) {
+    const uint32_t len = hi - lo, per = (len + DECIDE_THREADS - 1) / DECIDE_THREADS;
+    const uint32_t b = lo + min(len, threadIdx.x * per), e = min(hi, b + per);
+    Summ acc{0, 0};
+    for (uint32_t s = b; s < e; s++) acc = summ_cat(acc, summ_slot(home_at(hc, s)));
+    sm[threadIdx.x] = acc;
+    __syncthreads();
+    for (int sp = 1; sp < DECIDE_THREADS; sp <<= 1) {  // inclusive Hillis-Steele scan of compositions
+        Summ prev = threadIdx.x >= (unsigned)sp ? sm[threadIdx.x - sp] : Summ{0, 0};
+        __syncthreads();
+        if (threadIdx.x >= (unsigned)sp) sm[threadIdx.x] = summ_cat(prev, sm[threadIdx.x]);
+        __syncthreads();
+    }
+    const Summ before = threadIdx.x ? sm[threadIdx.x - 1] : Summ{0, 0};
+    int64_t c = max(before.m, carry_in + before.q);
+    int64_t last = -1;
+    for (uint32_t s = b; s < e; s++) {
+        const int64_t k = home_at(hc, s);
+        if (c + k == 0) last = s;
+        else c = c + k - 1;
+    }
+    __syncthreads();
+    __shared__ long long red[DECIDE_THREADS];
+    red[threadIdx.x] = last;
+    __syncthreads();
+    for (int sp = DECIDE_THREADS / 2; sp > 0; sp >>= 1) {
+        if (threadIdx.x < (unsigned)sp) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + sp]);
+        __syncthreads();
+    }
+    const int64_t r = red[0];
+    __syncthreads();
+    return r;
+}
 __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, const uint64_t *__restrict__ tie_list,
                                                                   uint32_t tie_cap, const uint32_t *__restrict__ hc,
                                                                   const Summ *__restrict__ summ, uint32_t C) {
@@ -925,32 +1042,33 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
     const uint32_t h1 = (uint32_t)(m1 >> 32);
     const int64_t c1 = block_carry_into(hc, summ, C, h1, sm);
     const int64_t c0 = block_carry_into(hc, summ, C, 0, sm);
-    const uint32_t W = min(C, 65536u), ws = C - W;
-    const int64_t cw = (c0 > 0 && ws > 0) ? block_carry_into(hc, summ, C, ws, sm) : 0;
+    // the run wrapping past slot C-1 starts after the last free slot below C: search a growing window
+    int64_t last_free = -2;  // -2: no wrapping run
+    if (c0 > 0) {
+        last_free = -1;
+        for (uint32_t W = 4096; last_free < 0; W *= 16) {
+            const uint32_t ws = W >= C ? 0 : C - W;
+            const int64_t cw = ws > 0 ? block_carry_into(hc, summ, C, ws, sm) : c0;
+            last_free = block_last_free(hc, ws, C, cw, sm);
+            if (ws == 0) break;
+        }
+    }
     if (threadIdx.x) return;
     uint32_t verdict = st->tie_len > tie_cap ? 1u : 0u;
     // first free slot at or after h1
     int64_t c = c1;
     uint32_t s = h1;
     for (;; s++) {
-        if (s >= C) { verdict = 1; break; }  // the run of h1 wraps
+        if (s >= C || s - h1 > (1u << 20)) { verdict = 1; break; }  // the run of h1 wraps (or is absurdly long)
         const int64_t k = home_at(hc, s);
         if (c + k == 0) break;
         c = c + k - 1;
     }
     if (m2 != ~0ull && s > (uint32_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
-    if (c0 > 0) {  // a run wraps past C-1: find where it starts
-        int64_t cc = ws > 0 ? cw : c0;
-        int64_t last_free = -1;
-        for (uint32_t t = ws; t < C; t++) {
-            const int64_t k = home_at(hc, t);
-            if (cc + k == 0) last_free = t;
-            else cc = cc + k - 1;
-        }
-        if (last_free < 0 || (int64_t)hmax >= last_free + 1) verdict = 1;
-    }
+    if (last_free != -2 && (last_free < 0 || (int64_t)hmax >= last_free + 1)) verdict = 1;  // tied pair may wrap
     st->tie_verdict = verdict;
     st->tie_winner = (uint32_t)m1;
+    st->dirty_len = 0;
 }
 // rebuild the home histogram for a new Zig capacity
 __global__ void __launch_bounds__(256) zbpe_home_build(Tables T, DevState *st) {

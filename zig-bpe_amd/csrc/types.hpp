@@ -10,7 +10,7 @@ constexpr uint32_t EMPTY_KEY = 0xFFFFFFFFu;  // (0xFFFF, 0xFFFF) is never a real
 constexpr uint32_t NO_ID = 0xFFFFFFFFu;
 constexpr int WAVE = 64;
 constexpr int SCAN_THREADS = 256;
-constexpr int SCAN_UNROLL = 4;                                       // 16-B vectors per thread per tile
+constexpr int SCAN_UNROLL = 4;                                       // 16-B vectors per lane per wave-tile
 constexpr int SCAN_TILE = SCAN_THREADS * SCAN_UNROLL * 8;            // tokens per tile (8192)
 constexpr int SCAN_REC_CAP = SCAN_TILE / 2;                          // occurrences per tile (non-overlapping)
 constexpr int LDS_BINS = 1024;                                       // neighbour tokens counted in LDS
@@ -39,7 +39,8 @@ struct DevState {
     uint32_t total_occ;      // running sum of last_occ (encode bookkeeping)
     uint32_t theta;          // hot-list threshold: every live id with count >= theta is in the hot list
     uint32_t hot_len;        // ids appended to the hot list (may exceed its capacity -> rebuild)
-    uint32_t pad[2];
+    uint32_t dirty_len;      // home-histogram blocks changed since their summaries were computed
+    uint32_t pad[1];
 };
 
 struct Tables {
@@ -53,10 +54,12 @@ struct Tables {
     uint32_t hot_cap;
     uint32_t *home_cnt; // u8 x 4 per word: live keys per home slot of the Zig map (nullptr: not kept)
     uint32_t home_mask; // Zig map capacity - 1 the histogram is kept for
+    uint32_t *home_dirty;  // 1 bit per SUMM_SLOTS block: summary stale
+    uint32_t *dirty_list;  // stale block indices (each listed once)
 };
 
 constexpr int COUNT_BINS = 64 + 26 * 32;  // count histogram for choosing theta: exact < 64, then 32 per octave
-constexpr int SUMM_SLOTS = 16384;         // home-histogram slots per max-plus block summary
+constexpr int SUMM_SLOTS = 4096;          // home-histogram slots per max-plus block summary
 struct Summ { int64_t q, m; };            // carry function c -> max(m, c + q) of a run of slots
 
 struct MaxRec { uint32_t cnt, ties, id; };
