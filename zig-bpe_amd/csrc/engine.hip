@@ -130,7 +130,7 @@ zbpe_status Engine::sync_state() {
     HIP_OK(hipMemcpyAsync(h_st, d_st, sizeof(DevState), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
     if (h_st->error)
-        return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow)",
+        return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow, 16 home count range, 32 dirty list overflow)",
                     h_st->error);
     return ZBPE_OK;
 }
@@ -141,7 +141,7 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     while (ht_cap_new < 2 * id_cap_new) ht_cap_new <<= 1;
     Tables N{};
     N.hot = T.hot; N.hot_cap = T.hot_cap; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
-    N.home_dirty = T.home_dirty; N.dirty_list = T.dirty_list;
+    N.home_dirty = T.home_dirty; N.dirty_list = T.dirty_list; N.dirty_cap = T.dirty_cap;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
     if (hipMalloc(&N.ht_key, ht_cap_new * 4) != hipSuccess || hipMalloc(&N.ht_id, ht_cap_new * 4) != hipSuccess ||
@@ -311,8 +311,10 @@ zbpe_status Engine::rebuild_home(uint64_t cap) {
     CHECK(ensure(&d_summ, summ_cap, nb, "home summaries"));
     CHECK(ensure(&T.dirty_list, dirty_list_cap, nb, "home dirty list"));
     CHECK(ensure(&T.home_dirty, dirty_bits_cap, nb / 32 + 1, "home dirty bits"));
+    T.dirty_cap = (uint32_t)dirty_list_cap;
     HIP_OK(hipMemsetAsync(T.home_cnt, 0, words * 4, stream));
     HIP_OK(hipMemsetAsync(T.home_dirty, 0, (nb / 32 + 1) * 4, stream));
+    HIP_OK(hipMemsetAsync(&d_st->dirty_len, 0, 4, stream));  // entries of the previous capacity are void
     T.home_mask = (uint32_t)(cap - 1);
     const uint32_t nid = h_st->num_ids;
     zbpe_home_build<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_st);
@@ -425,7 +427,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     T.home_mask = 0;
     if (T.home_cnt) { (void)hipFree(T.home_cnt); T.home_cnt = nullptr; home_words_cap = 0; }
     if (T.home_dirty) { (void)hipFree(T.home_dirty); T.home_dirty = nullptr; dirty_bits_cap = 0; }
-    if (T.dirty_list) { (void)hipFree(T.dirty_list); T.dirty_list = nullptr; dirty_list_cap = 0; }
+    if (T.dirty_list) { (void)hipFree(T.dirty_list); T.dirty_list = nullptr; dirty_list_cap = 0; T.dirty_cap = 0; }
     hot_stale = true;
     HIP_OK(hipMemsetAsync(d_left, 0, 65536 * 4, stream));
     HIP_OK(hipMemsetAsync(d_right, 0, 65536 * 4, stream));
@@ -509,7 +511,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         }
         HIP_OK(hipEventRecord(ev[1], stream));
         // ---- replace: apply + count update ---------------------------------------------------------
-        zbpe_apply<<<(int)std::min<uint64_t>(2048, top / 256 + 1), 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, d_st, X);
+        zbpe_apply<<<(int)std::min<uint64_t>(2048, top / 256 + 1), 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, d_st, X);
         LAUNCH_OK();
         zbpe_update<<<update_blocks(X), 256, 0, stream>>>(T, d_st, d_left, d_right, a, b, X, key);
         LAUNCH_OK();
@@ -622,7 +624,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
             zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
             LAUNCH_OK();
         }
-        zbpe_apply<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, d_st, X);
+        zbpe_apply<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, d_st, X);
         LAUNCH_OK();
         zbpe_reset_merge<<<1, 256, 0, stream>>>(d_st, d_left, d_right, 0);
         LAUNCH_OK();

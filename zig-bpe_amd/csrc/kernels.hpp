@@ -75,7 +75,11 @@ __device__ inline void home_add(const Tables &T, DevState *st, uint32_t key, boo
     const uint32_t old = add ? atomicAdd(&T.home_cnt[s >> 2], 1u << sh) : atomicSub(&T.home_cnt[s >> 2], 1u << sh);
     if (((old >> sh) & 0xffu) == (add ? 0xffu : 0u)) atomicOr(&st->error, 16u);
     const uint32_t blk = s / SUMM_SLOTS, bit = 1u << (blk & 31);
-    if (!(atomicOr(&T.home_dirty[blk >> 5], bit) & bit)) T.dirty_list[atomicAdd(&st->dirty_len, 1u)] = blk;
+    if (!(atomicOr(&T.home_dirty[blk >> 5], bit) & bit)) {
+        const uint32_t j = atomicAdd(&st->dirty_len, 1u);
+        if (j < T.dirty_cap) T.dirty_list[j] = blk;
+        else atomicOr(&st->error, 32u);
+    }
 }
 // Wave-aggregated append: one atomic per wave. Every lane of the wave must call it.
 __device__ inline uint32_t wave_append(uint32_t *counter, bool flag) {
@@ -511,8 +515,8 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs(ScanArgs A) {
 
 // apply: tok[p] = X, next live slot after p (the `b`) becomes a hole. Occurrences are disjoint.
 __global__ void __launch_bounds__(256) zbpe_apply(uint16_t *tok, int64_t n, const uint32_t *__restrict__ rec,
-                                                  const DevState *st, uint32_t X) {
-    const uint32_t cnt = st->rec_count;
+                                                  uint32_t rec_cap, const DevState *st, uint32_t X) {
+    const uint32_t cnt = min(st->rec_count, rec_cap);
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
         int64_t p = rec[i];
         tok[p] = (uint16_t)X;
@@ -908,7 +912,7 @@ __global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st,
                                                          Summ *__restrict__ out) {
     constexpr int PER = SUMM_SLOTS / 256;  // 16 slots = 4 words per thread
     __shared__ Summ sm[256];
-    const uint32_t nwork = all_nb ? all_nb : st->dirty_len;
+    const uint32_t nwork = all_nb ? all_nb : min(st->dirty_len, T.dirty_cap);
     for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
         const uint32_t blk = all_nb ? w : T.dirty_list[w];
         const uint32_t beg = blk * SUMM_SLOTS + threadIdx.x * PER;

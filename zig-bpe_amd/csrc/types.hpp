@@ -56,6 +56,7 @@ struct Tables {
     uint32_t home_mask; // Zig map capacity - 1 the histogram is kept for
     uint32_t *home_dirty;  // 1 bit per SUMM_SLOTS block: summary stale
     uint32_t *dirty_list;  // stale block indices (each listed once)
+    uint32_t dirty_cap;
 };
 
 constexpr int COUNT_BINS = 64 + 26 * 32;  // count histogram for choosing theta: exact < 64, then 32 per octave
