@@ -98,8 +98,14 @@ zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches);
 
 /* Tuning / test options: "debug_checks" (0/1), "exact_ties" (resolve every tie by the exact
  * first-occurrence emulation and cross-check the GPU cluster test), "compact_den" (compact when
- * holes > slots/den), "scan_blocks_per_cu". */
+ * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..4: unroll 4/8, non-temporal
+ * loads; see engine.hip kScanVariants), "hot_target" (ids kept by the argmax hot list). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
+
+/* Benchmark diagnostic: time `reps` launches of the pair-scan kernel for pair (a, b), a != b, over
+ * the stream of the uploaded corpus (zbpe_upload) as it stands; the first launch is not timed.
+ * *gbps = 2 B per stream slot / average launch time. */
+zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, double *avg_ms, double *gbps);
 
 /* Host-only diagnostic (no device work): the Zig 0.13 pair-map iteration order emulation used by
  * the exact tie fallback. Given every live pair's first-occurrence position, key (first |

@@ -90,8 +90,15 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "exact_ties") e.force_exact_ties = value != 0;
     else if (k == "compact_den" && value > 0) e.compact_den = (uint64_t)value;
     else if (k == "scan_blocks_per_cu" && value > 0) e.scan_blocks_per_cu = (int)value;
+    else if (k == "scan_variant") return e.set_scan_variant((int)value);
+    else if (k == "hot_target" && value > 0) e.hot_target = (uint64_t)value;
     else return e.fail(ZBPE_INVALID_ARGUMENT, "unknown option %s", name);
     return ZBPE_OK;
+}
+
+zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, double *avg_ms, double *gbps) {
+    if (!ctx || !avg_ms || !gbps || reps < 1 || a == b) return ZBPE_INVALID_ARGUMENT;
+    return ctx->eng.bench_scan(a, b, reps, avg_ms, gbps);
 }
 
 zbpe_status zbpe_zig_order_winner(const uint32_t *first_pos, const uint32_t *keys, const uint32_t *counts, size_t n,

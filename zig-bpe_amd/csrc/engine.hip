@@ -88,11 +88,7 @@ zbpe_status Engine::init(int dev) {
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
     // the initial byte-pair histogram keeps 128 KiB of bins in LDS
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_count_byte_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4));
-    {
-        int nb = 0;
-        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)zbpe_scan_pairs, SCAN_THREADS, 0));
-        scan_blocks_per_cu = std::max(1, nb);
-    }
+    CHECK(set_scan_variant(0));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dev));
     num_cus = prop.multiProcessorCount;
@@ -379,9 +375,59 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     return ZBPE_OK;
 }
 
+using ScanFn = void (*)(ScanArgs);
+static const ScanFn kScanVariants[] = {zbpe_scan_pairs_t<4, false>, zbpe_scan_pairs_t<8, false>, zbpe_scan_pairs_t<4, true>,
+                                       zbpe_scan_pairs_t<8, true>, zbpe_scan_pairs_t<2, false>};
+static const int kScanUnroll[] = {4, 8, 4, 8, 2};
+
+zbpe_status Engine::set_scan_variant(int v) {
+    if (v < 0 || v >= (int)(sizeof(kScanVariants) / sizeof(kScanVariants[0])))
+        return fail(ZBPE_INVALID_ARGUMENT, "scan variant %d out of range", v);
+    int nb = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)kScanVariants[v], SCAN_THREADS, 0));
+    scan_variant = v;
+    scan_blocks_per_cu = std::max(1, nb);
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::launch_scan(const ScanArgs &A) {
+    hipLaunchKernelGGL(kScanVariants[scan_variant], dim3(scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, A);
+    LAUNCH_OK();
+    return ZBPE_OK;
+}
+
+// scan-kernel microbenchmark on the current stream: `reps` launches for pair (a, b)
+zbpe_status Engine::bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms, double *gbps) {
+    if (!uploaded) return fail(ZBPE_INVALID_ARGUMENT, "no corpus uploaded");
+    HIP_OK(hipSetDevice(device));
+    if (!stream_ready) {
+        CHECK(alloc_stream(n_text));
+        stream_ready = true;
+    }
+    CHECK(ensure(&d_rec, rec_cap, (size_t)n_slots / 2 + 1, "occurrence records"));
+    ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 1};
+    double total = 0;
+    for (int r = 0; r < reps; r++) {
+        HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
+        HIP_OK(hipEventRecord(ev[0], stream));
+        CHECK(launch_scan(A));
+        HIP_OK(hipEventRecord(ev[1], stream));
+        zbpe_reset_merge<<<256, 256, 0, stream>>>(d_st, d_left, d_right, 65536);
+        LAUNCH_OK();
+        HIP_OK(hipEventSynchronize(ev[1]));
+        float ms;
+        HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        if (r) total += ms;  // first launch warms up
+    }
+    *avg_ms = reps > 1 ? total / (reps - 1) : 0;
+    *gbps = *avg_ms > 0 ? 2.0 * (double)n_slots / (*avg_ms * 1e-3) / 1e9 : 0;
+    return ZBPE_OK;
+}
+
 // persistent grid: as many blocks as are resident at once, fewer for short streams
 int Engine::scan_grid(int64_t slots) const {
-    const int64_t wave_tiles = (slots / 8 + 64 * SCAN_UNROLL - 1) / (64 * SCAN_UNROLL);
+    const int unroll = kScanUnroll[scan_variant];
+    const int64_t wave_tiles = (slots / 8 + 64 * unroll - 1) / (64 * unroll);
     const int64_t blocks = (wave_tiles + SCAN_THREADS / 64 - 1) / (SCAN_THREADS / 64);
     return (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)num_cus * scan_blocks_per_cu));
 }
@@ -400,6 +446,7 @@ zbpe_status Engine::alloc_stream(size_t n) {
     }
     n_slots = (int64_t)n;
     n_live = (int64_t)n;
+    stream_ready = false;
     return ZBPE_OK;
 }
 
@@ -494,8 +541,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 1};
         HIP_OK(hipEventRecord(ev[0], stream));
         if (!self) {
-            zbpe_scan_pairs<<<scan_grid(n_slots), SCAN_THREADS, 0, stream>>>(A);
-            LAUNCH_OK();
+            CHECK(launch_scan(A));
             stats.scan_launches++;
         } else {
             stats.self_pair_merges++;
@@ -611,7 +657,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
         }
         ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 0};
         if (a != b) {
-            zbpe_scan_pairs<<<scan_grid(n_slots), SCAN_THREADS, 0, stream>>>(A);
+            CHECK(launch_scan(A));
             LAUNCH_OK();
         } else {
             const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);

@@ -8,6 +8,8 @@
 #include "../../include/zbpe.h"
 #include "types.hpp"
 
+namespace zbpe { struct ScanArgs; }
+
 namespace zbpe {
 
 constexpr int ARGMAX_MAX_BLOCKS = 1024;
@@ -21,7 +23,8 @@ struct Engine {
     // corpus (this rank's shard) and token stream
     uint8_t *d_text = nullptr;
     size_t text_cap = 0, n_text = 0;
-    bool uploaded = false, trained = false;
+    bool uploaded = false, trained = false, stream_ready = false;
+    int scan_variant = 0;
     uint16_t *d_tok[2] = {nullptr, nullptr};
     size_t tok_cap0 = 0, tok_cap1 = 0;
     int cur = 0;
@@ -83,6 +86,8 @@ struct Engine {
     zbpe_status encode(const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n, uint16_t *out,
                        size_t *out_len);
     zbpe_status verify_counts(uint64_t *mismatches);
+    zbpe_status set_scan_variant(int v);
+    zbpe_status bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms, double *gbps);
 
    private:
     zbpe_status sync_state();
@@ -92,6 +97,7 @@ struct Engine {
     zbpe_status compact();
     zbpe_status launch_argmax();
     int scan_grid(int64_t slots) const;
+    zbpe_status launch_scan(const ScanArgs &A);
     zbpe_status rebuild_hot();
     zbpe_status rebuild_home(uint64_t cap);
     zbpe_status select_ready();

@@ -370,9 +370,8 @@ __device__ inline uint32_t match8(uint4 v, uint32_t a) {
 // Layout: a wave owns wave-tiles of 64 lanes x SCAN_UNROLL 16-B vectors (2048 tokens, 4 KiB)
 // and grid-strides over them with no block barrier in the loop; lanes hold 8 consecutive tokens,
 // neighbours across lanes come from shuffles. Occurrence starts are staged per wave in LDS and
-// flushed with one global atomic per ~WAVE_REC tokens of records.
+// flushed with one global atomic per 256*UNROLL records.
 // ------------------------------------------------------------------------------------------
-constexpr int WAVE_REC = 1024;  // LDS record slots per wave
 __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -398,18 +397,66 @@ __device__ inline void wave_flush_records(const ScanArgs &A, const uint32_t *rec
     if (lane == 0 && base + n > A.rec_cap) atomicOr(&A.st->error, 8u);
 }
 
-__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs(ScanArgs A) {
+// occurrences of (a, b) starting in vector vi (8 tokens) whose bits are set in m; returns the hit mask.
+// Window = vectors vi-1, vi, vi+1 re-read from cache (they were just streamed by this wave).
+__device__ inline uint32_t occ_vector(const ScanArgs &A, NeighbourHist &H, int64_t vi, int64_t nvec, uint32_t m,
+                                      uint32_t &xx) {
+    const uint16_t *tok = A.tok;
+    const int64_t n = A.n;
+    const uint4 HOLES = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+    const uint4 pv = vi > 0 ? reinterpret_cast<const uint4 *>(tok)[vi - 1] : HOLES;
+    const uint4 cv = reinterpret_cast<const uint4 *>(tok)[vi];
+    const uint4 nv = vi + 1 < nvec ? reinterpret_cast<const uint4 *>(tok)[vi + 1] : HOLES;
+    // window of 14 tokens tok[p0-2 .. p0+11], p0 = 8*vi, in four u64 (no scratch)
+    const uint64_t W0 = (uint64_t)pv.w | ((uint64_t)cv.x << 32);
+    const uint64_t W1 = (uint64_t)cv.y | ((uint64_t)cv.z << 32);
+    const uint64_t W2 = (uint64_t)cv.w | ((uint64_t)nv.x << 32);
+    const uint64_t W3 = (uint64_t)nv.y;
+    auto win = [&](int i) -> uint32_t {
+        uint64_t q = i < 4 ? W0 : i < 8 ? W1 : i < 12 ? W2 : W3;
+        return (uint32_t)(q >> ((i & 3) * 16)) & 0xffffu;
+    };
+    uint32_t hits = 0;
+    while (m) {
+        const int k = __ffs(m) - 1;
+        m &= m - 1;
+        const int64_t p = vi * 8 + k;
+        const uint32_t t0 = win(k), t1 = win(k + 1), t3 = win(k + 3), t4 = win(k + 4), t5 = win(k + 5);
+        // fast path: tok[p-2 .. p+3] all live and inside the stream
+        const bool fast = p >= 2 && p + 3 < n && t0 != HOLE && t1 != HOLE && t3 != HOLE && t4 != HOLE && t5 != HOLE;
+        int hit;
+        if (fast) {
+            hit = t3 == A.b;
+            if (hit && A.count_deltas) {
+                const bool merged_end = (t1 == A.b) && (t0 == A.a);
+                if (!merged_end) H.left((uint16_t)t1);
+                const bool r_occ = (t4 == A.a) && (t5 == A.b);
+                if (r_occ) xx++;
+                else H.right((uint16_t)t4);
+            }
+        } else {
+            hit = occ_slow(A, H, p, xx);
+        }
+        if (hit) hits |= 1u << k;
+    }
+    return hits;
+}
+
+template <int UNROLL, bool NT>
+__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
+    constexpr int STAGE = 4;                      // vectors per lane per record-staging step
+    constexpr uint32_t WREC = 64 * STAGE * 8 / 2;  // at most one occurrence per 2 tokens
+    static_assert(UNROLL % STAGE == 0 || UNROLL < STAGE, "UNROLL must be a multiple of 4 (or < 4)");
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
-    __shared__ uint32_t s_rec[SCAN_THREADS / 64][WAVE_REC];
+    __shared__ uint32_t s_rec[SCAN_THREADS / 64][WREC];
     __shared__ uint32_t s_any;
     for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
     if (threadIdx.x == 0) s_any = 0;
     __syncthreads();
     NeighbourHist H{s_left, s_right, A.left, A.right};
     const uint16_t *tok = A.tok;
-    const int64_t n = A.n;
-    const int64_t nvec = (n + 7) / 8;
-    constexpr int WT_VEC = 64 * SCAN_UNROLL;  // vectors per wave-tile
+    const int64_t nvec = (A.n + 7) / 8;
+    constexpr int WT_VEC = 64 * UNROLL;  // vectors per wave-tile
     const int64_t nwt = (nvec + WT_VEC - 1) / WT_VEC;
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
     const int64_t wstride = (int64_t)gridDim.x * (SCAN_THREADS / 64);
@@ -418,82 +465,59 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs(ScanArgs A) {
     uint32_t xx = 0, any = 0;
     for (int64_t wt = (int64_t)blockIdx.x * (SCAN_THREADS / 64) + wib; wt < nwt; wt += wstride) {
         const int64_t vbase = wt * WT_VEC;
-        uint4 v[SCAN_UNROLL];
+        // phase 1: stream UNROLL x 16 B per lane, keep only the positions holding `a`
+        uint4 v[UNROLL];
 #pragma unroll
-        for (int u = 0; u < SCAN_UNROLL; u++) {
+        for (int u = 0; u < UNROLL; u++) {
             const int64_t vi = vbase + u * 64 + lane;
-            v[u] = vi < nvec ? reinterpret_cast<const uint4 *>(tok)[vi] : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-        }
-        uint32_t occ = 0;  // bit 8u+k: occurrence starts at token k of vector u
-#pragma unroll
-        for (int u = 0; u < SCAN_UNROLL; u++) {
-            const int64_t vi = vbase + u * 64 + lane;
-            uint32_t m = match8(v[u], A.a);
-            if (__ballot(m != 0) == 0) continue;  // wave-uniform: no `a` in this KiB
-            // neighbours: next vector's first 4 tokens, previous vector's last 2 tokens
-            uint32_t nx = __shfl_down((int)v[u].x, 1), ny = __shfl_down((int)v[u].y, 1);
-            uint32_t pw = __shfl_up((int)v[u].w, 1);
-            if (m) {
-                if (lane == 63) {
-                    if (vi + 1 < nvec) {
-                        uint2 t = reinterpret_cast<const uint2 *>(tok)[2 * (vi + 1)];
-                        nx = t.x; ny = t.y;
-                    } else { nx = 0xffffffffu; ny = 0xffffffffu; }
+            if (vi < nvec) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(tok) + vi;
+                if constexpr (NT) {
+                    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
+                    v[u] = make_uint4(x.x, x.y, x.z, x.w);
+                } else {
+                    v[u] = *src;
                 }
-                if (lane == 0) pw = vi > 0 ? reinterpret_cast<const uint32_t *>(tok)[4 * vi - 1] : 0xffffffffu;
-                // window of 14 tokens tok[p0-2 .. p0+11], p0 = 8*vi, kept in four u64 (no scratch)
-                const uint64_t W0 = (uint64_t)pw | ((uint64_t)v[u].x << 32);
-                const uint64_t W1 = (uint64_t)v[u].y | ((uint64_t)v[u].z << 32);
-                const uint64_t W2 = (uint64_t)v[u].w | ((uint64_t)nx << 32);
-                const uint64_t W3 = (uint64_t)ny;
-                auto win = [&](int i) -> uint32_t {
-                    uint64_t q = i < 4 ? W0 : i < 8 ? W1 : i < 12 ? W2 : W3;
-                    return (uint32_t)(q >> ((i & 3) * 16)) & 0xffffu;
-                };
-                while (m) {
-                    const int k = __ffs(m) - 1;
-                    m &= m - 1;
-                    const int64_t p = vi * 8 + k;
-                    const uint32_t t0 = win(k), t1 = win(k + 1), t3 = win(k + 3), t4 = win(k + 4), t5 = win(k + 5);
-                    // fast path: tok[p-2 .. p+3] all live and inside the stream
-                    const bool fast = p >= 2 && p + 3 < n && t0 != HOLE && t1 != HOLE && t3 != HOLE && t4 != HOLE &&
-                                      t5 != HOLE;
-                    int hit;
-                    if (fast) {
-                        hit = t3 == A.b;
-                        if (hit && A.count_deltas) {
-                            const bool merged_end = (t1 == A.b) && (t0 == A.a);
-                            if (!merged_end) H.left((uint16_t)t1);
-                            const bool r_occ = (t4 == A.a) && (t5 == A.b);
-                            if (r_occ) xx++;
-                            else H.right((uint16_t)t4);
-                        }
-                    } else {
-                        hit = occ_slow(A, H, p, xx);
-                    }
-                    if (hit) occ |= 1u << (8 * u + k);
-                }
+            } else {
+                v[u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
             }
         }
-        // stage this wave-tile's occurrence starts (order is irrelevant to zbpe_apply)
-        const uint32_t c = __popc(occ);
-        const uint32_t incl = wave_incl_scan(c);
-        const uint32_t total = (uint32_t)__shfl((int)incl, 63);
-        if (total == 0) continue;
-        any = 1;
-        if (nbuf + total > WAVE_REC) {
-            wave_lds_sync();
-            wave_flush_records(A, wrec, nbuf);
-            nbuf = 0;
-            wave_lds_sync();
+        uint64_t cand = 0;  // bit 8u+k: token k of vector u is `a`
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) cand |= (uint64_t)match8(v[u], A.a) << (8 * u);
+        if (__ballot(cand != 0) == 0) continue;  // wave-uniform: no `a` in these 64*UNROLL*16 B
+        // phase 2 (lanes with candidates): resolve occurrences, stage them per STAGE vectors
+#pragma unroll
+        for (int ug = 0; ug < UNROLL; ug += STAGE) {
+            uint32_t occ = 0;  // bit 8(u-ug)+k
+            uint64_t c = (cand >> (8 * ug)) & ((STAGE * 8 >= 64) ? ~0ull : ((1ull << (STAGE * 8)) - 1));
+#pragma unroll 1
+            while (c) {
+                const int u = (__ffsll((unsigned long long)c) - 1) >> 3;
+                const uint32_t m = (uint32_t)(c >> (8 * u)) & 0xffu;
+                c &= ~(0xffull << (8 * u));
+                occ |= occ_vector(A, H, vbase + (ug + u) * 64 + lane, nvec, m, xx) << (8 * u);
+            }
+            const uint32_t cnt = __popc(occ);
+            const uint32_t incl = wave_incl_scan(cnt);
+            const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+            if (total == 0) continue;
+            any = 1;
+            if (nbuf + total > WREC) {
+                wave_lds_sync();
+                wave_flush_records(A, wrec, nbuf);
+                nbuf = 0;
+                wave_lds_sync();
+            }
+            uint32_t o = nbuf + incl - cnt;
+            while (occ) {
+                const int bit = __ffs(occ) - 1;
+                occ &= occ - 1;
+                wrec[o++] = (uint32_t)((vbase + (ug + (bit >> 3)) * 64 + lane) * 8 + (bit & 7));
+            }
+            nbuf += total;
         }
-        uint32_t o = nbuf + incl - c;
-        while (occ) {
-            const int bit = __ffs(occ) - 1;
-            occ &= occ - 1;
-            wrec[o++] = (uint32_t)((vbase + (bit >> 3) * 64 + lane) * 8 + (bit & 7));
-        }
-        nbuf += total;
     }
     if (nbuf) {
         wave_lds_sync();
@@ -512,6 +536,9 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs(ScanArgs A) {
         }
     }
 }
+
+// default variant and the alternatives selectable for A/B runs (option "scan_variant")
+#define zbpe_scan_pairs zbpe_scan_pairs_t<SCAN_UNROLL, false>
 
 // apply: tok[p] = X, next live slot after p (the `b`) becomes a hole. Occurrences are disjoint.
 __global__ void __launch_bounds__(256) zbpe_apply(uint16_t *tok, int64_t n, const uint32_t *__restrict__ rec,

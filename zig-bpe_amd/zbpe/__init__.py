@@ -136,7 +136,7 @@ class Stats(ctypes.Structure):
 EXPORTS = (
     "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_destroy", "zbpe_last_error",
     "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts",
-    "zbpe_set_option", "zbpe_zig_order_winner", "zbpe_version",
+    "zbpe_set_option", "zbpe_bench_scan", "zbpe_zig_order_winner", "zbpe_version",
 )
 
 _lib = None
@@ -164,6 +164,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_encode.argtypes = [vp, u16p, sz, vp, sz, u16p, ctypes.POINTER(sz)]
     L.zbpe_verify_counts.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.zbpe_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
+    L.zbpe_bench_scan.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(ctypes.c_double)]
     L.zbpe_zig_order_winner.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
     L.zbpe_version.restype = ctypes.c_char_p
     for name in EXPORTS:
@@ -249,6 +251,11 @@ class Engine:
         self._check(self._L.zbpe_encode(self._ctx, _ptr(tri_p), len(tri) // 3, _ptr(buf), len(text), _ptr(out),
                                         ctypes.byref(n)), "zbpe_encode")
         return out[: n.value].copy()
+
+    def bench_scan(self, a: int, b: int, reps: int = 10):
+        ms, gbps = ctypes.c_double(0), ctypes.c_double(0)
+        self._check(self._L.zbpe_bench_scan(self._ctx, a, b, reps, ctypes.byref(ms), ctypes.byref(gbps)), "zbpe_bench_scan")
+        return ms.value, gbps.value
 
     def verify_counts(self) -> int:
         mm = ctypes.c_uint64(0)
