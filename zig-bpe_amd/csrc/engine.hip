@@ -376,9 +376,11 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
 }
 
 using ScanFn = void (*)(ScanArgs);
-static const ScanFn kScanVariants[] = {zbpe_scan_pairs_t<4, false>, zbpe_scan_pairs_t<8, false>, zbpe_scan_pairs_t<4, true>,
-                                       zbpe_scan_pairs_t<8, true>, zbpe_scan_pairs_t<2, false>};
-static const int kScanUnroll[] = {4, 8, 4, 8, 2};
+// 0 is the default (unroll 4, non-temporal loads, next-token filter); the others for A/B runs
+static const ScanFn kScanVariants[] = {zbpe_scan_pairs_t<4, true, true>,  zbpe_scan_pairs_t<8, true, true>,
+                                       zbpe_scan_pairs_t<4, false, true>, zbpe_scan_pairs_t<4, true, false>,
+                                       zbpe_scan_pairs_t<2, true, true>};
+static const int kScanUnroll[] = {4, 8, 4, 4, 2};
 
 zbpe_status Engine::set_scan_variant(int v) {
     if (v < 0 || v >= (int)(sizeof(kScanVariants) / sizeof(kScanVariants[0])))

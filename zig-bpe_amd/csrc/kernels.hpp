@@ -442,7 +442,7 @@ __device__ inline uint32_t occ_vector(const ScanArgs &A, NeighbourHist &H, int64
     return hits;
 }
 
-template <int UNROLL, bool NT>
+template <int UNROLL, bool NT, bool FILTER>
 __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
     constexpr int STAGE = 4;                      // vectors per lane per record-staging step
     constexpr uint32_t WREC = 64 * STAGE * 8 / 2;  // at most one occurrence per 2 tokens
@@ -487,6 +487,24 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
 #pragma unroll
         for (int u = 0; u < UNROLL; u++) cand |= (uint64_t)match8(v[u], A.a) << (8 * u);
         if (__ballot(cand != 0) == 0) continue;  // wave-uniform: no `a` in these 64*UNROLL*16 B
+        if constexpr (FILTER) {
+            // keep `a` only where the next slot holds `b` or a hole (the next lane's first token via
+            // a shuffle; lane 63 cannot see it and keeps its last candidate for phase 2)
+            uint64_t f = 0;
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++) {
+                const uint32_t nx = (uint32_t)__shfl_down((int)v[u].x, 1) & 0xffffu;
+                uint32_t nb = 0;  // bit k: token k+1 (k < 7) or the next vector's token 0 is b / HOLE
+#pragma unroll
+                for (int k = 0; k < 7; k++) {
+                    const uint32_t t = tok_at(v[u], k + 1);
+                    nb |= (t == A.b || t == HOLE ? 1u : 0u) << k;
+                }
+                nb |= (lane == 63 || nx == A.b || nx == HOLE ? 1u : 0u) << 7;
+                f |= (uint64_t)nb << (8 * u);
+            }
+            cand &= f;
+        }
         // phase 2 (lanes with candidates): resolve occurrences, stage them per STAGE vectors
 #pragma unroll
         for (int ug = 0; ug < UNROLL; ug += STAGE) {
@@ -538,7 +556,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
 }
 
 // default variant and the alternatives selectable for A/B runs (option "scan_variant")
-#define zbpe_scan_pairs zbpe_scan_pairs_t<SCAN_UNROLL, false>
+#define zbpe_scan_pairs zbpe_scan_pairs_t<SCAN_UNROLL, true, true>
 
 // apply: tok[p] = X, next live slot after p (the `b`) becomes a hole. Occurrences are disjoint.
 __global__ void __launch_bounds__(256) zbpe_apply(uint16_t *tok, int64_t n, const uint32_t *__restrict__ rec,
