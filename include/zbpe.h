@@ -99,7 +99,8 @@ zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches);
 /* Tuning / test options: "debug_checks" (0/1), "exact_ties" (resolve every tie by the exact
  * first-occurrence emulation and cross-check the GPU cluster test), "compact_den" (compact when
  * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..4: unroll 4/8, non-temporal
- * loads; see engine.hip kScanVariants), "hot_target" (ids kept by the argmax hot list). */
+ * loads; see engine.hip kScanVariants), "scan_auto" (0/1: per merge, plain loads instead of
+ * non-temporal ones when matches are dense), "hot_target" (ids kept by the argmax hot list). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* Benchmark diagnostic: time `reps` launches of the pair-scan kernel for pair (a, b), a != b, over

@@ -91,6 +91,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "compact_den" && value > 0) e.compact_den = (uint64_t)value;
     else if (k == "scan_blocks_per_cu" && value > 0) e.scan_blocks_per_cu = (int)value;
     else if (k == "scan_variant") return e.set_scan_variant((int)value);
+    else if (k == "scan_auto") e.scan_auto = value != 0;
     else if (k == "hot_target" && value > 0) e.hot_target = (uint64_t)value;
     else return e.fail(ZBPE_INVALID_ARGUMENT, "unknown option %s", name);
     return ZBPE_OK;

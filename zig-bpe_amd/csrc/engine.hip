@@ -392,8 +392,12 @@ zbpe_status Engine::set_scan_variant(int v) {
     return ZBPE_OK;
 }
 
-zbpe_status Engine::launch_scan(const ScanArgs &A) {
-    hipLaunchKernelGGL(kScanVariants[scan_variant], dim3(scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, A);
+zbpe_status Engine::launch_scan(const ScanArgs &A, uint64_t expected_occ) {
+    // default variant: non-temporal loads pay when matches are rare; when they are dense the
+    // phase-2 window re-reads want the lines cached (variant 2: plain loads)
+    int v = scan_variant;
+    if (v == 0 && scan_auto && expected_occ * 64 > (uint64_t)A.n) v = 2;
+    hipLaunchKernelGGL(kScanVariants[v], dim3(scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, A);
     LAUNCH_OK();
     return ZBPE_OK;
 }
@@ -412,7 +416,7 @@ zbpe_status Engine::bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms,
     for (int r = 0; r < reps; r++) {
         HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
         HIP_OK(hipEventRecord(ev[0], stream));
-        CHECK(launch_scan(A));
+        CHECK(launch_scan(A, 0));
         HIP_OK(hipEventRecord(ev[1], stream));
         zbpe_reset_merge<<<256, 256, 0, stream>>>(d_st, d_left, d_right, 65536);
         LAUNCH_OK();
@@ -543,7 +547,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 1};
         HIP_OK(hipEventRecord(ev[0], stream));
         if (!self) {
-            CHECK(launch_scan(A));
+            CHECK(launch_scan(A, top));
             stats.scan_launches++;
         } else {
             stats.self_pair_merges++;
@@ -659,7 +663,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
         }
         ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 0};
         if (a != b) {
-            CHECK(launch_scan(A));
+            CHECK(launch_scan(A, (uint64_t)n_slots / 64));
             LAUNCH_OK();
         } else {
             const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);

@@ -25,6 +25,7 @@ struct Engine {
     size_t text_cap = 0, n_text = 0;
     bool uploaded = false, trained = false, stream_ready = false;
     int scan_variant = 0;
+    bool scan_auto = true;  // pick plain vs non-temporal loads per merge from the expected match density
     uint16_t *d_tok[2] = {nullptr, nullptr};
     size_t tok_cap0 = 0, tok_cap1 = 0;
     int cur = 0;
@@ -97,7 +98,7 @@ struct Engine {
     zbpe_status compact();
     zbpe_status launch_argmax();
     int scan_grid(int64_t slots) const;
-    zbpe_status launch_scan(const ScanArgs &A);
+    zbpe_status launch_scan(const ScanArgs &A, uint64_t expected_occ);
     zbpe_status rebuild_hot();
     zbpe_status rebuild_home(uint64_t cap);
     zbpe_status select_ready();
