@@ -5,7 +5,7 @@
 //   [argmax of the previous update is already on the host]
 //   tie? -> zbpe_tie_occupy, zbpe_tie_resolve (+ exact emulation if undecided)
 //   zbpe_scan_pairs | (compact, zbpe_self_tiles, zbpe_self_carry, zbpe_scan_self) for (a, a)
-//   zbpe_apply, zbpe_update, zbpe_reset_merge, zbpe_argmax_hot/final -> one D2H + sync
+//   zbpe_replace (apply + count update), zbpe_select (argmax + resets) -> one D2H + sync
 #include "engine.hpp"
 
 #include <algorithm>
@@ -53,10 +53,10 @@ Engine::~Engine() { release(); }
 void Engine::release() {
     auto f = [](void *p) { if (p) (void)hipFree(p); };
     f(d_text); f(d_tok[0]); f(d_tok[1]);
-    f(T.ht_key); f(T.ht_id); f(T.id_key); f(T.id_cnt);
+    f(T.ht); f(T.id_key); f(T.id_cnt);
     f(d_left); f(d_right); f(d_st); f(d_rec); f(d_partial); f(d_hist);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list); f(d_sup);
     if (h_st) (void)hipHostFree(h_st);
     if (h_count_hist) (void)hipHostFree(h_count_hist);
     for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -66,7 +66,7 @@ void Engine::release() {
     d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr;
     d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
     d_summ = nullptr; d_count_hist = nullptr; h_count_hist = nullptr; hot_cap_alloc = home_words_cap = 0; home_slots = 0;
-    dirty_list_cap = dirty_bits_cap = 0;
+    dirty_list_cap = dirty_bits_cap = 0; d_sup = nullptr; sup_cap = 0;
     for (auto &e : ev) e = nullptr;
 }
 
@@ -140,20 +140,20 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     N.home_dirty = T.home_dirty; N.dirty_list = T.dirty_list; N.dirty_cap = T.dirty_cap;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
-    if (hipMalloc(&N.ht_key, ht_cap_new * 4) != hipSuccess || hipMalloc(&N.ht_id, ht_cap_new * 4) != hipSuccess ||
-        hipMalloc(&N.id_key, id_cap_new * 4) != hipSuccess || hipMalloc(&N.id_cnt, id_cap_new * 4) != hipSuccess) {
+    if (hipMalloc(&N.ht, ht_cap_new * 8) != hipSuccess || hipMalloc(&N.id_key, id_cap_new * 4) != hipSuccess ||
+        hipMalloc(&N.id_cnt, id_cap_new * 4) != hipSuccess) {
         (void)hipGetLastError();
-        for (void *p : {(void *)N.ht_key, (void *)N.ht_id, (void *)N.id_key, (void *)N.id_cnt}) if (p) (void)hipFree(p);
+        for (void *p : {(void *)N.ht, (void *)N.id_key, (void *)N.id_cnt}) if (p) (void)hipFree(p);
         return fail(ZBPE_OUT_OF_MEMORY, "pair table allocation (%zu ids) failed", id_cap_new);
     }
-    HIP_OK(hipMemsetAsync(N.ht_key, 0xFF, ht_cap_new * 4, stream));
+    HIP_OK(hipMemsetAsync(N.ht, 0xFF, ht_cap_new * 8, stream));
     if (T.id_key) {  // rebuild from the old tables
         uint32_t old_n = h_st->num_ids;
         HIP_OK(hipMemsetAsync(&d_st->num_ids, 0, 4, stream));
         zbpe_rebuild<<<std::min<uint32_t>(2048, (old_n + 255) / 256 + 1), 256, 0, stream>>>(T.id_key, T.id_cnt, old_n, N, d_st);
         LAUNCH_OK();
         HIP_OK(hipStreamSynchronize(stream));
-        (void)hipFree(T.ht_key); (void)hipFree(T.ht_id); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt);
+        (void)hipFree(T.ht); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt);
         stats_rebuilds++;
     }
     T = N;
@@ -245,14 +245,12 @@ zbpe_status Engine::rebuild_hot() {
     return ZBPE_OK;
 }
 
-zbpe_status Engine::launch_argmax() {
+zbpe_status Engine::launch_argmax(uint32_t X, int roll) {
     if (hot_stale) CHECK(rebuild_hot());
-    const uint32_t cap = T.hot_cap;
-    int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, (cap + 4 * ARGMAX_THREADS - 1) / (4 * ARGMAX_THREADS));
+    const uint64_t work = std::max<uint64_t>(T.hot_cap / 4, X);
+    int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, (work + ARGMAX_THREADS - 1) / ARGMAX_THREADS);
     blocks = std::max(blocks, 1);
-    zbpe_argmax_hot<<<blocks, ARGMAX_THREADS, 0, stream>>>(T, d_st, d_partial);
-    LAUNCH_OK();
-    zbpe_argmax_final<<<1, 256, 0, stream>>>(d_partial, blocks, T, d_tok[cur], n_slots, d_st);
+    zbpe_select<<<blocks, ARGMAX_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], n_slots, d_left, d_right, X, roll);
     LAUNCH_OK();
     return ZBPE_OK;
 }
@@ -283,7 +281,7 @@ zbpe_status Engine::select_ready() {
             return ZBPE_OK;
         }
         hot_stale = true;
-        CHECK(launch_argmax());
+        CHECK(launch_argmax(0, 0));
         CHECK(sync_state());
     }
     return fail(ZBPE_INTERNAL, "hot list rebuild did not converge (live %d, hot_len %u, theta %u)", h_st->live, h_st->hot_len,
@@ -305,6 +303,7 @@ zbpe_status Engine::rebuild_home(uint64_t cap) {
     }
     const size_t nb = (cap + SUMM_SLOTS - 1) / SUMM_SLOTS;
     CHECK(ensure(&d_summ, summ_cap, nb, "home summaries"));
+    CHECK(ensure(&d_sup, sup_cap, nb / SUPER_BLOCKS + 1, "home super-block summaries"));
     CHECK(ensure(&T.dirty_list, dirty_list_cap, nb, "home dirty list"));
     CHECK(ensure(&T.home_dirty, dirty_bits_cap, nb / 32 + 1, "home dirty bits"));
     T.dirty_cap = (uint32_t)dirty_list_cap;
@@ -340,7 +339,11 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     LAUNCH_OK();
     zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)cap, 0, d_summ);
     LAUNCH_OK();
-    zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, T.home_cnt, d_summ, (uint32_t)cap);
+    const uint32_t nb = (uint32_t)((cap + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
+    zbpe_super_summary<<<(nsb + 3) / 4, 256, 0, stream>>>(d_summ, nb, d_sup);
+    LAUNCH_OK();
+    HomeView V{T.home_cnt, d_summ, d_sup, (uint32_t)cap, nb, nsb};
+    zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V);
     LAUNCH_OK();
     CHECK(sync_state());
     if (h_st->tie_len != ties)
@@ -470,10 +473,10 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     // ---- generateInitialTokens + initial histogram ------------------------------------------------
     CHECK(alloc_stream(n));
     if (!T.id_key || T.id_cap < (1u << 20)) {
-        if (T.id_key) { (void)hipFree(T.ht_key); (void)hipFree(T.ht_id); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt); T = Tables{}; }
+        if (T.id_key) { (void)hipFree(T.ht); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt); T.ht = nullptr; T.id_key = T.id_cnt = nullptr; }
         CHECK(alloc_tables(1u << 20));
     } else {
-        HIP_OK(hipMemsetAsync(T.ht_key, 0xFF, ((size_t)T.ht_mask + 1) * 4, stream));
+        HIP_OK(hipMemsetAsync(T.ht, 0xFF, ((size_t)T.ht_mask + 1) * 8, stream));
     }
     HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
     home_slots = 0;
@@ -497,7 +500,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     }
     HIP_OK(hipEventRecord(ev[1], stream));
     CHECK(sync_state());
-    CHECK(launch_argmax());
+    CHECK(launch_argmax(0, 0));
     HIP_OK(hipEventRecord(ev[2], stream));
     CHECK(sync_state());
     CHECK(select_ready());
@@ -563,15 +566,15 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         }
         HIP_OK(hipEventRecord(ev[1], stream));
         // ---- replace: apply + count update ---------------------------------------------------------
-        zbpe_apply<<<(int)std::min<uint64_t>(2048, top / 256 + 1), 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, d_st, X);
-        LAUNCH_OK();
-        zbpe_update<<<update_blocks(X), 256, 0, stream>>>(T, d_st, d_left, d_right, a, b, X, key);
-        LAUNCH_OK();
-        zbpe_reset_merge<<<(X + 255) / 256, 256, 0, stream>>>(d_st, d_left, d_right, X);
-        LAUNCH_OK();
+        {
+            const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top / 256 + 1);
+            zbpe_replace<<<ab + update_blocks(X), 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, T, d_st,
+                                                                   d_left, d_right, a, b, X, key, ab);
+            LAUNCH_OK();
+        }
         HIP_OK(hipEventRecord(ev[2], stream));
-        // ---- select for the next merge -------------------------------------------------------------
-        CHECK(launch_argmax());
+        // ---- select for the next merge (also clears the neighbour histograms, rolls the counters) -----
+        CHECK(launch_argmax(X, 1));
         HIP_OK(hipEventRecord(ev[3], stream));
         CHECK(sync_state());
         CHECK(select_ready());

@@ -59,8 +59,8 @@ struct Engine {
     size_t hot_cap_alloc = 0;
     size_t home_words_cap = 0, dirty_list_cap = 0, dirty_bits_cap = 0;
     uint64_t home_slots = 0;    // Zig capacity the home histogram is kept for (0: none)
-    Summ *d_summ = nullptr;
-    size_t summ_cap = 0;
+    Summ *d_summ = nullptr, *d_sup = nullptr;
+    size_t summ_cap = 0, sup_cap = 0;
     bool hot_stale = true;
     uint64_t hot_target = 1u << 16;  // ids the hot list aims to hold after a rebuild
     uint64_t hot_rebuilds = 0, home_rebuilds = 0;
@@ -96,7 +96,7 @@ struct Engine {
     zbpe_status maybe_grow_tables(uint32_t X);
     zbpe_status alloc_stream(size_t n);
     zbpe_status compact();
-    zbpe_status launch_argmax();
+    zbpe_status launch_argmax(uint32_t X, int roll);
     int scan_grid(int64_t slots) const;
     zbpe_status launch_scan(const ScanArgs &A, uint64_t expected_occ);
     zbpe_status rebuild_hot();

@@ -47,23 +47,23 @@ __device__ inline uint32_t fmix32(uint32_t h) {
 __device__ inline uint32_t ht_find(const Tables &T, uint32_t key) {
     uint32_t s = fmix32(key) & T.ht_mask;
     for (uint32_t probes = 0; probes <= T.ht_mask; ++probes) {
-        uint32_t k = T.ht_key[s];
-        if (k == key) return T.ht_id[s];
-        if (k == EMPTY_KEY) return NO_ID;
+        const unsigned long long e = T.ht[s];
+        if ((uint32_t)(e >> 32) == key) return (uint32_t)e;
+        if (e == ~0ull) return NO_ID;
         s = (s + 1) & T.ht_mask;
     }
     return NO_ID;
 }
-// Insert a key known to be absent (callers guarantee uniqueness within a launch).
 __device__ inline uint32_t ht_find_count(const Tables &T, uint32_t key) {
     uint32_t id = ht_find(T, key);
     return id == NO_ID ? 0 : T.id_cnt[id];
 }
+// Insert a key known to be absent (callers guarantee uniqueness within a launch).
 __device__ inline void ht_insert_new(const Tables &T, uint32_t key, uint32_t id) {
     uint32_t s = fmix32(key) & T.ht_mask;
+    const unsigned long long e = ((unsigned long long)key << 32) | id;
     for (;;) {
-        uint32_t prev = atomicCAS(&T.ht_key[s], EMPTY_KEY, key);
-        if (prev == EMPTY_KEY) { T.ht_id[s] = id; return; }
+        if (atomicCAS(&T.ht[s], ~0ull, e) == ~0ull) return;
         s = (s + 1) & T.ht_mask;
     }
 }
@@ -575,11 +575,10 @@ __global__ void __launch_bounds__(256) zbpe_apply(uint16_t *tok, int64_t n, cons
 // (t, X) = left[t], group 2 decrements (b, t) by right[t], group 3 creates (X, t) = right[t];
 // one extra thread handles (b, a) -> (X, X) and the merged pair itself. Groups are padded to whole
 // waves so the wave-aggregated id / hot-list appends see uniform control flow.
-__global__ void __launch_bounds__(256) zbpe_update(Tables T, DevState *st, const uint32_t *__restrict__ left,
-                                                   const uint32_t *__restrict__ right, uint32_t a, uint32_t b, uint32_t X,
-                                                   uint32_t top_key) {
+__device__ inline void update_body(const Tables &T, DevState *st, const uint32_t *__restrict__ left,
+                                   const uint32_t *__restrict__ right, uint32_t a, uint32_t b, uint32_t X, uint32_t top_key,
+                                   uint32_t gid) {
     const uint32_t nX = (X + 63) & ~63u;
-    const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
     const uint32_t g = gid / nX, t = gid - g * nX;
     int live_delta = 0;
     if (g == 0 || g == 2) {
@@ -610,18 +609,20 @@ __global__ void __launch_bounds__(256) zbpe_update(Tables T, DevState *st, const
         const bool hot = ok && c >= st->theta;
         const uint32_t j = wave_append(&st->hot_len, hot);
         if (hot && j < T.hot_cap) T.hot[j] = id;
-    } else if (gid == 4 * nX) {
-        const uint32_t occ = st->rec_count, xx = st->xx;
-        if (xx) {
-            pair_dec(T, st, pair_key(b, a), xx);
-            pair_new(T, st, pair_key(X, X), xx);
-        }
-        const uint32_t top_id = ht_find(T, top_key);
-        if (top_id == NO_ID) atomicOr(&st->error, 4u);
-        else {
-            const uint32_t old = atomicSub(&T.id_cnt[top_id], occ);
-            if (old < occ) atomicOr(&st->error, 2u);
-            if (old == occ) { live_delta--; home_add(T, st, top_key, false); }
+    } else if (gid >= 4 * nX && gid < 4 * nX + 3) {  // three independent chains for the specials
+        const uint32_t which = gid - 4 * nX;
+        const uint32_t xx = st->xx;
+        if (which == 0 && xx) pair_dec(T, st, pair_key(b, a), xx);
+        if (which == 1 && xx) pair_new(T, st, pair_key(X, X), xx);
+        if (which == 2) {
+            const uint32_t occ = st->rec_count;
+            const uint32_t top_id = ht_find(T, top_key);
+            if (top_id == NO_ID) atomicOr(&st->error, 4u);
+            else {
+                const uint32_t old = atomicSub(&T.id_cnt[top_id], occ);
+                if (old < occ) atomicOr(&st->error, 2u);
+                if (old == occ) { live_delta--; home_add(T, st, top_key, false); }
+            }
         }
     }
     if (g < 4) {
@@ -631,7 +632,26 @@ __global__ void __launch_bounds__(256) zbpe_update(Tables T, DevState *st, const
         atomicAdd(&st->live, live_delta);
     }
 }
-__host__ __device__ inline uint32_t update_blocks(uint32_t X) { return (4 * ((X + 63) & ~63u) + 64 + 255) / 256; }
+__host__ __device__ inline uint32_t update_blocks(uint32_t X) { return (4 * ((X + 63) & ~63u) + 3 + 255) / 256; }
+
+// replaceTopPairWithNewToken in one launch: blocks [0, apply_blocks) rewrite the stream at the
+// recorded occurrences (X at the start, a hole at the consumed b), the rest update the counts.
+__global__ void __launch_bounds__(256) zbpe_replace(uint16_t *tok, int64_t n, const uint32_t *__restrict__ rec,
+                                                    uint32_t rec_cap, Tables T, DevState *st, const uint32_t *__restrict__ left,
+                                                    const uint32_t *__restrict__ right, uint32_t a, uint32_t b, uint32_t X,
+                                                    uint32_t top_key, uint32_t apply_blocks) {
+    if (blockIdx.x < apply_blocks) {
+        const uint32_t cnt = min(st->rec_count, rec_cap);
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += apply_blocks * 256) {
+            const int64_t p = rec[i];
+            tok[p] = (uint16_t)X;
+            const int64_t q = next_live(tok, n, p);
+            if (q >= 0) tok[q] = HOLE;
+        }
+        return;
+    }
+    update_body(T, st, left, right, a, b, X, top_key, (blockIdx.x - apply_blocks) * 256 + threadIdx.x);
+}
 
 // end of merge: clear the neighbour histograms [0, X) and roll the per-merge counters
 __global__ void __launch_bounds__(256) zbpe_reset_merge(DevState *st, uint32_t *left, uint32_t *right, uint32_t X) {
@@ -898,20 +918,68 @@ __global__ void __launch_bounds__(256) zbpe_hot_build(Tables T, DevState *st) {
         if (take && j < T.hot_cap) T.hot[j] = i;
     }
 }
-__global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_argmax_hot(Tables T, const DevState *st, MaxRec *__restrict__ partial) {
-    const uint32_t n = min(st->hot_len, T.hot_cap), theta = st->theta;
+// Fused select: argmax over the hot list, the final reduction by the last block to finish
+// (agent-scope release/acquire around the ticket, cdna_hip_programming.md Guideline 16), the
+// stream's last-pair count, and the end-of-merge resets (neighbour histograms, counters) when
+// roll != 0. One launch per merge instead of three.
+__global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState *st, MaxRec *__restrict__ partial,
+                                                              const uint16_t *__restrict__ tok, int64_t n, uint32_t *left,
+                                                              uint32_t *right, uint32_t X, int roll) {
+    for (uint32_t t = blockIdx.x * ARGMAX_THREADS + threadIdx.x; t < X; t += gridDim.x * ARGMAX_THREADS) {
+        left[t] = 0;
+        right[t] = 0;
+    }
+    const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
     MaxRec r{0, 0, NO_ID};
-    for (uint32_t i = blockIdx.x * ARGMAX_THREADS + threadIdx.x; i < n; i += gridDim.x * ARGMAX_THREADS) {
+    for (uint32_t i = blockIdx.x * ARGMAX_THREADS + threadIdx.x; i < nh; i += gridDim.x * ARGMAX_THREADS) {
         const uint32_t id = T.hot[i], c = T.id_cnt[id];
         if (c >= theta && c) r = max_combine(r, MaxRec{c, 1u, id});
     }
     r = wave_max(r);
     __shared__ MaxRec sm[ARGMAX_THREADS / WAVE];
+    __shared__ uint32_t s_last;
     if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = r;
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < ARGMAX_THREADS / WAVE; w++) r = max_combine(r, sm[w]);
         partial[blockIdx.x] = r;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = atomicAdd(&st->ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    MaxRec q{0, 0, NO_ID};
+    for (uint32_t i = threadIdx.x; i < gridDim.x; i += ARGMAX_THREADS) q = max_combine(q, partial[i]);
+    q = wave_max(q);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = q;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < ARGMAX_THREADS / WAVE; w++) q = max_combine(q, sm[w]);
+        st->top_count = q.cnt;
+        st->tie_count = q.cnt ? q.ties : 0;
+        st->top_id = q.id;
+        st->top_key = q.id != NO_ID ? T.id_key[q.id] : EMPTY_KEY;
+        if (q.ties > 1) {
+            int64_t j = n - 1;
+            while (j >= 0 && tok[j] == HOLE) j--;
+            int64_t i = j - 1;
+            while (i >= 0 && tok[i] == HOLE) i--;
+            st->lastpair_count = i >= 0 ? ht_find_count(T, pair_key(tok[i], tok[j])) : 0;
+        }
+        if (roll) {
+            st->last_occ = st->rec_count;
+            st->total_occ += st->rec_count;
+            st->rec_count = 0;
+            st->xx = 0;
+        }
+        st->ticket = 0;
     }
 }
 
@@ -982,91 +1050,99 @@ __global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st,
         __syncthreads();
     }
 }
-constexpr int DECIDE_THREADS = 1024;
-// ordered block-wide composition over raw slots [lo, hi) (no wrap)
-__device__ Summ block_compose_slots(const uint32_t *hc, uint32_t lo, uint32_t hi, Summ *sm) {
-    Summ acc{0, 0};
+// super-block summaries: one wave composes SUPER_BLOCKS block summaries
+__global__ void __launch_bounds__(256) zbpe_super_summary(const Summ *__restrict__ summ, uint32_t nb, Summ *__restrict__ sup) {
+    const uint32_t nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w >= nsb) return;
+    const uint32_t bi = w * SUPER_BLOCKS + lane;
+    Summ x = bi < nb ? summ[bi] : Summ{0, 0};
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // ordered tree: lane i absorbs lane i+off
+        Summ y;
+        y.q = __shfl_down(x.q, off);
+        y.m = __shfl_down(x.m, off);
+        if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
+    }
+    if (lane == 0) sup[w] = x;
+}
+// ordered composition by one wave of f(i), i in [lo, hi) (each lane a contiguous chunk)
+template <typename F>
+__device__ inline Summ wave_compose(uint32_t lo, uint32_t hi, F f) {
+    const uint32_t lane = threadIdx.x & 63;
+    Summ x{0, 0};
     if (hi > lo) {
-        const uint32_t len = hi - lo, per = (len + DECIDE_THREADS - 1) / DECIDE_THREADS;
-        const uint32_t b = lo + threadIdx.x * per, e = min(hi, b + per);
-        for (uint32_t s = b; s < e; s++) acc = summ_cat(acc, summ_slot(home_at(hc, s)));
+        const uint32_t per = (hi - lo + 63) / 64, b = lo + min(hi - lo, lane * per), e = min(hi, b + per);
+        for (uint32_t i = b; i < e; i++) x = summ_cat(x, f(i));
     }
-    sm[threadIdx.x] = acc;
-    __syncthreads();
-    for (int st = 1; st < DECIDE_THREADS; st <<= 1) {
-        if ((threadIdx.x & (2 * st - 1)) == 0) sm[threadIdx.x] = summ_cat(sm[threadIdx.x], sm[threadIdx.x + st]);
-        __syncthreads();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        Summ y;
+        y.q = __shfl_down(x.q, off);
+        y.m = __shfl_down(x.m, off);
+        if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
     }
-    Summ r = sm[0];
-    __syncthreads();
+    Summ r;
+    r.q = __shfl(x.q, 0);
+    r.m = __shfl(x.m, 0);
     return r;
 }
-__device__ Summ block_compose_blocks(const Summ *summ, uint32_t b0, uint32_t b1, Summ *sm) {
-    Summ acc{0, 0};
-    if (b1 > b0) {
-        const uint32_t len = b1 - b0, per = (len + DECIDE_THREADS - 1) / DECIDE_THREADS;
-        const uint32_t b = b0 + threadIdx.x * per, e = min(b1, b + per);
-        for (uint32_t i = b; i < e; i++) acc = summ_cat(acc, summ[i]);
-    }
-    sm[threadIdx.x] = acc;
-    __syncthreads();
-    for (int st = 1; st < DECIDE_THREADS; st <<= 1) {
-        if ((threadIdx.x & (2 * st - 1)) == 0) sm[threadIdx.x] = summ_cat(sm[threadIdx.x], sm[threadIdx.x + st]);
-        __syncthreads();
-    }
-    Summ r = sm[0];
-    __syncthreads();
-    return r;
+struct HomeView {
+    const uint32_t *hc;
+    const Summ *summ, *sup;
+    uint32_t C, nb, nsb;
+};
+// carry into slot s = m of the composition over slots s+1 .. s-1 (circular), by one wave:
+// partial block, blocks to the end of the super-block, the other super-blocks, blocks up to s's
+// block, partial block
+__device__ inline int64_t wave_carry_into(const HomeView &V, uint32_t s) {
+    const uint32_t b = s / SUMM_SLOTS, sb = b / SUPER_BLOCKS;
+    auto slot = [&](uint32_t i) { return summ_slot(home_at(V.hc, i)); };
+    auto blk = [&](uint32_t i) { return V.summ[i]; };
+    auto sup = [&](uint32_t i) { return V.sup[i % V.nsb]; };
+    Summ x = wave_compose(s + 1, min(V.C, (b + 1) * SUMM_SLOTS), slot);
+    x = summ_cat(x, wave_compose(b + 1, min(V.nb, (sb + 1) * SUPER_BLOCKS), blk));
+    x = summ_cat(x, wave_compose(sb + 1, sb + V.nsb, sup));
+    x = summ_cat(x, wave_compose(sb * SUPER_BLOCKS, b, blk));
+    x = summ_cat(x, wave_compose(b * SUMM_SLOTS, s, slot));
+    return x.m;
 }
-// carry into slot s = m of the composition over slots s+1 .. s-1 (circular)
-__device__ int64_t block_carry_into(const uint32_t *hc, const Summ *summ, uint32_t C, uint32_t s, Summ *sm) {
-    const uint32_t nb = (C + SUMM_SLOTS - 1) / SUMM_SLOTS, b = s / SUMM_SLOTS;
-    Summ a = block_compose_slots(hc, s + 1, min(C, (b + 1) * SUMM_SLOTS), sm);
-    Summ x = block_compose_blocks(summ, b + 1, nb, sm);
-    Summ y = block_compose_blocks(summ, 0, b, sm);
-    Summ z = block_compose_slots(hc, b * SUMM_SLOTS, s, sm);
-    return summ_cat(summ_cat(summ_cat(a, x), y), z).m;
-}
-// last free slot in [lo, hi) given the carry into lo (-1 if none): ordered scan of chunk functions
-__device__ int64_t block_last_free(const uint32_t *hc, uint32_t lo, uint32_t hi, int64_t carry_in, Summ *sm) {
-    const uint32_t len = hi - lo, per = (len + DECIDE_THREADS - 1) / DECIDE_THREADS;
-    const uint32_t b = lo + min(len, threadIdx.x * per), e = min(hi, b + per);
-    Summ acc{0, 0};
-    for (uint32_t s = b; s < e; s++) acc = summ_cat(acc, summ_slot(home_at(hc, s)));
-    sm[threadIdx.x] = acc;
-    __syncthreads();
-    for (int sp = 1; sp < DECIDE_THREADS; sp <<= 1) {  // inclusive Hillis-Steele scan of compositions
-        Summ prev = threadIdx.x >= (unsigned)sp ? sm[threadIdx.x - sp] : Summ{0, 0};
-        __syncthreads();
-        if (threadIdx.x >= (unsigned)sp) sm[threadIdx.x] = summ_cat(prev, sm[threadIdx.x]);
-        __syncthreads();
+// last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none)
+__device__ inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int64_t carry_in) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t per = (hi - lo + 63) / 64, b = lo + min(hi - lo, lane * per), e = min(hi, b + per);
+    Summ x{0, 0};
+    for (uint32_t i = b; i < e; i++) x = summ_cat(x, summ_slot(home_at(V.hc, i)));
+    // exclusive ordered scan over lanes
+    Summ inc = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        Summ y;
+        y.q = __shfl_up(inc.q, off);
+        y.m = __shfl_up(inc.m, off);
+        if ((int)lane >= off) inc = summ_cat(y, inc);
     }
-    const Summ before = threadIdx.x ? sm[threadIdx.x - 1] : Summ{0, 0};
-    int64_t c = max(before.m, carry_in + before.q);
-    int64_t last = -1;
-    for (uint32_t s = b; s < e; s++) {
-        const int64_t k = home_at(hc, s);
-        if (c + k == 0) last = s;
+    Summ ex;
+    ex.q = __shfl_up(inc.q, 1);
+    ex.m = __shfl_up(inc.m, 1);
+    if (lane == 0) ex = Summ{0, 0};
+    int64_t c = max(ex.m, carry_in + ex.q);
+    long long last = -1;
+    for (uint32_t i = b; i < e; i++) {
+        const int64_t k = home_at(V.hc, i);
+        if (c + k == 0) last = i;
         else c = c + k - 1;
     }
-    __syncthreads();
-    __shared__ long long red[DECIDE_THREADS];
-    red[threadIdx.x] = last;
-    __syncthreads();
-    for (int sp = DECIDE_THREADS / 2; sp > 0; sp >>= 1) {
-        if (threadIdx.x < (unsigned)sp) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + sp]);
-        __syncthreads();
-    }
-    const int64_t r = red[0];
-    __syncthreads();
-    return r;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) last = max(last, (long long)__shfl_xor(last, off));
+    return last;
 }
+constexpr int DECIDE_THREADS = 256;
 __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, const uint64_t *__restrict__ tie_list,
-                                                                  uint32_t tie_cap, const uint32_t *__restrict__ hc,
-                                                                  const Summ *__restrict__ summ, uint32_t C) {
-    __shared__ Summ sm[DECIDE_THREADS];
+                                                                  uint32_t tie_cap, HomeView V) {
     __shared__ uint64_t s1[DECIDE_THREADS], s2[DECIDE_THREADS];
     __shared__ uint32_t sh[DECIDE_THREADS];
+    __shared__ long long s_c1, s_c0, s_cw, s_last;
     const uint32_t len = min(st->tie_len, tie_cap);
     uint64_t m1 = ~0ull, m2 = ~0ull;
     uint32_t hmax = 0;
@@ -1087,34 +1163,33 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
         __syncthreads();
     }
     m1 = s1[0]; m2 = s2[0]; hmax = sh[0];
-    __syncthreads();
     const uint32_t h1 = (uint32_t)(m1 >> 32);
-    const int64_t c1 = block_carry_into(hc, summ, C, h1, sm);
-    const int64_t c0 = block_carry_into(hc, summ, C, 0, sm);
-    // the run wrapping past slot C-1 starts after the last free slot below C: search a growing window
-    int64_t last_free = -2;  // -2: no wrapping run
-    if (c0 > 0) {
-        last_free = -1;
-        for (uint32_t W = 4096; last_free < 0; W *= 16) {
-            const uint32_t ws = W >= C ? 0 : C - W;
-            const int64_t cw = ws > 0 ? block_carry_into(hc, summ, C, ws, sm) : c0;
-            last_free = block_last_free(hc, ws, C, cw, sm);
-            if (ws == 0) break;
-        }
+    const uint32_t ws = V.C > 4096 ? V.C - 4096 : 0;
+    // three carries in parallel, one per wave
+    const int w = threadIdx.x >> 6;
+    if (w == 0) { const int64_t c = wave_carry_into(V, h1); if ((threadIdx.x & 63) == 0) s_c1 = c; }
+    if (w == 1) { const int64_t c = wave_carry_into(V, 0); if ((threadIdx.x & 63) == 0) s_c0 = c; }
+    if (w == 2) { const int64_t c = ws ? wave_carry_into(V, ws) : 0; if ((threadIdx.x & 63) == 0) s_cw = c; }
+    __syncthreads();
+    // the run wrapping past slot C-1 (if any) starts after the last free slot of [ws, C)
+    if (w == 2) {
+        const int64_t lf = s_c0 > 0 ? wave_last_free(V, ws, V.C, ws ? s_cw : s_c0) : -2;
+        if ((threadIdx.x & 63) == 0) s_last = lf;
     }
+    __syncthreads();
     if (threadIdx.x) return;
     uint32_t verdict = st->tie_len > tie_cap ? 1u : 0u;
-    // first free slot at or after h1
-    int64_t c = c1;
+    int64_t c = s_c1;  // first free slot at or after h1
     uint32_t s = h1;
     for (;; s++) {
-        if (s >= C || s - h1 > (1u << 20)) { verdict = 1; break; }  // the run of h1 wraps (or is absurdly long)
-        const int64_t k = home_at(hc, s);
+        if (s >= V.C || s - h1 > (1u << 20)) { verdict = 1; break; }  // the run of h1 wraps (or is absurdly long)
+        const int64_t k = home_at(V.hc, s);
         if (c + k == 0) break;
         c = c + k - 1;
     }
     if (m2 != ~0ull && s > (uint32_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
-    if (last_free != -2 && (last_free < 0 || (int64_t)hmax >= last_free + 1)) verdict = 1;  // tied pair may wrap
+    const long long lf = s_last;
+    if (lf != -2 && (lf < 0 || (long long)hmax >= lf + 1)) verdict = 1;  // a tied pair may have wrapped
     st->tie_verdict = verdict;
     st->tie_winner = (uint32_t)m1;
     st->dirty_len = 0;

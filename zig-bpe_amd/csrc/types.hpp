@@ -40,12 +40,11 @@ struct DevState {
     uint32_t theta;          // hot-list threshold: every live id with count >= theta is in the hot list
     uint32_t hot_len;        // ids appended to the hot list (may exceed its capacity -> rebuild)
     uint32_t dirty_len;      // home-histogram blocks changed since their summaries were computed
-    uint32_t pad[1];
+    uint32_t ticket;         // zbpe_select: blocks done (the last one reduces), reset by it
 };
 
 struct Tables {
-    uint32_t *ht_key;   // [ht_cap]
-    uint32_t *ht_id;    // [ht_cap]
+    unsigned long long *ht;  // [ht_cap] slot = key << 32 | id, ~0 = empty (one 8-B load per probe)
     uint32_t ht_mask;
     uint32_t *id_key;   // [id_cap]
     uint32_t *id_cnt;   // [id_cap]
@@ -61,6 +60,7 @@ struct Tables {
 
 constexpr int COUNT_BINS = 64 + 26 * 32;  // count histogram for choosing theta: exact < 64, then 32 per octave
 constexpr int SUMM_SLOTS = 4096;          // home-histogram slots per max-plus block summary
+constexpr int SUPER_BLOCKS = 64;          // block summaries per super-block summary
 struct Summ { int64_t q, m; };            // carry function c -> max(m, c + q) of a run of slots
 
 struct MaxRec { uint32_t cnt, ties, id; };
