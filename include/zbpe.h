@@ -68,6 +68,13 @@ zbpe_status zbpe_create(int device, zbpe_ctx **out);
 zbpe_status zbpe_comm_unique_id(void *out128);
 zbpe_status zbpe_create_dist(int device, int rank, int world, const void *unique_id128, zbpe_ctx **out);
 
+/* Same, with the collectives done by a host callback instead of RCCL (e.g. torch.distributed with
+ * gloo; lets several ranks share one GPU in tests). op 0: in-place sum of `count` u32 in buf;
+ * op 1: in-place min of `count` u32; op 2: all-gather, buf holds world * count bytes and this
+ * rank's count bytes are at rank * count. Return 0 on success. */
+typedef int (*zbpe_collective_fn)(void *user, int op, void *buf, size_t count);
+zbpe_status zbpe_create_dist_host(int device, int rank, int world, zbpe_collective_fn fn, void *user, zbpe_ctx **out);
+
 void zbpe_destroy(zbpe_ctx *ctx);
 const char *zbpe_last_error(const zbpe_ctx *ctx);
 

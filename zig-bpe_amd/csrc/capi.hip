@@ -37,13 +37,38 @@ zbpe_status zbpe_create(int device, zbpe_ctx **out) {
 }
 
 zbpe_status zbpe_comm_unique_id(void *out128) {
-    (void)out128;
-    return ZBPE_COMM_ERROR;
+    if (!out128) return ZBPE_INVALID_ARGUMENT;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return ZBPE_COMM_ERROR;
+    memcpy(out128, &id, sizeof(id));
+    return ZBPE_OK;
 }
+
+static zbpe_status finish_dist(zbpe_ctx *c, int rank, int world, std::unique_ptr<zbpe::Comm> comm, zbpe_ctx **out) {
+    zbpe_status s = c->eng.init_dist(rank, world, std::move(comm));
+    *out = c;
+    return s;
+}
+
 zbpe_status zbpe_create_dist(int device, int rank, int world, const void *unique_id128, zbpe_ctx **out) {
-    (void)unique_id128;
-    if (world == 1 && rank == 0) return zbpe_create(device, out);
-    return ZBPE_COMM_ERROR;
+    if (!out || world < 1 || rank < 0 || rank >= world || (world > 1 && !unique_id128)) return ZBPE_INVALID_ARGUMENT;
+    zbpe_status s = zbpe_create(device, out);
+    if (s != ZBPE_OK || world == 1) return s;
+    auto comm = std::make_unique<zbpe::RcclComm>();
+    if (!comm->init(rank, world, unique_id128)) return (*out)->eng.fail(ZBPE_COMM_ERROR, "ncclCommInitRank failed (rank %d of %d)", rank, world);
+    return finish_dist(*out, rank, world, std::move(comm), out);
+}
+
+zbpe_status zbpe_create_dist_host(int device, int rank, int world, zbpe_collective_fn fn, void *user, zbpe_ctx **out) {
+    if (!out || !fn || world < 1 || rank < 0 || rank >= world) return ZBPE_INVALID_ARGUMENT;
+    zbpe_status s = zbpe_create(device, out);
+    if (s != ZBPE_OK) return s;
+    auto comm = std::make_unique<zbpe::HostComm>();
+    comm->fn = fn;
+    comm->user = user;
+    comm->rank = rank;
+    comm->world = world;
+    return finish_dist(*out, rank, world, std::move(comm), out);
 }
 
 void zbpe_destroy(zbpe_ctx *ctx) { delete ctx; }
@@ -52,7 +77,7 @@ const char *zbpe_last_error(const zbpe_ctx *ctx) { return ctx ? ctx->eng.err.c_s
 
 zbpe_status zbpe_upload(zbpe_ctx *ctx, const uint8_t *text, size_t n) {
     if (!ctx || (!text && n)) return ZBPE_INVALID_ARGUMENT;
-    return ctx->eng.upload(text, n);
+    return ctx->eng.upload(text, n, ctx->eng.world > 1);
 }
 
 zbpe_status zbpe_train_resident(zbpe_ctx *ctx, uint16_t vocab_size, int verbose, uint16_t *out_triples,
@@ -66,7 +91,7 @@ zbpe_status zbpe_train(zbpe_ctx *ctx, const uint8_t *text, size_t n, uint16_t vo
     if (!ctx || !out_n_merges || (!text && n)) return ZBPE_INVALID_ARGUMENT;
     *out_n_merges = 0;
     if (vocab_size < 256) return ctx->eng.fail(ZBPE_INVALID_VOCAB_SIZE, "vocabSize %u < 256", vocab_size);
-    zbpe_status s = ctx->eng.upload(text, n);
+    zbpe_status s = ctx->eng.upload(text, n, ctx->eng.world > 1);
     if (s != ZBPE_OK) return s;
     return zbpe_train_resident(ctx, vocab_size, verbose, out_triples, out_counts, out_n_merges, stats);
 }

@@ -54,7 +54,7 @@ void Engine::release() {
     auto f = [](void *p) { if (p) (void)hipFree(p); };
     f(d_text); f(d_tok[0]); f(d_tok[1]);
     f(T.ht); f(T.id_key); f(T.id_cnt);
-    f(d_left); f(d_right); f(d_st); f(d_rec); f(d_partial); f(d_hist);
+    f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list); f(d_sup);
     if (h_st) (void)hipHostFree(h_st);
@@ -62,7 +62,11 @@ void Engine::release() {
     for (auto &e : ev) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
     d_text = nullptr; d_tok[0] = d_tok[1] = nullptr; T = Tables{};
-    d_left = d_right = nullptr; d_st = nullptr; d_rec = nullptr; d_partial = nullptr; d_hist = nullptr;
+    d_delta = nullptr; d_st = nullptr; d_rec = nullptr; d_partial = nullptr; d_hist = nullptr;
+    d_bnd_mine = d_bnd_all = nullptr; d_x0 = nullptr; d_shard_fn = d_fns_all = nullptr;
+    if (h_bnd) (void)hipHostFree(h_bnd);
+    h_bnd = nullptr;
+    comm.reset();
     d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr;
     d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
     d_summ = nullptr; d_count_hist = nullptr; h_count_hist = nullptr; hot_cap_alloc = home_words_cap = 0; home_slots = 0;
@@ -79,8 +83,8 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIP_OK(hipHostMalloc((void **)&h_st, sizeof(DevState), hipHostMallocDefault));
     HIP_OK(hipMalloc(&d_st, sizeof(DevState)));
-    HIP_OK(hipMalloc(&d_left, 65536 * sizeof(uint32_t)));
-    HIP_OK(hipMalloc(&d_right, 65536 * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_delta, DELTA_WORDS * sizeof(uint32_t)));
+    HIP_OK(hipMemset(d_delta, 0, DELTA_WORDS * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
     HIP_OK(hipMalloc(&d_count_hist, COUNT_BINS * sizeof(uint32_t)));
@@ -111,14 +115,44 @@ zbpe_status Engine::ensure(T_ **p, size_t &cap, size_t need, const char *what) {
     return ZBPE_OK;
 }
 
-zbpe_status Engine::upload(const uint8_t *text, size_t n) {
-    if (n > (size_t)0xFFFFFFF0u) return fail(ZBPE_INVALID_ARGUMENT, "shard of %zu bytes exceeds 2^32 tokens", n);
+// Stage this rank's shard [s, e) of the corpus in HBM (the whole corpus on one GPU or when
+// shard == false). The first byte after the shard feeds the boundary pair of the initial histogram;
+// the bytes around it are the initial halo.
+zbpe_status Engine::upload(const uint8_t *text, size_t n, bool shard) {
+    const size_t s = shard ? (size_t)((unsigned __int128)n * rank / world) : 0;
+    const size_t e = shard ? (size_t)((unsigned __int128)n * (rank + 1) / world) : n;
+    if (n >= (size_t)0xFFFFFFF0u) return fail(ZBPE_INVALID_ARGUMENT, "corpus of %zu bytes exceeds 2^32 tokens", n);
     HIP_OK(hipSetDevice(device));
-    CHECK(ensure(&d_text, text_cap, round_up(n + 64, 64), "corpus"));
-    if (n) HIP_OK(hipMemcpyAsync(d_text, text, n, hipMemcpyHostToDevice, stream));
+    CHECK(ensure(&d_text, text_cap, round_up(e - s + 64, 64), "corpus"));
+    if (e > s) HIP_OK(hipMemcpyAsync(d_text, text + s, e - s, hipMemcpyHostToDevice, stream));
     HIP_OK(hipStreamSynchronize(stream));
-    n_text = n;
+    n_text = e - s;
+    shard_offset = (uint32_t)s;
+    next_byte = e < n && shard ? (int)text[e] : -1;
+    Halo H{};
+    H.left[0] = H.left[1] = HOLE;
+    H.right[0] = H.right[1] = H.right[2] = HOLE;
+    if (shard) {
+        for (size_t i = s; i > 0 && H.nleft < 2; i--) H.left[H.nleft++] = text[i - 1];
+        for (size_t i = e; i < n && H.nright < 3; i++) H.right[H.nright++] = text[i];
+    }
+    halo0 = H;
+    sharded = shard;
     uploaded = true;
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::init_dist(int r, int w, std::unique_ptr<Comm> c) {
+    rank = r;
+    world = w;
+    comm = std::move(c);
+    HIP_OK(hipSetDevice(device));
+    HIP_OK(hipMalloc(&d_bnd_mine, sizeof(Boundary)));
+    HIP_OK(hipMalloc(&d_bnd_all, (size_t)w * sizeof(Boundary)));
+    HIP_OK(hipHostMalloc((void **)&h_bnd, (size_t)w * sizeof(Boundary), hipHostMallocDefault));
+    HIP_OK(hipMalloc(&d_x0, 16));
+    HIP_OK(hipMalloc(&d_shard_fn, 16));
+    HIP_OK(hipMalloc(&d_fns_all, (size_t)w * 4 + 16));
     return ZBPE_OK;
 }
 
@@ -250,7 +284,8 @@ zbpe_status Engine::launch_argmax(uint32_t X, int roll) {
     const uint64_t work = std::max<uint64_t>(T.hot_cap / 4, X);
     int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, (work + ARGMAX_THREADS - 1) / ARGMAX_THREADS);
     blocks = std::max(blocks, 1);
-    zbpe_select<<<blocks, ARGMAX_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], n_slots, d_left, d_right, X, roll);
+    zbpe_select<<<blocks, ARGMAX_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], n_slots, d_delta, X, roll, d_bnd_all,
+                                                       world);
     LAUNCH_OK();
     return ZBPE_OK;
 }
@@ -359,8 +394,11 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     CHECK(ensure(&d_gather, gather_cap, (size_t)D, "live pairs"));
     HIP_OK(hipMemsetAsync(d_first, 0xFF, (size_t)nid * 4, stream));
     HIP_OK(hipMemsetAsync(&d_st->gather_len, 0, 4, stream));
-    zbpe_first_occ<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, T, d_first, d_st);
-    LAUNCH_OK();
+    {
+        ScanArgs A{d_tok[cur], n_slots, 0, 0, nullptr, nullptr, d_st, nullptr, 0, 0, nullptr, nullptr, halo};
+        zbpe_first_occ<<<2048, 256, 0, stream>>>(A, shard_offset, T, d_first, d_st);
+        LAUNCH_OK();
+    }
     zbpe_gather_live<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_first, d_st, d_gather, (uint32_t)gather_cap);
     LAUNCH_OK();
     CHECK(sync_state());
@@ -369,6 +407,19 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     std::vector<LiveRec> recs(g);
     HIP_OK(hipMemcpyAsync(recs.data(), d_gather, (size_t)g * sizeof(LiveRec), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
+    if (world > 1) {
+        // every rank holds the same live keys: in key order the local first positions line up, so one
+        // all-reduce(min) gives the global first occurrence of each pair
+        std::sort(recs.begin(), recs.end(), [](const LiveRec &x, const LiveRec &y) { return x.key < y.key; });
+        std::vector<uint32_t> pos(g);
+        for (uint32_t i = 0; i < g; i++) pos[i] = recs[i].first_pos;
+        CHECK(ensure(&d_first, first_cap, std::max<size_t>(g, nid), "first occurrences"));
+        HIP_OK(hipMemcpyAsync(d_first, pos.data(), (size_t)g * 4, hipMemcpyHostToDevice, stream));
+        if (!comm->allreduce_u32(d_first, g, COMM_MIN_U32, stream)) return fail(ZBPE_COMM_ERROR, "all-reduce(min) failed");
+        HIP_OK(hipMemcpyAsync(pos.data(), d_first, (size_t)g * 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        for (uint32_t i = 0; i < g; i++) recs[i].first_pos = pos[i];
+    }
     std::vector<ZigOrderInput> in(g);
     for (uint32_t i = 0; i < g; i++) in[i] = ZigOrderInput{recs[i].first_pos, recs[i].key, recs[i].count};
     if (!zig_order_winner(std::move(in), top, call_after, winner))
@@ -414,14 +465,15 @@ zbpe_status Engine::bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms,
         stream_ready = true;
     }
     CHECK(ensure(&d_rec, rec_cap, (size_t)n_slots / 2 + 1, "occurrence records"));
-    ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 1};
+    uint32_t *tail = d_delta + DELTA_WORDS - 32;
+    ScanArgs A{d_tok[cur], n_slots, a, b, d_delta, d_delta + 65536, d_st, d_rec, (uint32_t)rec_cap, 1, tail, tail + 1, Halo{}};
     double total = 0;
     for (int r = 0; r < reps; r++) {
         HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
         HIP_OK(hipEventRecord(ev[0], stream));
         CHECK(launch_scan(A, 0));
         HIP_OK(hipEventRecord(ev[1], stream));
-        zbpe_reset_merge<<<256, 256, 0, stream>>>(d_st, d_left, d_right, 65536);
+        zbpe_reset_merge<<<256, 256, 0, stream>>>(d_st, d_delta, d_delta + 65536, 65536);
         LAUNCH_OK();
         HIP_OK(hipEventSynchronize(ev[1]));
         float ms;
@@ -459,6 +511,24 @@ zbpe_status Engine::alloc_stream(size_t n) {
     return ZBPE_OK;
 }
 
+// halo of this rank from the gathered boundary records (walks past shards with too few live tokens)
+void Engine::halo_from_boundaries() {
+    Halo H{};
+    H.left[0] = H.left[1] = HOLE;
+    H.right[0] = H.right[1] = H.right[2] = HOLE;
+    for (int r = rank - 1; r >= 0 && H.nleft < 2; r--)
+        for (int k = 0; k < h_bnd[r].nlast && H.nleft < 2; k++) H.left[H.nleft++] = h_bnd[r].last[k];
+    for (int r = rank + 1; r < world && H.nright < 3; r++)
+        for (int k = 0; k < h_bnd[r].nfirst && H.nright < 3; k++) H.right[H.nright++] = h_bnd[r].first[k];
+    halo = H;
+}
+
+zbpe_status Engine::comm_sum(uint32_t *d, size_t n) {
+    if (world > 1 && n && !comm->allreduce_u32(d, n, COMM_SUM_U32, stream))
+        return fail(ZBPE_COMM_ERROR, "all-reduce of %zu u32 failed", n);
+    return ZBPE_OK;
+}
+
 zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triples, uint64_t *out_counts,
                           size_t *out_n_merges, zbpe_stats *out_stats) {
     const double t_start = now_s();
@@ -466,6 +536,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     *out_n_merges = 0;
     if (vocab_size < 256) return fail(ZBPE_INVALID_VOCAB_SIZE, "vocabSize %u < 256", vocab_size);
     if (!uploaded) return fail(ZBPE_INVALID_ARGUMENT, "no corpus uploaded");
+    if (!sharded && world > 1) return fail(ZBPE_INVALID_ARGUMENT, "distributed context: upload the corpus with zbpe_upload");
     HIP_OK(hipSetDevice(device));
     const size_t n = n_text;
     double ev_count = 0, ev_select = 0, ev_replace = 0;
@@ -485,19 +556,26 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     if (T.home_dirty) { (void)hipFree(T.home_dirty); T.home_dirty = nullptr; dirty_bits_cap = 0; }
     if (T.dirty_list) { (void)hipFree(T.dirty_list); T.dirty_list = nullptr; dirty_list_cap = 0; T.dirty_cap = 0; }
     hot_stale = true;
-    HIP_OK(hipMemsetAsync(d_left, 0, 65536 * 4, stream));
-    HIP_OK(hipMemsetAsync(d_right, 0, 65536 * 4, stream));
+    halo = halo0;
+    HIP_OK(hipMemsetAsync(d_delta, 0, DELTA_WORDS * 4, stream));
     HIP_OK(hipMemsetAsync(d_hist, 0, 65536 * 4, stream));
     HIP_OK(hipEventRecord(ev[0], stream));
-    if (n >= 2) {
+    if (n + (next_byte >= 0 ? 1 : 0) >= 2) {
         const int hb = std::max(1, num_cus);
         for (uint32_t lo : {0u, 128u}) {
-            zbpe_count_byte_pairs<<<hb, HIST_THREADS, 32768 * 4, stream>>>(d_text, n, -1, lo, d_hist);
+            zbpe_count_byte_pairs<<<hb, HIST_THREADS, 32768 * 4, stream>>>(d_text, n, next_byte, lo, d_hist);
             LAUNCH_OK();
         }
-        zbpe_hist_to_table<<<256, 256, 0, stream>>>(d_hist, T, d_st);
-        LAUNCH_OK();
     }
+    CHECK(comm_sum(d_hist, 65536));  // every rank builds the same table from the summed histogram
+    if (world > 1) {  // boundary tokens of every shard (the first select needs the stream's last pair)
+        zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, n_live, d_bnd_mine);
+        LAUNCH_OK();
+        if (!comm->allgather(d_bnd_mine, d_bnd_all, sizeof(Boundary), stream))
+            return fail(ZBPE_COMM_ERROR, "all-gather of shard boundaries failed");
+    }
+    zbpe_hist_to_table<<<256, 256, 0, stream>>>(d_hist, T, d_st);
+    LAUNCH_OK();
     HIP_OK(hipEventRecord(ev[1], stream));
     CHECK(sync_state());
     CHECK(launch_argmax(0, 0));
@@ -514,7 +592,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     size_t merges = 0;
     for (uint32_t X = 256; X < vocab_size; X++) {
         if (h_st->live <= 0) {  // sortedCodePointPairs.len == 0 (basic_tokenizer.zig:188-191)
-            fprintf(stderr, "No more pairs to merge. Stopping early.\n");
+            if (rank == 0) fprintf(stderr, "No more pairs to merge. Stopping early.\n");
             break;
         }
         const uint32_t top = h_st->top_count, ties = h_st->tie_count;
@@ -524,7 +602,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         stats.sort_pairs_calls++;
         if (ties > 1) ev_select += now_s() - t_sel;
         const uint32_t a = key & 0xFFFF, b = key >> 16;
-        if (verbose)
+        if (verbose && rank == 0)
             fprintf(stderr, "merge %u/%u: (%u,%u) -> %u had %u occurrences\n", X - 256 + 1, vocab_size - 256u, a, b, X, top);
         out_triples[3 * merges + 0] = (uint16_t)a;
         out_triples[3 * merges + 1] = (uint16_t)b;
@@ -546,8 +624,10 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
             ev_replace += ms * 1e-3;
         }
+        // delta layout for this merge: left[0, X) | right[X, 2X) | xx | occurrences
+        uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
         // ---- count: scan the stream for (a, b) -----------------------------------------------------
-        ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 1};
+        ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_rec, (uint32_t)rec_cap, 1, tail, tail + 1, halo};
         HIP_OK(hipEventRecord(ev[0], stream));
         if (!self) {
             CHECK(launch_scan(A, top));
@@ -559,22 +639,39 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             CHECK(ensure(&d_carry, carry_cap, ntiles, "self carry"));
             zbpe_self_tiles<<<ntiles, SELF_THREADS, 0, stream>>>(d_tok[cur], n_slots, a, d_tile_fn);
             LAUNCH_OK();
-            zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry);
+            if (world > 1) {  // parity of the run of a's entering this shard from the ranks to the left
+                zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, nullptr, d_shard_fn);
+                LAUNCH_OK();
+                if (!comm->allgather(d_shard_fn, d_fns_all, 4, stream)) return fail(ZBPE_COMM_ERROR, "all-gather of run carries failed");
+                zbpe_self_x0<<<1, 1, 0, stream>>>(d_fns_all, rank, d_x0);
+                LAUNCH_OK();
+            }
+            zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, world > 1 ? d_x0 : nullptr, nullptr);
             LAUNCH_OK();
             zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
             LAUNCH_OK();
         }
         HIP_OK(hipEventRecord(ev[1], stream));
+        // ---- exchange: sum the count deltas of all shards (one RCCL all-reduce per merge) ---------------
+        CHECK(comm_sum(d_delta, 2ull * X + 2));
         // ---- replace: apply + count update ---------------------------------------------------------
         {
             const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top / 256 + 1);
-            zbpe_replace<<<ab + update_blocks(X), 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, T, d_st,
-                                                                   d_left, d_right, a, b, X, key, ab);
+            ReplaceArgs R{d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, left, right, tail, a, b, X, key, ab, halo,
+                          (self && world > 1) ? d_x0 : nullptr};
+            zbpe_replace<<<ab + update_blocks(X), 256, 0, stream>>>(R, T, d_st);
             LAUNCH_OK();
         }
+        if (world > 1) {  // boundary tokens of every shard for the next merge's halos
+            zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, n_live, d_bnd_mine);
+            LAUNCH_OK();
+            if (!comm->allgather(d_bnd_mine, d_bnd_all, sizeof(Boundary), stream))
+                return fail(ZBPE_COMM_ERROR, "all-gather of shard boundaries failed");
+        }
         HIP_OK(hipEventRecord(ev[2], stream));
-        // ---- select for the next merge (also clears the neighbour histograms, rolls the counters) -----
+        // ---- select for the next merge (also clears the deltas, rolls the counters) ----------------------
         CHECK(launch_argmax(X, 1));
+        if (world > 1) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
         HIP_OK(hipEventRecord(ev[3], stream));
         CHECK(sync_state());
         CHECK(select_ready());
@@ -591,11 +688,13 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             stats.count_pairs_calls++;
             stats.replace_pair_calls++;
         }
-        const uint32_t occ = h_st->last_occ;
-        if (!self && occ != top)
-            return fail(ZBPE_INTERNAL, "merge %u: scan found %u occurrences of (%u,%u), count was %u", X, occ, a, b, top);
-        n_live -= occ;
-        holes += occ;
+        if (world > 1) halo_from_boundaries();
+        const uint32_t gocc = h_st->last_gocc;
+        if (!self && gocc != top)
+            return fail(ZBPE_INTERNAL, "merge %u: scan found %u occurrences of (%u,%u), count was %u", X, gocc, a, b, top);
+        const uint64_t gone = (uint64_t)h_st->last_occ + h_st->consumed;  // slots of this shard that became holes
+        n_live -= gone;
+        holes += gone;
         if (holes * compact_den > (uint64_t)n_slots) {
             HIP_OK(hipEventRecord(ev[0], stream));
             CHECK(compact());
@@ -612,9 +711,27 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     stats.count_pairs_s = ev_count;
     stats.sort_pairs_s = ev_select;
     stats.replace_pair_s = ev_replace;
+    stats.final_tokens = (uint64_t)n_live;
+    if (world > 1) {  // stream lengths are per shard: sum them
+        uint64_t v[4] = {stats.final_tokens, stats.sum_tokens, stats.scan_alg_bytes, stats.scan_read_bytes};
+        uint32_t w[8];
+        for (int i = 0; i < 4; i++) { w[2 * i] = (uint32_t)v[i]; w[2 * i + 1] = (uint32_t)(v[i] >> 32); }
+        // exact u64 sums from u32 halves: sum low halves with carries folded in on the host
+        uint32_t *d_w = d_delta + DELTA_WORDS - 16;
+        uint32_t lo[8], hi[8];
+        for (int i = 0; i < 4; i++) { lo[2 * i] = w[2 * i] & 0xFFFF; lo[2 * i + 1] = w[2 * i] >> 16; hi[2 * i] = w[2 * i + 1]; hi[2 * i + 1] = 0; }
+        HIP_OK(hipMemcpyAsync(d_w, lo, 32, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(d_w + 8, hi, 32, hipMemcpyHostToDevice, stream));
+        CHECK(comm_sum(d_w, 16));
+        HIP_OK(hipMemcpyAsync(lo, d_w, 32, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipMemcpyAsync(hi, d_w + 8, 32, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        for (int i = 0; i < 4; i++) v[i] = (uint64_t)lo[2 * i] + ((uint64_t)lo[2 * i + 1] << 16) + ((uint64_t)hi[2 * i] << 32);
+        stats.final_tokens = v[0]; stats.sum_tokens = v[1]; stats.scan_alg_bytes = v[2]; stats.scan_read_bytes = v[3];
+        HIP_OK(hipMemsetAsync(d_w, 0, 64, stream));
+    }
     stats.total_s = now_s() - t_start;
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
-    stats.final_tokens = (uint64_t)n_live;
     stats.distinct_pairs = (uint64_t)std::max(h_st->live, 0);
     stats.pair_ids = h_st->num_ids;
     trained = true;
@@ -624,6 +741,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
 
 zbpe_status Engine::verify_counts(uint64_t *mismatches) {
     if (!trained) return fail(ZBPE_INVALID_ARGUMENT, "verify_counts needs a trained context");
+    if (world > 1) return fail(ZBPE_INVALID_ARGUMENT, "verify_counts is single-GPU only");
     HIP_OK(hipSetDevice(device));
     CHECK(sync_state());
     const uint32_t nid = h_st->num_ids;
@@ -649,7 +767,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
         if (triples[3 * k + 2] == HOLE || triples[3 * k] == HOLE || triples[3 * k + 1] == HOLE)
             return fail(ZBPE_INVALID_ARGUMENT, "merge %zu uses token 65535", k);
     }
-    CHECK(upload(text, n));
+    CHECK(upload(text, n, false));
     trained = false;
     CHECK(alloc_stream(n));
     HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
@@ -664,7 +782,8 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
             n_live -= h_st->total_occ;
             if (holes) { CHECK(compact()); holes = 0; }
         }
-        ScanArgs A{d_tok[cur], n_slots, a, b, d_left, d_right, d_st, d_rec, (uint32_t)rec_cap, 0};
+        uint32_t *tail = d_delta + DELTA_WORDS - 32;  // scratch: encode keeps no counts
+        ScanArgs A{d_tok[cur], n_slots, a, b, d_delta, d_delta + 65536, d_st, d_rec, (uint32_t)rec_cap, 0, tail, tail + 1, Halo{}};
         if (a != b) {
             CHECK(launch_scan(A, (uint64_t)n_slots / 64));
             LAUNCH_OK();
@@ -674,14 +793,14 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
             CHECK(ensure(&d_carry, carry_cap, ntiles, "self carry"));
             zbpe_self_tiles<<<ntiles, SELF_THREADS, 0, stream>>>(d_tok[cur], n_slots, a, d_tile_fn);
             LAUNCH_OK();
-            zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry);
+            zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, nullptr, nullptr);
             LAUNCH_OK();
             zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
             LAUNCH_OK();
         }
         zbpe_apply<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, d_st, X);
         LAUNCH_OK();
-        zbpe_reset_merge<<<1, 256, 0, stream>>>(d_st, d_left, d_right, 0);
+        zbpe_reset_merge<<<1, 256, 0, stream>>>(d_st, d_delta, d_delta + 65536, 0);
         LAUNCH_OK();
         if ((k & 63) == 63) {
             CHECK(sync_state());

@@ -3,9 +3,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <memory>
 #include <string>
 
 #include "../../include/zbpe.h"
+#include "comm.hpp"
 #include "types.hpp"
 
 namespace zbpe { struct ScanArgs; }
@@ -13,6 +15,7 @@ namespace zbpe { struct ScanArgs; }
 namespace zbpe {
 
 constexpr int ARGMAX_MAX_BLOCKS = 1024;
+constexpr size_t DELTA_WORDS = 2 * 65536 + 64;  // left | right | xx | occurrences (+ scratch)
 
 struct Engine {
     int device = 0;
@@ -34,7 +37,18 @@ struct Engine {
 
     // pair table and per-merge scratch
     Tables T{};
-    uint32_t *d_left = nullptr, *d_right = nullptr, *d_hist = nullptr;
+    uint32_t *d_delta = nullptr, *d_hist = nullptr;
+
+    // multi-GPU: this rank's shard and its neighbours' boundary tokens
+    int rank = 0, world = 1;
+    std::unique_ptr<Comm> comm;
+    bool sharded = false;
+    uint32_t shard_offset = 0;  // global position of the shard's first byte
+    int next_byte = -1;         // first byte of the next shard (-1: none)
+    Halo halo0{}, halo{};
+    Boundary *d_bnd_mine = nullptr, *d_bnd_all = nullptr, *h_bnd = nullptr;
+    uint8_t *d_x0 = nullptr;
+    uint32_t *d_shard_fn = nullptr, *d_fns_all = nullptr;
     DevState *d_st = nullptr, *h_st = nullptr;
     uint32_t *d_rec = nullptr;
     size_t rec_cap = 0;
@@ -81,7 +95,8 @@ struct Engine {
     zbpe_status fail(zbpe_status s, const char *fmt, ...);
     template <typename T_>
     zbpe_status ensure(T_ **p, size_t &cap, size_t need, const char *what);
-    zbpe_status upload(const uint8_t *text, size_t n);
+    zbpe_status upload(const uint8_t *text, size_t n, bool shard);
+    zbpe_status init_dist(int rank, int world, std::unique_ptr<Comm> comm);
     zbpe_status train(uint16_t vocab_size, int verbose, uint16_t *out_triples, uint64_t *out_counts,
                       size_t *out_n_merges, zbpe_stats *out_stats);
     zbpe_status encode(const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n, uint16_t *out,
@@ -102,6 +117,8 @@ struct Engine {
     zbpe_status rebuild_hot();
     zbpe_status rebuild_home(uint64_t cap);
     zbpe_status select_ready();
+    void halo_from_boundaries();
+    zbpe_status comm_sum(uint32_t *d, size_t n);
     zbpe_status resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner);
 };
 

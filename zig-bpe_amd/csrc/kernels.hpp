@@ -310,34 +310,63 @@ struct ScanArgs {
     uint32_t *rec;       // occurrence start positions
     uint32_t rec_cap;
     int count_deltas;    // 0: encode mode (records only)
+    uint32_t *xx_out;    // adjacent occurrences (b,a) -> (X,X), summed over ranks
+    uint32_t *occ_out;   // occurrences, summed over ranks
+    Halo halo;           // live tokens beyond the shard (multi-GPU); empty on one GPU
 };
 
-// General occurrence handler (any holes, any position). Returns 1 if (p, next_live(p)) == (a, b).
+// Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
+constexpr int64_t NONE_POS = INT64_MIN;
+__device__ inline uint32_t tok_h(const ScanArgs &A, int64_t p) {
+    if (p >= A.n) return A.halo.right[p - A.n];
+    if (p < 0) return A.halo.left[-p - 1];
+    return A.tok[p];
+}
+__device__ inline int64_t next_live_h(const ScanArgs &A, int64_t p) {
+    if (p < A.n) {
+        const int64_t k = next_live(A.tok, A.n, p);
+        if (k >= 0) return k;
+        return A.halo.nright > 0 ? A.n : NONE_POS;
+    }
+    const int64_t i = p - A.n + 1;
+    return i < A.halo.nright ? A.n + i : NONE_POS;
+}
+__device__ inline int64_t prev_live_h(const ScanArgs &A, int64_t p) {
+    if (p >= 0) {
+        const int64_t k = p > 0 ? prev_live(A.tok, p) : -1;
+        if (k >= 0) return k;
+        return A.halo.nleft > 0 ? -1 : NONE_POS;
+    }
+    const int64_t i = -p;  // p = -1 -> the token before it is left[1]
+    return i < A.halo.nleft ? -(i + 1) : NONE_POS;
+}
+
+// General occurrence handler (any holes, any position, shard boundaries through the halo).
+// Returns 1 if (p, next live) == (a, b).
 __device__ inline int occ_slow(const ScanArgs &A, NeighbourHist &H, int64_t p, uint32_t &xx) {
-    const uint16_t *tok = A.tok;
-    int64_t q = next_live(tok, A.n, p);
-    if (q < 0 || tok[q] != A.b) return 0;
+    const int64_t q = next_live_h(A, p);
+    if (q == NONE_POS || tok_h(A, q) != A.b) return 0;
     if (A.count_deltas) {
-        int64_t l = prev_live(tok, p);
-        if (l >= 0) {
-            uint16_t tl = tok[l];
+        const int64_t l = prev_live_h(A, p);
+        if (l != NONE_POS) {
+            const uint32_t tl = tok_h(A, l);
             bool merged_end = false;
             if (tl == A.b) {
-                int64_t pl = prev_live(tok, l);
-                merged_end = pl >= 0 && tok[pl] == A.a;
+                const int64_t pl = prev_live_h(A, l);
+                merged_end = pl != NONE_POS && tok_h(A, pl) == A.a;
             }
-            if (!merged_end) H.left(tl);
+            if (!merged_end) H.left((uint16_t)tl);
         }
-        int64_t r = next_live(tok, A.n, q);
-        if (r >= 0) {
-            uint16_t tr = tok[r];
+        const int64_t r = next_live_h(A, q);
+        if (r != NONE_POS) {
+            const uint32_t tr = tok_h(A, r);
             bool r_occ = false;
             if (tr == A.a) {
-                int64_t rn = next_live(tok, A.n, r);
-                r_occ = rn >= 0 && tok[rn] == A.b;
+                const int64_t rn = next_live_h(A, r);
+                r_occ = rn != NONE_POS && tok_h(A, rn) == A.b;
             }
             if (r_occ) xx++;
-            else H.right(tr);
+            else H.right((uint16_t)tr);
         }
     }
     return 1;
@@ -390,7 +419,10 @@ __device__ inline uint32_t wave_incl_scan(uint32_t x) {
 __device__ inline void wave_flush_records(const ScanArgs &A, const uint32_t *rec, uint32_t n) {
     const int lane = threadIdx.x & 63;
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&A.st->rec_count, n);
+    if (lane == 0) {
+        base = atomicAdd(&A.st->rec_count, n);
+        atomicAdd(A.occ_out, n);
+    }
     base = (uint32_t)__shfl((int)base, 0);
     for (uint32_t i = lane; i < n; i += 64)
         if (base + i < A.rec_cap) A.rec[base + i] = rec[i];
@@ -543,7 +575,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
     }
     // flush LDS neighbour histograms and the xx count
     xx = wave_sum(xx);
-    if (lane == 0 && xx) atomicAdd(&A.st->xx, xx);
+    if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     if (lane == 0 && any) s_any = 1;
     __syncthreads();
     if (s_any) {
@@ -576,8 +608,8 @@ __global__ void __launch_bounds__(256) zbpe_apply(uint16_t *tok, int64_t n, cons
 // one extra thread handles (b, a) -> (X, X) and the merged pair itself. Groups are padded to whole
 // waves so the wave-aggregated id / hot-list appends see uniform control flow.
 __device__ inline void update_body(const Tables &T, DevState *st, const uint32_t *__restrict__ left,
-                                   const uint32_t *__restrict__ right, uint32_t a, uint32_t b, uint32_t X, uint32_t top_key,
-                                   uint32_t gid) {
+                                   const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
+                                   uint32_t b, uint32_t X, uint32_t top_key, uint32_t gid) {
     const uint32_t nX = (X + 63) & ~63u;
     const uint32_t g = gid / nX, t = gid - g * nX;
     int live_delta = 0;
@@ -609,13 +641,13 @@ __device__ inline void update_body(const Tables &T, DevState *st, const uint32_t
         const bool hot = ok && c >= st->theta;
         const uint32_t j = wave_append(&st->hot_len, hot);
         if (hot && j < T.hot_cap) T.hot[j] = id;
-    } else if (gid >= 4 * nX && gid < 4 * nX + 3) {  // three independent chains for the specials
+    } else if (gid >= 4 * nX && gid < 4 * nX + 3) {  // three independent chains for the specials (xx, occ: all ranks)
         const uint32_t which = gid - 4 * nX;
-        const uint32_t xx = st->xx;
+        const uint32_t xx = tail[0];
         if (which == 0 && xx) pair_dec(T, st, pair_key(b, a), xx);
         if (which == 1 && xx) pair_new(T, st, pair_key(X, X), xx);
         if (which == 2) {
-            const uint32_t occ = st->rec_count;
+            const uint32_t occ = tail[1];
             const uint32_t top_id = ht_find(T, top_key);
             if (top_id == NO_ID) atomicOr(&st->error, 4u);
             else {
@@ -635,24 +667,62 @@ __device__ inline void update_body(const Tables &T, DevState *st, const uint32_t
 __host__ __device__ inline uint32_t update_blocks(uint32_t X) { return (4 * ((X + 63) & ~63u) + 3 + 255) / 256; }
 
 // replaceTopPairWithNewToken in one launch: blocks [0, apply_blocks) rewrite the stream at the
-// recorded occurrences (X at the start, a hole at the consumed b), the rest update the counts.
-__global__ void __launch_bounds__(256) zbpe_replace(uint16_t *tok, int64_t n, const uint32_t *__restrict__ rec,
-                                                    uint32_t rec_cap, Tables T, DevState *st, const uint32_t *__restrict__ left,
-                                                    const uint32_t *__restrict__ right, uint32_t a, uint32_t b, uint32_t X,
-                                                    uint32_t top_key, uint32_t apply_blocks) {
-    if (blockIdx.x < apply_blocks) {
-        const uint32_t cnt = min(st->rec_count, rec_cap);
-        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += apply_blocks * 256) {
-            const int64_t p = rec[i];
-            tok[p] = (uint16_t)X;
-            const int64_t q = next_live(tok, n, p);
-            if (q >= 0) tok[q] = HOLE;
+// recorded occurrences (X at the start, a hole at the consumed b), the rest update the counts
+// (identical on every rank: the deltas were summed), and one thread checks whether this shard's
+// first live token is the b of an occurrence owned by the left rank (then it becomes a hole).
+struct ReplaceArgs {
+    uint16_t *tok;
+    int64_t n;
+    const uint32_t *rec;
+    uint32_t rec_cap;
+    const uint32_t *left, *right, *tail;  // summed deltas; tail = {xx, occurrences}
+    uint32_t a, b, X, top_key;
+    uint32_t apply_blocks;
+    Halo halo;
+    const uint8_t *x0;  // self pairs: parity of the run of a's entering the shard (nullptr: none)
+};
+__global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, DevState *st) {
+    if (blockIdx.x < R.apply_blocks) {
+        const uint32_t cnt = min(st->rec_count, R.rec_cap);
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += R.apply_blocks * 256) {
+            const int64_t p = R.rec[i];
+            R.tok[p] = (uint16_t)R.X;
+            const int64_t q = next_live(R.tok, R.n, p);
+            if (q >= 0) R.tok[q] = HOLE;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->consumed = 0;
+            if (R.halo.nleft > 0 || R.x0) {
+                const int64_t f = next_live(R.tok, R.n, -1);
+                if (f >= 0) {
+                    const uint32_t tf = R.tok[f];
+                    const bool c = R.a != R.b ? (R.halo.nleft > 0 && R.halo.left[0] == R.a && tf == R.b)
+                                              : (tf == R.a && R.x0 && (*R.x0 & 1));
+                    if (c) {
+                        R.tok[f] = HOLE;
+                        st->consumed = 1;
+                    }
+                }
+            }
         }
         return;
     }
-    update_body(T, st, left, right, a, b, X, top_key, (blockIdx.x - apply_blocks) * 256 + threadIdx.x);
+    update_body(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, (blockIdx.x - R.apply_blocks) * 256 + threadIdx.x);
 }
 
+// this shard's boundary record: first 3 / last 2 live tokens (holes skipped) and its live count
+__global__ void zbpe_boundary(const uint16_t *__restrict__ tok, int64_t n, int64_t nlive, Boundary *out) {
+    if (threadIdx.x || blockIdx.x) return;
+    Boundary B{};
+    for (int k = 0; k < 3; k++) B.first[k] = HOLE;
+    B.last[0] = B.last[1] = HOLE;
+    for (int64_t p = 0; p < n && B.nfirst < 3; p++)
+        if (tok[p] != HOLE) B.first[B.nfirst++] = tok[p];
+    for (int64_t p = n - 1; p >= 0 && B.nlast < 2; p--)
+        if (tok[p] != HOLE) B.last[B.nlast++] = tok[p];
+    B.nlive = (uint32_t)nlive;
+    *out = B;
+}
 // end of merge: clear the neighbour histograms [0, X) and roll the per-merge counters
 __global__ void __launch_bounds__(256) zbpe_reset_merge(DevState *st, uint32_t *left, uint32_t *right, uint32_t X) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
@@ -698,8 +768,11 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_self_tiles(const uint16_t *
     }
 }
 // carry_in[t] = parity of the a-run entering tile t. One block; each thread composes a segment.
+// carry_in[t] = parity of the a-run entering tile t, starting from *x0 (the run entering the shard
+// from the ranks to the left; nullptr = 0). shard_fn (optional) = the whole shard as one function.
 __global__ void __launch_bounds__(1024) zbpe_self_carry(const uint8_t *__restrict__ tile_fn, int64_t ntiles,
-                                                        uint8_t *__restrict__ carry_in) {
+                                                        uint8_t *__restrict__ carry_in, const uint8_t *x0,
+                                                        uint32_t *shard_fn) {
     // function of a tile: x -> all_a ? x ^ p : p   (x, p parities)
     __shared__ uint8_t s_all[1024], s_par[1024];
     const int64_t per = (ntiles + 1023) / 1024;
@@ -714,12 +787,15 @@ __global__ void __launch_bounds__(1024) zbpe_self_carry(const uint8_t *__restric
     s_par[threadIdx.x] = par;
     __syncthreads();
     if (threadIdx.x == 0) {  // sequential exclusive composition over 1024 segments
-        uint8_t x = 0;
+        uint8_t x = x0 ? (*x0 & 1) : 0, A = 1, P = 0;
         for (int t = 0; t < 1024; t++) {
+            if (s_all[t]) P ^= s_par[t];
+            else { A = 0; P = s_par[t]; }
             uint8_t nx = s_all[t] ? (x ^ s_par[t]) : s_par[t];
             s_par[t] = x;  // carry into segment t
             x = nx;
         }
+        if (shard_fn) *shard_fn = (uint32_t)A | ((uint32_t)P << 1);
     }
     __syncthreads();
     uint8_t x = s_par[threadIdx.x];
@@ -728,6 +804,16 @@ __global__ void __launch_bounds__(1024) zbpe_self_carry(const uint8_t *__restric
         uint8_t f = tile_fn[t], fa = f & 1, fp = (f >> 1) & 1;
         x = fa ? (x ^ fp) : fp;
     }
+}
+// parity of the a-run entering shard `rank` from the gathered whole-shard functions of ranks < rank
+__global__ void zbpe_self_x0(const uint32_t *__restrict__ fns, int rank, uint8_t *x0) {
+    if (threadIdx.x || blockIdx.x) return;
+    uint8_t x = 0;
+    for (int r = 0; r < rank; r++) {
+        const uint32_t f = fns[r];
+        x = (f & 1) ? (x ^ ((f >> 1) & 1)) : ((f >> 1) & 1);
+    }
+    *x0 = x;
 }
 __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A, const uint8_t *__restrict__ carry_in) {
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
@@ -764,17 +850,23 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A, const
         if (tok[p] != a) { lastna = rel; continue; }
         uint32_t off_par = lastna >= 0 ? (uint32_t)((rel - lastna - 1) & 1) : ((carry + (uint32_t)rel) & 1);
         if (off_par) continue;
-        if (p + 1 >= n || tok[p + 1] != a) continue;
+        // the shard is compacted: positions past its end continue in the right halo, before it in the left
+        auto at = [&](int64_t q) -> uint32_t {
+            if (q < n) return q >= 0 ? tok[q] : (-q - 1 < A.halo.nleft ? A.halo.left[-q - 1] : HOLE);
+            return q - n < A.halo.nright ? A.halo.right[q - n] : HOLE;
+        };
+        if (at(p + 1) != a) continue;
         // occurrence at p
         if (A.count_deltas) {
             // offset 0 in the run: the left neighbour is not the end of a previous occurrence
-            const bool run_start = lastna >= 0 ? (rel - lastna - 1 == 0) : (rel == 0 && (p == 0 || tok[p - 1] != a));
-            if (run_start && p > 0) H.left(tok[p - 1]);
-            if (p + 2 < n) {
-                uint16_t tr = tok[p + 2];
-                bool r_occ = (tr == a) && (p + 3 < n) && (tok[p + 3] == a);
+            const bool run_start = lastna >= 0 ? (rel - lastna - 1 == 0) : (rel == 0 && at(p - 1) != a);
+            const uint32_t tl = at(p - 1);
+            if (run_start && tl != HOLE) H.left((uint16_t)tl);
+            const uint32_t tr = at(p + 2);
+            if (tr != HOLE) {
+                const bool r_occ = (tr == a) && (at(p + 3) == a);
                 if (r_occ) xx++;
-                else H.right(tr);
+                else H.right((uint16_t)tr);
             }
         }
         uint32_t slot = atomicAdd(&s_nrec, 1u);
@@ -783,7 +875,10 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A, const
     __syncthreads();
     const uint32_t nrec = s_nrec;
     if (nrec) {
-        if (threadIdx.x == 0) s_base = atomicAdd(&A.st->rec_count, nrec);
+        if (threadIdx.x == 0) {
+            s_base = atomicAdd(&A.st->rec_count, nrec);
+            atomicAdd(A.occ_out, nrec);
+        }
         __syncthreads();
         const uint32_t base = s_base;
         for (uint32_t i = threadIdx.x; i < nrec; i += SELF_THREADS)
@@ -791,7 +886,7 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A, const
         if (threadIdx.x == 0 && base + nrec > A.rec_cap) atomicOr(&A.st->error, 8u);
     }
     xx = wave_sum(xx);
-    if ((threadIdx.x & 63) == 0 && xx) atomicAdd(&A.st->xx, xx);
+    if ((threadIdx.x & 63) == 0 && xx) atomicAdd(A.xx_out, xx);
     if (nrec) {
         for (int i = threadIdx.x; i < LDS_BINS; i += SELF_THREADS) {
             uint32_t l = s_left[i], r = s_right[i];
@@ -923,12 +1018,9 @@ __global__ void __launch_bounds__(256) zbpe_hot_build(Tables T, DevState *st) {
 // stream's last-pair count, and the end-of-merge resets (neighbour histograms, counters) when
 // roll != 0. One launch per merge instead of three.
 __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState *st, MaxRec *__restrict__ partial,
-                                                              const uint16_t *__restrict__ tok, int64_t n, uint32_t *left,
-                                                              uint32_t *right, uint32_t X, int roll) {
-    for (uint32_t t = blockIdx.x * ARGMAX_THREADS + threadIdx.x; t < X; t += gridDim.x * ARGMAX_THREADS) {
-        left[t] = 0;
-        right[t] = 0;
-    }
+                                                              const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
+                                                              uint32_t X, int roll, const Boundary *__restrict__ bnd, int world) {
+    for (uint32_t t = blockIdx.x * ARGMAX_THREADS + threadIdx.x; t < 2 * X; t += gridDim.x * ARGMAX_THREADS) delta[t] = 0;
     const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
     MaxRec r{0, 0, NO_ID};
     for (uint32_t i = blockIdx.x * ARGMAX_THREADS + threadIdx.x; i < nh; i += gridDim.x * ARGMAX_THREADS) {
@@ -967,17 +1059,24 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
         st->top_id = q.id;
         st->top_key = q.id != NO_ID ? T.id_key[q.id] : EMPTY_KEY;
         if (q.ties > 1) {
-            int64_t j = n - 1;
-            while (j >= 0 && tok[j] == HOLE) j--;
-            int64_t i = j - 1;
-            while (i >= 0 && tok[i] == HOLE) i--;
-            st->lastpair_count = i >= 0 ? ht_find_count(T, pair_key(tok[i], tok[j])) : 0;
+            uint32_t lt[2];  // last live token of the whole stream, then the one before
+            int got = 0;
+            if (world > 1) {
+                for (int r = world - 1; r >= 0 && got < 2; r--)
+                    for (int k = 0; k < bnd[r].nlast && got < 2; k++) lt[got++] = bnd[r].last[k];
+            } else {
+                for (int64_t p = n - 1; p >= 0 && got < 2; p--)
+                    if (tok[p] != HOLE) lt[got++] = tok[p];
+            }
+            st->lastpair_count = got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0;
         }
         if (roll) {
+            uint32_t *tail = delta + 2 * X;
             st->last_occ = st->rec_count;
             st->total_occ += st->rec_count;
+            st->last_gocc = tail[1];
             st->rec_count = 0;
-            st->xx = 0;
+            tail[0] = tail[1] = 0;
         }
         st->ticket = 0;
     }
@@ -1202,16 +1301,15 @@ __global__ void __launch_bounds__(256) zbpe_home_build(Tables T, DevState *st) {
 }
 
 // exact fallback: first occurrence position of every live pair in the current stream
-__global__ void __launch_bounds__(256) zbpe_first_occ(const uint16_t *__restrict__ tok, int64_t n, Tables T, uint32_t *first,
-                                                      DevState *st) {
-    for (int64_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
-        uint16_t x = tok[p];
+__global__ void __launch_bounds__(256) zbpe_first_occ(ScanArgs A, uint32_t offset, Tables T, uint32_t *first, DevState *st) {
+    for (int64_t p = blockIdx.x * 256 + threadIdx.x; p < A.n; p += (int64_t)gridDim.x * 256) {
+        const uint16_t x = A.tok[p];
         if (x == HOLE) continue;
-        int64_t q = next_live(tok, n, p);
-        if (q < 0) continue;
-        uint32_t id = ht_find(T, pair_key(x, tok[q]));
+        const int64_t q = next_live_h(A, p);  // the pair leaving the shard is owned here
+        if (q == NONE_POS) continue;
+        const uint32_t id = ht_find(T, pair_key(x, tok_h(A, q)));
         if (id == NO_ID) { atomicOr(&st->error, 4u); continue; }
-        atomicMin(&first[id], (uint32_t)p);
+        atomicMin(&first[id], offset + (uint32_t)p);
     }
 }
 __global__ void __launch_bounds__(256) zbpe_gather_live(Tables T, const uint32_t *__restrict__ first, DevState *st,

@@ -41,6 +41,9 @@ struct DevState {
     uint32_t hot_len;        // ids appended to the hot list (may exceed its capacity -> rebuild)
     uint32_t dirty_len;      // home-histogram blocks changed since their summaries were computed
     uint32_t ticket;         // zbpe_select: blocks done (the last one reduces), reset by it
+    uint32_t last_gocc;      // occurrences merged by the last merge on all ranks
+    uint32_t consumed;       // 1: this shard's first live token was the b of the left rank's last occurrence
+    uint32_t pad2[2];
 };
 
 struct Tables {
@@ -62,6 +65,23 @@ constexpr int COUNT_BINS = 64 + 26 * 32;  // count histogram for choosing theta:
 constexpr int SUMM_SLOTS = 4096;          // home-histogram slots per max-plus block summary
 constexpr int SUPER_BLOCKS = 64;          // block summaries per super-block summary
 struct Summ { int64_t q, m; };            // carry function c -> max(m, c + q) of a run of slots
+
+// Live tokens just outside this rank's shard (multi-GPU): left[0] is the last live token before the
+// shard, left[1] the one before it; right[0..2] the first live tokens after it.
+struct Halo {
+    uint16_t left[2];
+    uint16_t right[3];
+    uint8_t nleft, nright;
+};
+// Per-rank boundary record exchanged after every merge (16 B): first 3 / last 2 live tokens and
+// the live-token count of the shard.
+struct Boundary {
+    uint16_t first[3];
+    uint16_t last[2];
+    uint8_t nfirst, nlast;
+    uint32_t nlive;
+};
+static_assert(sizeof(Boundary) == 16, "Boundary is exchanged as 16 bytes");
 
 struct MaxRec { uint32_t cnt, ties, id; };
 struct LiveRec { uint32_t first_pos, key, count, pad; };

@@ -134,12 +134,42 @@ class Stats(ctypes.Structure):
 
 
 EXPORTS = (
-    "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_destroy", "zbpe_last_error",
+    "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_create_dist_host", "zbpe_destroy", "zbpe_last_error",
     "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts",
     "zbpe_set_option", "zbpe_bench_scan", "zbpe_zig_order_winner", "zbpe_version",
 )
 
 _lib = None
+COLLECTIVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t)
+
+
+def torch_collective(rank: int, world: int, group=None):
+    """zbpe_collective_fn over torch.distributed (e.g. gloo on the CPU): op 0 sum / op 1 min of u32
+    in place, op 2 all-gather of `count` bytes per rank. Used by zbpe_create_dist_host."""
+    import torch
+    import torch.distributed as dist
+
+    def cb(_user, op, buf, count):
+        try:
+            if op in (0, 1):
+                arr = np.ctypeslib.as_array((ctypes.c_uint32 * count).from_address(buf))
+                t = torch.from_numpy(arr.astype(np.int64))
+                dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MIN, group=group)
+                arr[:] = (t.numpy() & 0xFFFFFFFF).astype(np.uint32)
+            elif op == 2:
+                arr = np.ctypeslib.as_array((ctypes.c_uint8 * (count * world)).from_address(buf))
+                mine = torch.from_numpy(arr[rank * count:(rank + 1) * count].copy())
+                outs = [torch.empty_like(mine) for _ in range(world)]
+                dist.all_gather(outs, mine, group=group)
+                arr[:] = torch.cat(outs).numpy()
+            else:
+                return 2
+            return 0
+        except Exception as e:  # noqa: BLE001 -- reported to the C side as a failed collective
+            sys.stderr.write(f"zbpe collective op {op} failed: {e}\n")
+            return 1
+
+    return COLLECTIVE_FN(cb)
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -154,6 +184,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.zbpe_comm_unique_id.argtypes = [vp]
     L.zbpe_create_dist.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
+    L.zbpe_create_dist_host.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, COLLECTIVE_FN, vp, ctypes.POINTER(vp)]
     L.zbpe_destroy.argtypes = [vp]
     L.zbpe_destroy.restype = None
     L.zbpe_last_error.argtypes = [vp]
@@ -182,11 +213,17 @@ def _ptr(a: np.ndarray):
 class Engine:
     """One device context (one GPU). Thin wrapper over the C ABI; not re-entrant (like the reference)."""
 
-    def __init__(self, device: int = 0, rank: int = 0, world: int = 1, unique_id: Optional[bytes] = None):
+    def __init__(self, device: int = 0, rank: int = 0, world: int = 1, unique_id: Optional[bytes] = None,
+                 collective=None):
+        """world > 1: RCCL with `unique_id` (from comm_unique_id() on rank 0), or a host `collective`
+        (torch_collective(rank, world)) so several ranks can share one GPU."""
         self._L = load_library()
         self._ctx = ctypes.c_void_p()
-        if world == 1:
+        self._collective = collective  # keep the callback alive
+        if world == 1 and collective is None:
             st = self._L.zbpe_create(device, ctypes.byref(self._ctx))
+        elif collective is not None:
+            st = self._L.zbpe_create_dist_host(device, rank, world, collective, None, ctypes.byref(self._ctx))
         else:
             uid = ctypes.create_string_buffer(unique_id or b"", 128)
             st = self._L.zbpe_create_dist(device, rank, world, uid, ctypes.byref(self._ctx))
@@ -485,5 +522,5 @@ __all__ = [
     "BasicTokenizer", "CharPair", "Merge", "Merges", "Engine", "Stats", "TrainError", "InvalidVocabSize", "InvalidUtf8",
     "OutOfMemory", "DeviceError", "InvalidToken", "InvalidFormat", "InvalidCharacter", "Overflow", "StreamTooLong",
     "InvalidArgument", "InternalError", "load_library", "synth_corpus", "comm_unique_id", "zig_order_winner",
-    "merges_to_text", "vocabStart", "EXPORTS",
+    "merges_to_text", "vocabStart", "EXPORTS", "torch_collective", "COLLECTIVE_FN",
 ]
