@@ -37,6 +37,8 @@ def parse():
     p.add_argument("--cpu-sample-merges", type=int, default=2)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--stats-out", default="")
+    p.add_argument("--share-gpu", action="store_true",
+                   help="all ranks on cuda:0 with host (gloo) collectives -- rehearses N>1 on one GPU")
     return p.parse_args()
 
 
@@ -79,13 +81,24 @@ def main():
     if args.gpus != world:
         world = args.gpus if world == 1 and args.gpus == 1 else world
     dist = None
+    comm_backend = "none"
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
         dist.init_process_group("gloo", init_method="env://")
-        uid = [zbpe.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng = zbpe.Engine(local_rank, rank=rank, world=world, unique_id=uid[0])
+        if args.share_gpu:
+            eng = zbpe.Engine(0, rank=rank, world=world, collective=zbpe.torch_collective(rank, world))
+            comm_backend = "gloo (host collectives, ranks share cuda:0)"
+        else:
+            uid = [zbpe.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            try:
+                eng = zbpe.Engine(local_rank, rank=rank, world=world, unique_id=uid[0])
+                comm_backend = "rccl"
+            except zbpe.ZbpeError as e:  # keep the GPU compute path; move only the exchange to gloo
+                sys.stderr.write(f"rank {rank}: RCCL init failed ({e}); using host (gloo) collectives\n")
+                eng = zbpe.Engine(local_rank, rank=rank, world=world, collective=zbpe.torch_collective(rank, world))
+                comm_backend = "gloo (host collectives; RCCL init failed)"
     else:
         eng = zbpe.Engine(0)
 
@@ -142,7 +155,8 @@ def main():
                     f"{args.n_bytes} bytes; no Wikipedia dump offline",
             "config": {"workload": "C4: train vocab_size=%d on a %d-byte corpus" % (args.vocab, args.n_bytes),
                        "corpus_bytes": args.n_bytes, "vocab_size": args.vocab, "merges": merges,
-                       "parallelism": "single GPU" if world == 1 else f"token stream sharded x{world}"},
+                       "parallelism": "single GPU" if world == 1 else f"token stream sharded x{world}",
+                       "comm": comm_backend},
             "roofline": {
                 "kernel": "zbpe_scan_pairs",
                 "bound": "hbm",

@@ -689,10 +689,18 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             stats.replace_pair_calls++;
         }
         if (world > 1) halo_from_boundaries();
+        if (debug_checks) {
+            uint64_t bad = 0;
+            uint32_t info[3] = {0, 0, 0};
+            CHECK(recount_check(&bad, info));
+            if (bad)
+                return fail(ZBPE_INTERNAL, "merge %u (%u,%u): %llu pair counts differ from a full recount (first: key (%u,%u) table %u, recount %u)",
+                            X, a, b, (unsigned long long)bad, info[0] & 0xFFFF, info[0] >> 16, info[1], info[2]);
+        }
         const uint32_t gocc = h_st->last_gocc;
         if (!self && gocc != top)
             return fail(ZBPE_INTERNAL, "merge %u: scan found %u occurrences of (%u,%u), count was %u", X, gocc, a, b, top);
-        const uint64_t gone = (uint64_t)h_st->last_occ + h_st->consumed;  // slots of this shard that became holes
+        const uint64_t gone = h_st->last_holes;  // slots of this shard that became holes
         n_live -= gone;
         holes += gone;
         if (holes * compact_den > (uint64_t)n_slots) {
@@ -741,19 +749,56 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
 
 zbpe_status Engine::verify_counts(uint64_t *mismatches) {
     if (!trained) return fail(ZBPE_INVALID_ARGUMENT, "verify_counts needs a trained context");
-    if (world > 1) return fail(ZBPE_INVALID_ARGUMENT, "verify_counts is single-GPU only");
+    return recount_check(mismatches, nullptr);
+}
+
+// Full recount of the current stream against the incremental table. Multi-GPU: each shard
+// recounts the pairs it owns; ids differ between ranks but the key sets are identical, so the
+// per-rank recounts line up in key order and one all-reduce sums them.
+zbpe_status Engine::recount_check(uint64_t *mismatches, uint32_t *first_bad_key) {
     HIP_OK(hipSetDevice(device));
     CHECK(sync_state());
     const uint32_t nid = h_st->num_ids;
     CHECK(ensure(&d_recount, recount_cap, std::max<uint32_t>(nid, 1), "recount"));
     HIP_OK(hipMemsetAsync(d_recount, 0, (size_t)std::max<uint32_t>(nid, 1) * 4, stream));
     HIP_OK(hipMemsetAsync(&d_st->mismatches, 0, 4, stream));
-    zbpe_recount<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, T, d_recount, d_st);
+    ScanArgs A{d_tok[cur], n_slots, 0, 0, nullptr, nullptr, d_st, nullptr, 0, 0, nullptr, nullptr, halo};
+    zbpe_recount<<<2048, 256, 0, stream>>>(A, T, d_recount, d_st);
     LAUNCH_OK();
-    zbpe_recount_compare<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_recount, d_st);
+    if (world == 1) {
+        zbpe_recount_compare<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_recount, d_st);
+        LAUNCH_OK();
+        CHECK(sync_state());
+        *mismatches = h_st->mismatches;
+        return ZBPE_OK;
+    }
+    uint32_t *d_dump = nullptr;
+    HIP_OK(hipMalloc(&d_dump, (size_t)nid * 12 + 16));
+    zbpe_recount_dump<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_recount, d_st, d_dump);
     LAUNCH_OK();
-    CHECK(sync_state());
-    *mismatches = h_st->mismatches;
+    std::vector<uint32_t> dump((size_t)nid * 3);
+    HIP_OK(hipMemcpyAsync(dump.data(), d_dump, (size_t)nid * 12, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    std::vector<uint32_t> order(nid);
+    for (uint32_t i = 0; i < nid; i++) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return dump[3 * x] < dump[3 * y]; });
+    std::vector<uint32_t> rc(nid + 1);
+    for (uint32_t i = 0; i < nid; i++) rc[i] = dump[3 * order[i] + 2];
+    rc[nid] = h_st->mismatches;
+    HIP_OK(hipMemcpyAsync(d_dump, rc.data(), (size_t)(nid + 1) * 4, hipMemcpyHostToDevice, stream));
+    if (!comm->allreduce_u32(d_dump, nid + 1, COMM_SUM_U32, stream)) { (void)hipFree(d_dump); return fail(ZBPE_COMM_ERROR, "recount all-reduce failed"); }
+    HIP_OK(hipMemcpyAsync(rc.data(), d_dump, (size_t)(nid + 1) * 4, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    (void)hipFree(d_dump);
+    uint64_t bad = rc[nid];
+    for (uint32_t i = 0; i < nid; i++) {
+        const uint32_t id = order[i];
+        if (rc[i] != dump[3 * id + 1]) {
+            if (!bad && first_bad_key) { first_bad_key[0] = dump[3 * id]; first_bad_key[1] = dump[3 * id + 1]; first_bad_key[2] = rc[i]; }
+            bad++;
+        }
+    }
+    *mismatches = bad;
     return ZBPE_OK;
 }
 

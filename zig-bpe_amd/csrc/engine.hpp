@@ -119,6 +119,7 @@ struct Engine {
     zbpe_status select_ready();
     void halo_from_boundaries();
     zbpe_status comm_sum(uint32_t *d, size_t n);
+    zbpe_status recount_check(uint64_t *mismatches, uint32_t *first_bad_key);
     zbpe_status resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner);
 };
 

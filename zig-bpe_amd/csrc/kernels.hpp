@@ -684,12 +684,18 @@ struct ReplaceArgs {
 __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, DevState *st) {
     if (blockIdx.x < R.apply_blocks) {
         const uint32_t cnt = min(st->rec_count, R.rec_cap);
+        uint32_t made = 0;  // an occurrence whose b lies in the next shard makes no hole here
         for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += R.apply_blocks * 256) {
             const int64_t p = R.rec[i];
             R.tok[p] = (uint16_t)R.X;
             const int64_t q = next_live(R.tok, R.n, p);
-            if (q >= 0) R.tok[q] = HOLE;
+            if (q >= 0) {
+                R.tok[q] = HOLE;
+                made++;
+            }
         }
+        made = wave_sum(made);
+        if ((threadIdx.x & 63) == 0 && made) atomicAdd(&st->holes_made, made);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->consumed = 0;
             if (R.halo.nleft > 0 || R.x0) {
@@ -701,6 +707,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
                     if (c) {
                         R.tok[f] = HOLE;
                         st->consumed = 1;
+                        atomicAdd(&st->holes_made, 1u);
                     }
                 }
             }
@@ -1075,6 +1082,8 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
             st->last_occ = st->rec_count;
             st->total_occ += st->rec_count;
             st->last_gocc = tail[1];
+            st->last_holes = st->holes_made;
+            st->holes_made = 0;
             st->rec_count = 0;
             tail[0] = tail[1] = 0;
         }
@@ -1324,16 +1333,25 @@ __global__ void __launch_bounds__(256) zbpe_gather_live(Tables T, const uint32_t
 }
 
 // verification: recount every live pair of the stream and compare with the maintained counts
-__global__ void __launch_bounds__(256) zbpe_recount(const uint16_t *__restrict__ tok, int64_t n, Tables T, uint32_t *recount,
-                                                    DevState *st) {
-    for (int64_t p = blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
-        uint16_t x = tok[p];
+// recount every pair this shard owns (the pair leaving the shard included, through the halo)
+__global__ void __launch_bounds__(256) zbpe_recount(ScanArgs A, Tables T, uint32_t *recount, DevState *st) {
+    for (int64_t p = blockIdx.x * 256 + threadIdx.x; p < A.n; p += (int64_t)gridDim.x * 256) {
+        const uint16_t x = A.tok[p];
         if (x == HOLE) continue;
-        int64_t q = next_live(tok, n, p);
-        if (q < 0) continue;
-        uint32_t id = ht_find(T, pair_key(x, tok[q]));
+        const int64_t q = next_live_h(A, p);
+        if (q == NONE_POS) continue;
+        const uint32_t id = ht_find(T, pair_key(x, tok_h(A, q)));
         if (id == NO_ID) { atomicAdd(&st->mismatches, 1u); continue; }
         atomicAdd(&recount[id], 1u);
+    }
+}
+// (key, table count, this shard's recount) of every id, for the cross-rank comparison
+__global__ void __launch_bounds__(256) zbpe_recount_dump(Tables T, const uint32_t *recount, const DevState *st, uint32_t *out) {
+    const uint32_t n = min(st->num_ids, T.id_cap);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        out[3 * i] = T.id_key[i];
+        out[3 * i + 1] = T.id_cnt[i];
+        out[3 * i + 2] = recount[i];
     }
 }
 __global__ void __launch_bounds__(256) zbpe_recount_compare(Tables T, const uint32_t *recount, DevState *st) {

@@ -43,7 +43,8 @@ struct DevState {
     uint32_t ticket;         // zbpe_select: blocks done (the last one reduces), reset by it
     uint32_t last_gocc;      // occurrences merged by the last merge on all ranks
     uint32_t consumed;       // 1: this shard's first live token was the b of the left rank's last occurrence
-    uint32_t pad2[2];
+    uint32_t holes_made;     // slots of this shard turned into holes by the current merge
+    uint32_t last_holes;     // holes_made of the last merge (rolled by zbpe_select)
 };
 
 struct Tables {
