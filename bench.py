@@ -165,7 +165,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": None,
-                "note": "achieved = sum over launches of 2 B x live tokens scanned / sum of launch durations (HIP events "
+                "note": "per GPU (rank 0): achieved = sum over launches of 2 B x live tokens scanned / sum of launch durations (HIP events "
                         "on the engine stream); bytes actually streamed incl. holes: %.3g" % (read_bytes / max(alg_bytes, 1)),
             },
             "pair_count_GBps": achieved,

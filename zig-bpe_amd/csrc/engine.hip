@@ -720,23 +720,25 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     stats.sort_pairs_s = ev_select;
     stats.replace_pair_s = ev_replace;
     stats.final_tokens = (uint64_t)n_live;
-    if (world > 1) {  // stream lengths are per shard: sum them
-        uint64_t v[4] = {stats.final_tokens, stats.sum_tokens, stats.scan_alg_bytes, stats.scan_read_bytes};
-        uint32_t w[8];
-        for (int i = 0; i < 4; i++) { w[2 * i] = (uint32_t)v[i]; w[2 * i + 1] = (uint32_t)(v[i] >> 32); }
-        // exact u64 sums from u32 halves: sum low halves with carries folded in on the host
+    if (world > 1) {  // stream lengths are per shard: sum them (scan bytes stay per rank, like scan time)
+        uint64_t v[2] = {stats.final_tokens, stats.sum_tokens};
+        uint32_t w[8] = {0};
+        for (int i = 0; i < 2; i++) {  // exact u64 sums from 16-bit limbs (<= 2^16 ranks)
+            w[4 * i] = (uint32_t)(v[i] & 0xFFFF);
+            w[4 * i + 1] = (uint32_t)((v[i] >> 16) & 0xFFFF);
+            w[4 * i + 2] = (uint32_t)((v[i] >> 32) & 0xFFFF);
+            w[4 * i + 3] = (uint32_t)(v[i] >> 48);
+        }
         uint32_t *d_w = d_delta + DELTA_WORDS - 16;
-        uint32_t lo[8], hi[8];
-        for (int i = 0; i < 4; i++) { lo[2 * i] = w[2 * i] & 0xFFFF; lo[2 * i + 1] = w[2 * i] >> 16; hi[2 * i] = w[2 * i + 1]; hi[2 * i + 1] = 0; }
-        HIP_OK(hipMemcpyAsync(d_w, lo, 32, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipMemcpyAsync(d_w + 8, hi, 32, hipMemcpyHostToDevice, stream));
-        CHECK(comm_sum(d_w, 16));
-        HIP_OK(hipMemcpyAsync(lo, d_w, 32, hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipMemcpyAsync(hi, d_w + 8, 32, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipMemcpyAsync(d_w, w, 32, hipMemcpyHostToDevice, stream));
+        CHECK(comm_sum(d_w, 8));
+        HIP_OK(hipMemcpyAsync(w, d_w, 32, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
-        for (int i = 0; i < 4; i++) v[i] = (uint64_t)lo[2 * i] + ((uint64_t)lo[2 * i + 1] << 16) + ((uint64_t)hi[2 * i] << 32);
-        stats.final_tokens = v[0]; stats.sum_tokens = v[1]; stats.scan_alg_bytes = v[2]; stats.scan_read_bytes = v[3];
-        HIP_OK(hipMemsetAsync(d_w, 0, 64, stream));
+        for (int i = 0; i < 2; i++)
+            v[i] = (uint64_t)w[4 * i] + ((uint64_t)w[4 * i + 1] << 16) + ((uint64_t)w[4 * i + 2] << 32) + ((uint64_t)w[4 * i + 3] << 48);
+        stats.final_tokens = v[0];
+        stats.sum_tokens = v[1];
+        HIP_OK(hipMemsetAsync(d_w, 0, 32, stream));
     }
     stats.total_s = now_s() - t_start;
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
