@@ -46,8 +46,8 @@ typedef struct zbpe_stats {
     uint64_t count_pairs_calls, sort_pairs_calls, replace_pair_calls;
     /* dominant kernel (zbpe_scan_pairs) measured with HIP events on the engine's stream */
     uint64_t scan_launches;
-    double scan_kernel_s;     /* sum of scan kernel durations */
-    uint64_t scan_alg_bytes;  /* algorithmic bytes: 2 B per live token scanned */
+    double scan_kernel_s;     /* sum of the timed scan kernel durations (see scan_timed_launches) */
+    uint64_t scan_alg_bytes;  /* algorithmic bytes of every scan: 2 B per live token */
     uint64_t scan_read_bytes; /* bytes the scan actually streamed (live tokens + holes) */
     uint64_t tie_iterations;  /* merges whose top count was shared by >1 pair */
     uint64_t tie_fallbacks;   /* ties resolved by the exact first-occurrence emulation */
@@ -57,6 +57,10 @@ typedef struct zbpe_stats {
     uint64_t distinct_pairs;  /* live pairs after the last merge */
     uint64_t pair_ids;        /* pair-table ids allocated (live + dead) */
     uint64_t sum_tokens;      /* sum over merges of the stream length n_t */
+    /* scan launches timed with HIP events (every merge_timing-th merge of a device-resident batch,
+     * every merge on the synchronous path) and their algorithmic bytes: scan_kernel_s covers these */
+    uint64_t scan_timed_launches;
+    uint64_t scan_timed_alg_bytes;
 } zbpe_stats;
 
 /* Create a single-GPU context on HIP device `device`. */
@@ -107,13 +111,24 @@ zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches);
  * first-occurrence emulation and cross-check the GPU cluster test), "compact_den" (compact when
  * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..4: unroll 4/8, non-temporal
  * loads; see engine.hip kScanVariants), "scan_auto" (0/1: per merge, plain loads instead of
- * non-temporal ones when matches are dense), "hot_target" (ids kept by the argmax hot list). */
+ * non-temporal ones when matches are dense), "hot_target" (ids kept by the argmax hot list),
+ * "block_skip" (0/1: stream only the 8192-slot blocks that hold the pair's rarer token),
+ * "trace" (0/1: record per-merge timings, see zbpe_trace), "merge_batch" (merges enqueued per host
+ * sync, 1 = synchronous loop), "merge_timing" (time every N-th merge of a batch with HIP events;
+ * 0 = none), "replace_split" (profiling: apply and count update as separate launches). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* Benchmark diagnostic: time `reps` launches of the pair-scan kernel for pair (a, b), a != b, over
  * the stream of the uploaded corpus (zbpe_upload) as it stands; the first launch is not timed.
  * *gbps = 2 B per stream slot / average launch time. */
 zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, double *avg_ms, double *gbps);
+
+/* Profiling diagnostic: with option "trace" = 1, train records one row of ZBPE_TRACE_COLS floats per
+ * merge: {merge index, count, live tokens, stream slots, slots streamed by the scan, scan ms,
+ * replace ms, select ms, wall ms of the merge, self pair (0/1), ties}. Copies up to `cap_rows`
+ * rows of the last train into `rows`; returns the number of rows recorded in *n_rows. */
+#define ZBPE_TRACE_COLS 11
+zbpe_status zbpe_trace(zbpe_ctx *ctx, float *rows, size_t cap_rows, size_t *n_rows);
 
 /* Host-only diagnostic (no device work): the Zig 0.13 pair-map iteration order emulation used by
  * the exact tie fallback. Given every live pair's first-occurrence position, key (first |

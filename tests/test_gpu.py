@@ -111,6 +111,22 @@ def test_debug_checks_hot_list_and_compaction(kind, n, vocab, seed):
     e.close()
 
 
+@pytest.mark.parametrize("g", synth_goldens(), ids=lambda g: g["name"])
+@pytest.mark.parametrize("batch,skip", [(1, 1), (3, 0), (256, 1)])
+def test_merge_batch_and_block_skip_agree(g, batch, skip):
+    """The synchronous loop (merge_batch 1), short and long device-resident batches (halting at self
+    pairs, undecided ties and capacity changes), with and without block skipping: same merges."""
+    e = zbpe.Engine(0)
+    e.set_option("merge_batch", batch)
+    e.set_option("block_skip", skip)
+    m, c, st = e.train(synth_text(g), g["vocab_size"])
+    assert m.tolist() == g["merges"]
+    assert c.tolist() == g["counts"]
+    assert st.final_tokens == g["final_tokens"]
+    assert e.verify_counts() == 0
+    e.close()
+
+
 def test_compaction_policies_agree(engine):
     text = zbpe.synth_corpus("words_utf8", 31, 300000)
     r = O.train(text, 700)

@@ -1,4 +1,5 @@
 // extern "C" entry points declared in include/zbpe.h.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -117,6 +118,11 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "scan_blocks_per_cu" && value > 0) e.scan_blocks_per_cu = (int)value;
     else if (k == "scan_variant") return e.set_scan_variant((int)value);
     else if (k == "scan_auto") e.scan_auto = value != 0;
+    else if (k == "block_skip") e.block_skip = value != 0;
+    else if (k == "trace") e.trace_on = value != 0;
+    else if (k == "merge_batch" && value >= 1) e.merge_batch = (uint32_t)std::min<int64_t>(value, zbpe::MAX_BATCH);
+    else if (k == "merge_timing" && value >= 0) e.merge_timing = (uint32_t)value;
+    else if (k == "replace_split") e.replace_split = value != 0;
     else if (k == "hot_target" && value > 0) e.hot_target = (uint64_t)value;
     else return e.fail(ZBPE_INVALID_ARGUMENT, "unknown option %s", name);
     return ZBPE_OK;
@@ -125,6 +131,15 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
 zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, double *avg_ms, double *gbps) {
     if (!ctx || !avg_ms || !gbps || reps < 1 || a == b) return ZBPE_INVALID_ARGUMENT;
     return ctx->eng.bench_scan(a, b, reps, avg_ms, gbps);
+}
+
+zbpe_status zbpe_trace(zbpe_ctx *ctx, float *rows, size_t cap_rows, size_t *n_rows) {
+    if (!ctx || !n_rows || (!rows && cap_rows)) return ZBPE_INVALID_ARGUMENT;
+    const auto &t = ctx->eng.trace;
+    *n_rows = t.size() / ZBPE_TRACE_COLS;
+    const size_t k = std::min(cap_rows, *n_rows);
+    if (k) memcpy(rows, t.data(), k * ZBPE_TRACE_COLS * sizeof(float));
+    return ZBPE_OK;
 }
 
 zbpe_status zbpe_zig_order_winner(const uint32_t *first_pos, const uint32_t *keys, const uint32_t *counts, size_t n,

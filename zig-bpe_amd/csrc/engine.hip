@@ -56,7 +56,9 @@ void Engine::release() {
     f(T.ht); f(T.id_key); f(T.id_cnt);
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list); f(d_sup);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo);
+    for (auto &e : bev) if (e) (void)hipEventDestroy(e);
+    bev.clear();
     if (h_st) (void)hipHostFree(h_st);
     if (h_count_hist) (void)hipHostFree(h_count_hist);
     for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -70,7 +72,7 @@ void Engine::release() {
     d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr;
     d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
     d_summ = nullptr; d_count_hist = nullptr; h_count_hist = nullptr; hot_cap_alloc = home_words_cap = 0; home_slots = 0;
-    dirty_list_cap = dirty_bits_cap = 0; d_sup = nullptr; sup_cap = 0;
+    dirty_list_cap = dirty_bits_cap = 0; d_sup = nullptr; sup_cap = 0; d_pres = nullptr; pres_cap = 0;
     for (auto &e : ev) e = nullptr;
 }
 
@@ -86,12 +88,19 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipMalloc(&d_delta, DELTA_WORDS * sizeof(uint32_t)));
     HIP_OK(hipMemset(d_delta, 0, DELTA_WORDS * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&T.tok_cnt, 65536 * sizeof(int32_t)));
+    HIP_OK(hipMalloc(&d_log, 65536 * sizeof(MergeLog)));
+    HIP_OK(hipMalloc(&d_halo, sizeof(Halo)));
+    h_log.resize(65536);
+    bev.resize(4 * MAX_BATCH);
+    for (auto &e : bev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
     HIP_OK(hipMalloc(&d_count_hist, COUNT_BINS * sizeof(uint32_t)));
     HIP_OK(hipHostMalloc((void **)&h_count_hist, COUNT_BINS * sizeof(uint32_t), hipHostMallocDefault));
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
     // the initial byte-pair histogram keeps 128 KiB of bins in LDS
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_count_byte_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4));
+    HIP_OK(hipFuncSetAttribute((const void *)zbpe_pres_build, hipFuncAttributeMaxDynamicSharedMemorySize, PRES_MAX_VP * 4));
     CHECK(set_scan_variant(0));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dev));
@@ -172,6 +181,7 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     Tables N{};
     N.hot = T.hot; N.hot_cap = T.hot_cap; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
     N.home_dirty = T.home_dirty; N.dirty_list = T.dirty_list; N.dirty_cap = T.dirty_cap;
+    N.tok_cnt = T.tok_cnt;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
     if (hipMalloc(&N.ht, ht_cap_new * 8) != hipSuccess || hipMalloc(&N.id_key, id_cap_new * 4) != hipSuccess ||
@@ -195,13 +205,16 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     return ZBPE_OK;
 }
 
-zbpe_status Engine::maybe_grow_tables(uint32_t X) {
-    const uint64_t need = (uint64_t)h_st->num_ids + 2ull * X + 8;
+// room for the new ids of `k` merges starting at X (each adds at most 2X + 1 pairs), and a rebuild
+// when dead ids dominate
+zbpe_status Engine::maybe_grow_tables(uint32_t X, uint32_t k) {
+    const uint64_t per = 2ull * (X + k) + 8;
+    const uint64_t need = (uint64_t)h_st->num_ids + per * k;
     const uint64_t live = (uint64_t)std::max(h_st->live, 0);
     const uint64_t dead = h_st->num_ids - live;
     if (need <= T.id_cap && !(dead > std::max<uint64_t>(live, 1u << 20))) return ZBPE_OK;
     uint64_t cap = T.id_cap;
-    while (live + 2ull * X + 8 > cap / 2) cap *= 2;
+    while (live + per * k > cap / 2) cap *= 2;
     CHECK(alloc_tables(cap));
     return sync_state();
 }
@@ -224,6 +237,7 @@ zbpe_status Engine::compact() {
     cur ^= 1;
     n_slots = n_live;
     stats.compactions++;
+    CHECK(build_presence());
     if (debug_checks) {
         uint64_t total = 0;
         HIP_OK(hipMemcpyAsync(&total, d_tile_off + ntiles, 8, hipMemcpyDeviceToHost, stream));
@@ -351,7 +365,7 @@ zbpe_status Engine::rebuild_home(uint64_t cap) {
     LAUNCH_OK();
     HIP_OK(hipMemsetAsync(T.home_dirty, 0, (nb / 32 + 1) * 4, stream));
     HIP_OK(hipMemsetAsync(&d_st->dirty_len, 0, 4, stream));
-    zbpe_home_summary<<<(unsigned)std::min<size_t>(nb, 4096), 256, 0, stream>>>(T, d_st, (uint32_t)cap, (uint32_t)nb, d_summ);
+    zbpe_home_summary<<<(unsigned)std::min<size_t>(nb, 4096), 256, 0, stream>>>(T, d_st, (uint32_t)cap, (uint32_t)nb, d_summ, 0);
     LAUNCH_OK();
     home_slots = cap;
     home_rebuilds++;
@@ -370,15 +384,15 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     HIP_OK(hipMemsetAsync(&d_st->tie_len, 0, 4, stream));
     const uint32_t hl = std::min<uint32_t>(h_st->hot_len, T.hot_cap);
     zbpe_tie_collect<<<std::min<uint32_t>(1024, hl / 256 + 1), 256, 0, stream>>>(T, d_st, top, (uint32_t)(cap - 1), d_tie_list,
-                                                                                  (uint32_t)tie_list_cap);
+                                                                                  (uint32_t)tie_list_cap, 0);
     LAUNCH_OK();
-    zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)cap, 0, d_summ);
+    zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)cap, 0, d_summ, 0);
     LAUNCH_OK();
     const uint32_t nb = (uint32_t)((cap + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
-    zbpe_super_summary<<<(nsb + 3) / 4, 256, 0, stream>>>(d_summ, nb, d_sup);
+    zbpe_super_summary<<<(nsb + 3) / 4, 256, 0, stream>>>(d_summ, nb, d_sup, d_st, 0);
     LAUNCH_OK();
     HomeView V{T.home_cnt, d_summ, d_sup, (uint32_t)cap, nb, nsb};
-    zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V);
+    zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 0);
     LAUNCH_OK();
     CHECK(sync_state());
     if (h_st->tie_len != ties)
@@ -493,6 +507,19 @@ int Engine::scan_grid(int64_t slots) const {
     return (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)num_cus * scan_blocks_per_cu));
 }
 
+// (re)build the token -> block presence bitmap from the current stream (block skipping)
+zbpe_status Engine::build_presence() {
+    if (!pres_on) return ZBPE_OK;
+    const uint64_t groups = std::max<uint64_t>(1, ((uint64_t)n_slots + (uint64_t)PRES_BLK * PRES_GROUP - 1) /
+                                                      ((uint64_t)PRES_BLK * PRES_GROUP));
+    CHECK(ensure(&d_pres, pres_cap, groups * pres_vp, "presence bitmap"));
+    pres_groups = (uint32_t)groups;
+    zbpe_pres_build<<<(unsigned)groups, PRES_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n_slots, pres_vp, d_pres);
+    LAUNCH_OK();
+    stats_pres_builds++;
+    return ZBPE_OK;
+}
+
 zbpe_status Engine::alloc_stream(size_t n) {
     const size_t need = round_up(n + 1, 64) + 64;
     CHECK(ensure(&d_tok[0], tok_cap0, need, "token stream"));
@@ -543,6 +570,9 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
 
     // ---- generateInitialTokens + initial histogram ------------------------------------------------
     CHECK(alloc_stream(n));
+    pres_vp = ((uint32_t)vocab_size + 63) & ~63u;
+    pres_on = block_skip && pres_vp <= PRES_MAX_VP;
+    CHECK(build_presence());
     if (!T.id_key || T.id_cap < (1u << 20)) {
         if (T.id_key) { (void)hipFree(T.ht); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt); T.ht = nullptr; T.id_key = T.id_cnt = nullptr; }
         CHECK(alloc_tables(1u << 20));
@@ -550,6 +580,11 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         HIP_OK(hipMemsetAsync(T.ht, 0xFF, ((size_t)T.ht_mask + 1) * 8, stream));
     }
     HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
+    {
+        const long long lt = (long long)n;
+        HIP_OK(hipMemcpyAsync(&d_st->live_tokens, &lt, sizeof(lt), hipMemcpyHostToDevice, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+    }
     home_slots = 0;
     T.home_mask = 0;
     if (T.home_cnt) { (void)hipFree(T.home_cnt); T.home_cnt = nullptr; home_words_cap = 0; }
@@ -569,11 +604,12 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     }
     CHECK(comm_sum(d_hist, 65536));  // every rank builds the same table from the summed histogram
     if (world > 1) {  // boundary tokens of every shard (the first select needs the stream's last pair)
-        zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, n_live, d_bnd_mine);
+        zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, n_live, d_bnd_mine, nullptr);
         LAUNCH_OK();
         if (!comm->allgather(d_bnd_mine, d_bnd_all, sizeof(Boundary), stream))
             return fail(ZBPE_COMM_ERROR, "all-gather of shard boundaries failed");
     }
+    HIP_OK(hipMemsetAsync(T.tok_cnt, 0, 65536 * sizeof(int32_t), stream));
     zbpe_hist_to_table<<<256, 256, 0, stream>>>(d_hist, T, d_st);
     LAUNCH_OK();
     HIP_OK(hipEventRecord(ev[1], stream));
@@ -588,134 +624,40 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         HIP_OK(hipEventElapsedTime(&ms, ev[1], ev[2])); ev_select += ms * 1e-3;
         stats.count_pairs_calls++;
     }
-    uint64_t holes = 0;
-    size_t merges = 0;
-    for (uint32_t X = 256; X < vocab_size; X++) {
+    run = RunCtx{};
+    run.out_triples = out_triples;
+    run.out_counts = out_counts;
+    run.verbose = verbose;
+    run.vocab = vocab_size;
+    trace.clear();
+    uint32_t X = 256;
+    while (X < vocab_size) {
         if (h_st->live <= 0) {  // sortedCodePointPairs.len == 0 (basic_tokenizer.zig:188-191)
             if (rank == 0) fprintf(stderr, "No more pairs to merge. Stopping early.\n");
             break;
         }
-        const uint32_t top = h_st->top_count, ties = h_st->tie_count;
-        uint32_t key = h_st->top_key;
-        const double t_sel = now_s();
-        if (ties > 1) CHECK(resolve_tie(top, ties, &key));
-        stats.sort_pairs_calls++;
-        if (ties > 1) ev_select += now_s() - t_sel;
-        const uint32_t a = key & 0xFFFF, b = key >> 16;
-        if (verbose && rank == 0)
-            fprintf(stderr, "merge %u/%u: (%u,%u) -> %u had %u occurrences\n", X - 256 + 1, vocab_size - 256u, a, b, X, top);
-        out_triples[3 * merges + 0] = (uint16_t)a;
-        out_triples[3 * merges + 1] = (uint16_t)b;
-        out_triples[3 * merges + 2] = (uint16_t)X;
-        if (out_counts) out_counts[merges] = top;
-        merges++;
-        stats.sum_tokens += (uint64_t)n_live;
-
-        CHECK(maybe_grow_tables(X));
-        CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(top, 1), "occurrence records"));
-        const bool self = a == b;
-        if (self && holes) {
-            HIP_OK(hipEventRecord(ev[3], stream));
-            CHECK(compact());
-            holes = 0;
-            HIP_OK(hipEventRecord(ev[4], stream));
-            HIP_OK(hipEventSynchronize(ev[4]));
-            float ms;
-            HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
-            ev_replace += ms * 1e-3;
+        if (merge_batch > 1 && !debug_checks && !force_exact_ties && vocab_size - X > 1) {
+            uint32_t done = 0;
+            bool halted = false;
+            CHECK(run_batch(X, &done, &halted));
+            X += done;
+            if (!halted) continue;
+            // the device stopped at merge X: clear the flag, make the selection valid, finish X here
+            HIP_OK(hipMemsetAsync(&d_st->halt, 0, 4, stream));
+            CHECK(sync_state());
+            CHECK(select_ready());
+            if (h_st->live <= 0) continue;
         }
-        // delta layout for this merge: left[0, X) | right[X, 2X) | xx | occurrences
-        uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
-        // ---- count: scan the stream for (a, b) -----------------------------------------------------
-        ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_rec, (uint32_t)rec_cap, 1, tail, tail + 1, halo};
-        HIP_OK(hipEventRecord(ev[0], stream));
-        if (!self) {
-            CHECK(launch_scan(A, top));
-            stats.scan_launches++;
-        } else {
-            stats.self_pair_merges++;
-            const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);
-            CHECK(ensure(&d_tile_fn, tile_fn_cap, ntiles, "self tiles"));
-            CHECK(ensure(&d_carry, carry_cap, ntiles, "self carry"));
-            zbpe_self_tiles<<<ntiles, SELF_THREADS, 0, stream>>>(d_tok[cur], n_slots, a, d_tile_fn);
-            LAUNCH_OK();
-            if (world > 1) {  // parity of the run of a's entering this shard from the ranks to the left
-                zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, nullptr, d_shard_fn);
-                LAUNCH_OK();
-                if (!comm->allgather(d_shard_fn, d_fns_all, 4, stream)) return fail(ZBPE_COMM_ERROR, "all-gather of run carries failed");
-                zbpe_self_x0<<<1, 1, 0, stream>>>(d_fns_all, rank, d_x0);
-                LAUNCH_OK();
-            }
-            zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, world > 1 ? d_x0 : nullptr, nullptr);
-            LAUNCH_OK();
-            zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
-            LAUNCH_OK();
-        }
-        HIP_OK(hipEventRecord(ev[1], stream));
-        // ---- exchange: sum the count deltas of all shards (one RCCL all-reduce per merge) ---------------
-        CHECK(comm_sum(d_delta, 2ull * X + 2));
-        // ---- replace: apply + count update ---------------------------------------------------------
-        {
-            const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top / 256 + 1);
-            ReplaceArgs R{d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, left, right, tail, a, b, X, key, ab, halo,
-                          (self && world > 1) ? d_x0 : nullptr};
-            zbpe_replace<<<ab + update_blocks(X), 256, 0, stream>>>(R, T, d_st);
-            LAUNCH_OK();
-        }
-        if (world > 1) {  // boundary tokens of every shard for the next merge's halos
-            zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, n_live, d_bnd_mine);
-            LAUNCH_OK();
-            if (!comm->allgather(d_bnd_mine, d_bnd_all, sizeof(Boundary), stream))
-                return fail(ZBPE_COMM_ERROR, "all-gather of shard boundaries failed");
-        }
-        HIP_OK(hipEventRecord(ev[2], stream));
-        // ---- select for the next merge (also clears the deltas, rolls the counters) ----------------------
-        CHECK(launch_argmax(X, 1));
-        if (world > 1) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipEventRecord(ev[3], stream));
-        CHECK(sync_state());
-        CHECK(select_ready());
-        {
-            float ms;
-            HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1])); ev_count += ms * 1e-3;
-            if (!self) {
-                stats.scan_kernel_s += ms * 1e-3;
-                stats.scan_alg_bytes += 2ull * (uint64_t)n_live;
-                stats.scan_read_bytes += 2ull * (uint64_t)n_slots;
-            }
-            HIP_OK(hipEventElapsedTime(&ms, ev[1], ev[2])); ev_replace += ms * 1e-3;
-            HIP_OK(hipEventElapsedTime(&ms, ev[2], ev[3])); ev_select += ms * 1e-3;
-            stats.count_pairs_calls++;
-            stats.replace_pair_calls++;
-        }
-        if (world > 1) halo_from_boundaries();
-        if (debug_checks) {
-            uint64_t bad = 0;
-            uint32_t info[3] = {0, 0, 0};
-            CHECK(recount_check(&bad, info));
-            if (bad)
-                return fail(ZBPE_INTERNAL, "merge %u (%u,%u): %llu pair counts differ from a full recount (first: key (%u,%u) table %u, recount %u)",
-                            X, a, b, (unsigned long long)bad, info[0] & 0xFFFF, info[0] >> 16, info[1], info[2]);
-        }
-        const uint32_t gocc = h_st->last_gocc;
-        if (!self && gocc != top)
-            return fail(ZBPE_INTERNAL, "merge %u: scan found %u occurrences of (%u,%u), count was %u", X, gocc, a, b, top);
-        const uint64_t gone = h_st->last_holes;  // slots of this shard that became holes
-        n_live -= gone;
-        holes += gone;
-        if (holes * compact_den > (uint64_t)n_slots) {
-            HIP_OK(hipEventRecord(ev[0], stream));
-            CHECK(compact());
-            holes = 0;
-            HIP_OK(hipEventRecord(ev[1], stream));
-            HIP_OK(hipEventSynchronize(ev[1]));
-            float ms;
-            HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
-            ev_replace += ms * 1e-3;
-        }
+        CHECK(merge_sync(X));
+        X++;
     }
+    const size_t merges = run.merges;
+    ev_count += run.ev_count;
+    ev_select += run.ev_select;
+    ev_replace += run.ev_replace;
     HIP_OK(hipStreamSynchronize(stream));
     *out_n_merges = merges;
+    stats.scan_read_bytes = 2ull * h_st->scanned_slots;
     stats.count_pairs_s = ev_count;
     stats.sort_pairs_s = ev_select;
     stats.replace_pair_s = ev_replace;
@@ -746,6 +688,267 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     stats.pair_ids = h_st->num_ids;
     trained = true;
     if (out_stats) *out_stats = stats;
+    return ZBPE_OK;
+}
+
+// Device-resident batch: enqueue up to merge_batch merges without a host sync. Every kernel
+// reads the merge's pair from DevState; zbpe_merge_begin / zbpe_tie_decide halt the batch at a
+// merge the device cannot finish alone (self pair, undecided tie, capacity change, hot-list
+// rebuild), after which every remaining kernel of the batch returns at once. One sync per batch.
+zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
+    const uint32_t K = std::min<uint32_t>(merge_batch, run.vocab - X0);
+    *done = 0;
+    *halted = false;
+    // headroom for K merges: ids, occurrence records (counts never grow), tie list; compaction
+    CHECK(maybe_grow_tables(X0, K));
+    if (hot_stale) CHECK(rebuild_hot());  // a table rebuild renumbered the ids the tie kernels read
+    if ((uint64_t)(n_slots - n_live) * compact_den > (uint64_t)n_slots) {
+        HIP_OK(hipEventRecord(ev[0], stream));
+        CHECK(compact());
+        HIP_OK(hipEventRecord(ev[1], stream));
+        HIP_OK(hipEventSynchronize(ev[1]));
+        float ms;
+        HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        run.ev_replace += ms * 1e-3;
+    }
+    const uint32_t top0 = h_st->top_count;
+    CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(top0, 1), "occurrence records"));
+    CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
+    if (world > 1) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
+    const uint64_t C = home_slots;
+    const uint32_t nb = (uint32_t)((C + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
+    const HomeView V{T.home_cnt, d_summ, d_sup, (uint32_t)C, nb, nsb};
+    const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top0 / 256 + 1);
+    const int64_t slots = n_slots;
+    const double t0 = now_s();
+    for (uint32_t i = 0; i < K; i++) {
+        const uint32_t X = X0 + i;
+        const bool timed = merge_timing && X % merge_timing == 0;
+        if (timed) HIP_OK(hipEventRecord(bev[4 * i], stream));
+        uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
+        zbpe_merge_begin<<<1, 64, 0, stream>>>(T, d_st, X, C, (uint32_t)rec_cap, d_log);
+        LAUNCH_OK();
+        if (C) {
+            zbpe_tie_collect<<<64, 256, 0, stream>>>(T, d_st, 0, (uint32_t)(C - 1), d_tie_list, (uint32_t)tie_list_cap, 1);
+            LAUNCH_OK();
+            zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)C, 0, d_summ, 1);
+            LAUNCH_OK();
+            zbpe_super_summary<<<(nsb + 3) / 4, 256, 0, stream>>>(d_summ, nb, d_sup, d_st, 1);
+            LAUNCH_OK();
+            zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 1);
+            LAUNCH_OK();
+        }
+        if (timed) HIP_OK(hipEventRecord(bev[4 * i + 1], stream));
+        ScanArgs A{d_tok[cur], slots, 0, 0, left, right, d_st, d_rec, (uint32_t)rec_cap, 1, tail, tail + 1, halo,
+                   pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 1, world > 1 ? d_halo : nullptr};
+        CHECK(launch_scan(A, top0));
+        if (timed) HIP_OK(hipEventRecord(bev[4 * i + 2], stream));
+        CHECK(comm_sum(d_delta, 2ull * X + 2));
+        ReplaceArgs R{d_tok[cur], slots, d_rec, (uint32_t)rec_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
+                      1, world > 1 ? d_halo : nullptr};
+        if (!replace_split) {
+            zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
+        } else {  // profiling: apply and count update as two launches
+            zbpe_replace<<<ab, 256, 0, stream>>>(R, T, d_st);
+            R.apply_blocks = 0;
+            zbpe_replace<<<update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
+        }
+        LAUNCH_OK();
+        if (world > 1) {
+            zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], slots, 0, d_bnd_mine, d_st);
+            LAUNCH_OK();
+            if (!comm->allgather(d_bnd_mine, d_bnd_all, sizeof(Boundary), stream))
+                return fail(ZBPE_COMM_ERROR, "all-gather of shard boundaries failed");
+            zbpe_halo_build<<<1, 1, 0, stream>>>(d_bnd_all, rank, world, d_halo, d_st);
+            LAUNCH_OK();
+        }
+        CHECK(launch_argmax(X, 1));
+        if (timed) HIP_OK(hipEventRecord(bev[4 * i + 3], stream));
+    }
+    if (world > 1) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
+    CHECK(sync_state());
+    const double wall = now_s() - t0;
+    batches++;
+    const uint32_t m = h_st->halt ? h_st->halt_at - X0 : K;
+    if (h_st->halt) {
+        *halted = true;
+        batch_halts++;
+        if (m > K) return fail(ZBPE_INTERNAL, "batch halted at merge %u outside [%u, %u)", h_st->halt_at, X0, X0 + K);
+    }
+    if (m) HIP_OK(hipMemcpy(h_log.data() + (X0 - 256), d_log + (X0 - 256), m * sizeof(MergeLog), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < m; i++) {
+        const MergeLog &L = h_log[X0 - 256 + i];
+        const uint32_t X = X0 + i, a = L.key & 0xFFFF, b = L.key >> 16;
+        if (run.verbose && rank == 0)
+            fprintf(stderr, "merge %u/%u: (%u,%u) -> %u had %u occurrences\n", X - 256 + 1, run.vocab - 256u, a, b, X, L.count);
+        run.out_triples[3 * run.merges + 0] = (uint16_t)a;
+        run.out_triples[3 * run.merges + 1] = (uint16_t)b;
+        run.out_triples[3 * run.merges + 2] = (uint16_t)X;
+        if (run.out_counts) run.out_counts[run.merges] = L.count;
+        run.merges++;
+        stats.sum_tokens += L.live;
+        stats.scan_alg_bytes += 2ull * L.live;
+        stats.scan_launches++;
+        stats.sort_pairs_calls++;
+        stats.count_pairs_calls++;
+        stats.replace_pair_calls++;
+        if (L.ties > 1) stats.tie_iterations++;
+        float ms_sel = 0, ms_scan = 0, ms_rep = 0;
+        if (merge_timing && X % merge_timing == 0) {
+            HIP_OK(hipEventElapsedTime(&ms_sel, bev[4 * i], bev[4 * i + 1]));
+            HIP_OK(hipEventElapsedTime(&ms_scan, bev[4 * i + 1], bev[4 * i + 2]));
+            HIP_OK(hipEventElapsedTime(&ms_rep, bev[4 * i + 2], bev[4 * i + 3]));
+            stats.scan_kernel_s += ms_scan * 1e-3;
+            stats.scan_timed_launches++;
+            stats.scan_timed_alg_bytes += 2ull * L.live;
+            // stage totals are extrapolated from the sampled merges
+            run.ev_count += merge_timing * ms_scan * 1e-3;
+            run.ev_select += merge_timing * ms_sel * 1e-3;
+            run.ev_replace += merge_timing * ms_rep * 1e-3;
+        }
+        if (trace_on) {
+            const float row[ZBPE_TRACE_COLS] = {(float)(X - 256), (float)L.count, (float)L.live, (float)slots, 0.f, ms_scan,
+                                                ms_rep, ms_sel, (float)(wall * 1e3 / K), 0.f, (float)L.ties};
+            trace.insert(trace.end(), row, row + ZBPE_TRACE_COLS);
+        }
+    }
+    n_live = h_st->live_tokens;
+    if (world > 1) halo_from_boundaries();
+    *done = m;
+    return ZBPE_OK;
+}
+
+// One merge on the synchronous path: the host reads the selection, resolves a tie (exact
+// fallback included), handles self pairs, and syncs once at the end.
+zbpe_status Engine::merge_sync(uint32_t X) {
+    const double t_merge = now_s();
+    const uint64_t slots_before = h_st->scanned_slots;
+    const int64_t live_before = n_live, slots_now = n_slots;
+    const uint32_t top = h_st->top_count, ties = h_st->tie_count;
+    uint32_t key = h_st->top_key;
+    const double t_sel = now_s();
+    if (ties > 1) CHECK(resolve_tie(top, ties, &key));
+    stats.sort_pairs_calls++;
+    if (ties > 1) run.ev_select += now_s() - t_sel;
+    const uint32_t a = key & 0xFFFF, b = key >> 16;
+    if (run.verbose && rank == 0)
+        fprintf(stderr, "merge %u/%u: (%u,%u) -> %u had %u occurrences\n", X - 256 + 1, run.vocab - 256u, a, b, X, top);
+    run.out_triples[3 * run.merges + 0] = (uint16_t)a;
+    run.out_triples[3 * run.merges + 1] = (uint16_t)b;
+    run.out_triples[3 * run.merges + 2] = (uint16_t)X;
+    if (run.out_counts) run.out_counts[run.merges] = top;
+    run.merges++;
+    stats.sum_tokens += (uint64_t)n_live;
+
+    CHECK(maybe_grow_tables(X, 1));
+    CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(top, 1), "occurrence records"));
+    const bool self = a == b;
+    if (self && n_slots != n_live) {
+        HIP_OK(hipEventRecord(ev[3], stream));
+        CHECK(compact());
+        HIP_OK(hipEventRecord(ev[4], stream));
+        HIP_OK(hipEventSynchronize(ev[4]));
+        float ms;
+        HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
+        run.ev_replace += ms * 1e-3;
+    }
+    // delta layout for this merge: left[0, X) | right[X, 2X) | xx | occurrences
+    uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
+    // ---- count: scan the stream for (a, b) -----------------------------------------------------
+    ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_rec, (uint32_t)rec_cap, 1, tail, tail + 1, halo,
+               pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt};
+    HIP_OK(hipEventRecord(ev[0], stream));
+    if (!self) {
+        CHECK(launch_scan(A, top));
+        stats.scan_launches++;
+    } else {
+        stats.self_pair_merges++;
+        const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);
+        CHECK(ensure(&d_tile_fn, tile_fn_cap, ntiles, "self tiles"));
+        CHECK(ensure(&d_carry, carry_cap, ntiles, "self carry"));
+        zbpe_self_tiles<<<ntiles, SELF_THREADS, 0, stream>>>(d_tok[cur], n_slots, a, d_tile_fn);
+        LAUNCH_OK();
+        if (world > 1) {  // parity of the run of a's entering this shard from the ranks to the left
+            zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, nullptr, d_shard_fn);
+            LAUNCH_OK();
+            if (!comm->allgather(d_shard_fn, d_fns_all, 4, stream)) return fail(ZBPE_COMM_ERROR, "all-gather of run carries failed");
+            zbpe_self_x0<<<1, 1, 0, stream>>>(d_fns_all, rank, d_x0);
+            LAUNCH_OK();
+        }
+        zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, world > 1 ? d_x0 : nullptr, nullptr);
+        LAUNCH_OK();
+        zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
+        LAUNCH_OK();
+    }
+    HIP_OK(hipEventRecord(ev[1], stream));
+    // ---- exchange: sum the count deltas of all shards (one RCCL all-reduce per merge) ---------------
+    CHECK(comm_sum(d_delta, 2ull * X + 2));
+    // ---- replace: apply + count update ---------------------------------------------------------
+    {
+        const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top / 256 + 1);
+        ReplaceArgs R{d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, left, right, tail, a, b, X, key, ab, halo,
+                      (self && world > 1) ? d_x0 : nullptr};
+        zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
+        LAUNCH_OK();
+    }
+    if (world > 1) {  // boundary tokens of every shard for the next merge's halos
+        zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, n_live, d_bnd_mine, nullptr);
+        LAUNCH_OK();
+        if (!comm->allgather(d_bnd_mine, d_bnd_all, sizeof(Boundary), stream))
+            return fail(ZBPE_COMM_ERROR, "all-gather of shard boundaries failed");
+    }
+    HIP_OK(hipEventRecord(ev[2], stream));
+    // ---- select for the next merge (also clears the deltas, rolls the counters) ----------------------
+    CHECK(launch_argmax(X, 1));
+    if (world > 1) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipEventRecord(ev[3], stream));
+    CHECK(sync_state());
+    CHECK(select_ready());
+    {
+        float ms;
+        float ms_r, ms_s;
+        HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1])); run.ev_count += ms * 1e-3;
+        if (!self) {
+            stats.scan_kernel_s += ms * 1e-3;
+            stats.scan_alg_bytes += 2ull * (uint64_t)n_live;
+            stats.scan_timed_launches++;
+            stats.scan_timed_alg_bytes += 2ull * (uint64_t)n_live;
+        }
+        HIP_OK(hipEventElapsedTime(&ms_r, ev[1], ev[2])); run.ev_replace += ms_r * 1e-3;
+        HIP_OK(hipEventElapsedTime(&ms_s, ev[2], ev[3])); run.ev_select += ms_s * 1e-3;
+        if (trace_on) {
+            const float row[ZBPE_TRACE_COLS] = {(float)(X - 256), (float)top, (float)live_before, (float)slots_now,
+                                                (float)(h_st->scanned_slots - slots_before), ms, ms_r, ms_s,
+                                                (float)((now_s() - t_merge) * 1e3), self ? 1.f : 0.f, (float)ties};
+            trace.insert(trace.end(), row, row + ZBPE_TRACE_COLS);
+        }
+        stats.count_pairs_calls++;
+        stats.replace_pair_calls++;
+    }
+    if (world > 1) halo_from_boundaries();
+    if (debug_checks) {
+        uint64_t bad = 0;
+        uint32_t info[3] = {0, 0, 0};
+        CHECK(recount_check(&bad, info));
+        if (bad)
+            return fail(ZBPE_INTERNAL, "merge %u (%u,%u): %llu pair counts differ from a full recount (first: key (%u,%u) table %u, recount %u)",
+                        X, a, b, (unsigned long long)bad, info[0] & 0xFFFF, info[0] >> 16, info[1], info[2]);
+    }
+    const uint32_t gocc = h_st->last_gocc;
+    if (!self && gocc != top)
+        return fail(ZBPE_INTERNAL, "merge %u: scan found %u occurrences of (%u,%u), count was %u", X, gocc, a, b, top);
+    const uint64_t gone = h_st->last_holes;  // slots of this shard that became holes
+    n_live -= gone;
+    (void)gone;
+    if ((uint64_t)(n_slots - n_live) * compact_den > (uint64_t)n_slots) {
+        HIP_OK(hipEventRecord(ev[0], stream));
+        CHECK(compact());
+        HIP_OK(hipEventRecord(ev[1], stream));
+        HIP_OK(hipEventSynchronize(ev[1]));
+        float ms;
+        HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        run.ev_replace += ms * 1e-3;
+    }
     return ZBPE_OK;
 }
 

@@ -5,6 +5,7 @@
 
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "../../include/zbpe.h"
 #include "comm.hpp"
@@ -16,6 +17,8 @@ namespace zbpe {
 
 constexpr int ARGMAX_MAX_BLOCKS = 1024;
 constexpr size_t DELTA_WORDS = 2 * 65536 + 64;  // left | right | xx | occurrences (+ scratch)
+constexpr uint32_t MAX_BATCH = 256;              // merges per device-resident batch (option "merge_batch")
+constexpr uint32_t PRES_MAX_VP = 32768;          // presence bitset of a block group fits one workgroup LDS (128 KiB)
 
 struct Engine {
     int device = 0;
@@ -76,6 +79,32 @@ struct Engine {
     Summ *d_summ = nullptr, *d_sup = nullptr;
     size_t summ_cap = 0, sup_cap = 0;
     bool hot_stale = true;
+    // block skipping
+    uint32_t *d_pres = nullptr;
+    size_t pres_cap = 0;
+    uint32_t pres_vp = 0, pres_groups = 0;
+    bool pres_on = false, block_skip = true;
+    uint64_t stats_pres_builds = 0;
+    // per-merge trace (option "trace"), ZBPE_TRACE_COLS floats per merge
+    bool trace_on = false;
+    std::vector<float> trace;
+    // device-resident merge loop
+    uint32_t merge_batch = 32;      // merges enqueued per host sync (1: synchronous loop)
+    bool merge_timing = true;
+    bool replace_split = false;     // profiling: apply and count update as separate launches       // HIP events around every scan of a batch (roofline, stats)
+    MergeLog *d_log = nullptr;
+    std::vector<MergeLog> h_log;
+    Halo *d_halo = nullptr;
+    std::vector<hipEvent_t> bev;
+    uint64_t batches = 0, batch_halts = 0;
+    struct RunCtx {
+        uint16_t *out_triples = nullptr;
+        uint64_t *out_counts = nullptr;
+        size_t merges = 0;
+        int verbose = 0;
+        uint16_t vocab = 0;
+        double ev_count = 0, ev_select = 0, ev_replace = 0;
+    } run;
     uint64_t hot_target = 1u << 16;  // ids the hot list aims to hold after a rebuild
     uint64_t hot_rebuilds = 0, home_rebuilds = 0;
     hipEvent_t ev[6] = {};
@@ -108,8 +137,11 @@ struct Engine {
    private:
     zbpe_status sync_state();
     zbpe_status alloc_tables(size_t id_cap);
-    zbpe_status maybe_grow_tables(uint32_t X);
+    zbpe_status maybe_grow_tables(uint32_t X, uint32_t k);
+    zbpe_status merge_sync(uint32_t X);
+    zbpe_status run_batch(uint32_t X0, uint32_t *done, bool *halted);
     zbpe_status alloc_stream(size_t n);
+    zbpe_status build_presence();
     zbpe_status compact();
     zbpe_status launch_argmax(uint32_t X, int roll);
     int scan_grid(int64_t slots) const;

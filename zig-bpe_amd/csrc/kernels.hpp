@@ -195,12 +195,19 @@ __global__ void __launch_bounds__(HIST_THREADS) zbpe_count_byte_pairs(const uint
     }
 }
 
+__device__ inline uint32_t wave_sum(uint32_t x);
 // hist[first*256+second] -> pair table entries
 __global__ void zbpe_hist_to_table(const uint32_t *__restrict__ hist, Tables T, DevState *st) {
-    uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= 65536) return;
+    // launched as <<<256, 256>>>: block = first byte
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     uint32_t c = hist[k];
     if (c) pair_new(T, st, pair_key(k >> 8, k & 0xff), c);
+    // token counts (a byte's pairs as first element; the stream's last byte is not counted)
+    __shared__ uint32_t s_sum[4];
+    const uint32_t w = wave_sum(c);
+    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0 && T.tok_cnt) T.tok_cnt[blockIdx.x] = (int32_t)(s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -313,7 +320,24 @@ struct ScanArgs {
     uint32_t *xx_out;    // adjacent occurrences (b,a) -> (X,X), summed over ranks
     uint32_t *occ_out;   // occurrences, summed over ranks
     Halo halo;           // live tokens beyond the shard (multi-GPU); empty on one GPU
+    // block skipping: pres[(block / 32) * vp + token] bit (block % 32) = token may occur in the block
+    uint32_t *pres;      // nullptr: stream every block
+    uint32_t vp;         // tokens per presence row
+    uint32_t X;          // the merge's new token (its presence bits are set where it is written)
+    const int32_t *tokcnt;  // token counts: the rarer of a, b keys the scan (nullptr: a)
+    int dyn;                // batch mode: a, b from st->cur_key, halo from *dhalo (if set); no-op when halted
+    const Halo *dhalo;
 };
+// batch mode: resolve the device-held parts of the arguments (false: the batch is halted)
+__device__ inline bool scan_args_resolve(ScanArgs &A) {
+    if (!A.dyn) return true;
+    if (A.st->halt) return false;
+    const uint32_t k = A.st->cur_key;
+    A.a = k & 0xFFFF;
+    A.b = k >> 16;
+    if (A.dhalo) A.halo = *A.dhalo;
+    return true;
+}
 
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
 constexpr int64_t NONE_POS = INT64_MIN;
@@ -474,16 +498,24 @@ __device__ inline uint32_t occ_vector(const ScanArgs &A, NeighbourHist &H, int64
     return hits;
 }
 
+__device__ inline void pres_set(const ScanArgs &A, int64_t pos) {
+    const uint64_t blk = (uint64_t)pos / PRES_BLK;
+    atomicOr(&A.pres[(blk / PRES_GROUP) * A.vp + A.X], 1u << (blk % PRES_GROUP));
+}
+
 template <int UNROLL, bool NT, bool FILTER>
 __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
+    if (!scan_args_resolve(A)) return;
     constexpr int STAGE = 4;                      // vectors per lane per record-staging step
     constexpr uint32_t WREC = 64 * STAGE * 8 / 2;  // at most one occurrence per 2 tokens
     static_assert(UNROLL % STAGE == 0 || UNROLL < STAGE, "UNROLL must be a multiple of 4 (or < 4)");
+    static_assert(PRES_BLK % (64 * UNROLL * 8) == 0, "presence blocks hold whole wave-tiles");
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
     __shared__ uint32_t s_rec[SCAN_THREADS / 64][WREC];
     __shared__ uint32_t s_any;
+    __shared__ unsigned long long s_scanned;
     for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
-    if (threadIdx.x == 0) s_any = 0;
+    if (threadIdx.x == 0) { s_any = 0; s_scanned = 0; }
     __syncthreads();
     NeighbourHist H{s_left, s_right, A.left, A.right};
     const uint16_t *tok = A.tok;
@@ -492,12 +524,43 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
     const int64_t nwt = (nvec + WT_VEC - 1) / WT_VEC;
     const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
     const int64_t wstride = (int64_t)gridDim.x * (SCAN_THREADS / 64);
+    // by_b: find occurrences from their second token (when b is the rarer one); exact with holes
+    const bool by_b = A.pres && A.tokcnt && A.a != A.b && A.tokcnt[A.b] < A.tokcnt[A.a];
+    const uint32_t key_tok = by_b ? A.b : A.a;
     uint32_t *wrec = s_rec[wib];
     uint32_t nbuf = 0;  // wave-uniform: records staged in wrec
-    uint32_t xx = 0, any = 0;
-    for (int64_t wt = (int64_t)blockIdx.x * (SCAN_THREADS / 64) + wib; wt < nwt; wt += wstride) {
+    uint32_t xx = 0, any = 0, tiles = 0;
+    if (by_b && blockIdx.x == 0 && threadIdx.x == 0 && A.halo.nright > 0 && A.halo.right[0] == A.b) {
+        // the occurrence leaving the shard: its b is the next shard's, so no tile here holds it
+        const int64_t p = prev_live(tok, A.n);
+        if (p >= 0 && tok[p] == A.a && occ_slow(A, H, p, xx)) {
+            const uint32_t j = atomicAdd(&A.st->rec_count, 1u);
+            atomicAdd(A.occ_out, 1u);
+            if (j < A.rec_cap) A.rec[j] = (uint32_t)p;
+            else atomicOr(&A.st->error, 8u);
+            pres_set(A, p);
+            any = 1;
+        }
+    }
+    for (int64_t wt0 = (int64_t)blockIdx.x * (SCAN_THREADS / 64) + wib; wt0 < nwt; wt0 += 64 * wstride) {
+      // block skipping: lane j looks up the presence bit of this wave's j-th next tile, so the
+      // lookups of 64 tiles cost one load latency instead of one per tile
+      uint64_t todo;
+      {
+          const int64_t mine = wt0 + (int64_t)lane * wstride;
+          bool pr = mine < nwt;
+          if (A.pres && pr) {
+              const uint64_t blk = (uint64_t)mine * WT_VEC * 8 / PRES_BLK;
+              pr = (A.pres[(blk / PRES_GROUP) * A.vp + key_tok] >> (blk % PRES_GROUP)) & 1u;
+          }
+          todo = __ballot(pr);
+      }
+      while (todo) {
+        const int64_t wt = wt0 + (int64_t)__builtin_ctzll(todo) * wstride;
+        todo &= todo - 1;
         const int64_t vbase = wt * WT_VEC;
-        // phase 1: stream UNROLL x 16 B per lane, keep only the positions holding `a`
+        tiles++;
+        // phase 1: stream UNROLL x 16 B per lane, keep only the positions holding the key token
         uint4 v[UNROLL];
 #pragma unroll
         for (int u = 0; u < UNROLL; u++) {
@@ -515,24 +578,34 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
                 v[u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
             }
         }
-        uint64_t cand = 0;  // bit 8u+k: token k of vector u is `a`
+        uint64_t cand = 0;  // bit 8u+k: token k of vector u is the key token
 #pragma unroll
-        for (int u = 0; u < UNROLL; u++) cand |= (uint64_t)match8(v[u], A.a) << (8 * u);
-        if (__ballot(cand != 0) == 0) continue;  // wave-uniform: no `a` in these 64*UNROLL*16 B
+        for (int u = 0; u < UNROLL; u++) cand |= (uint64_t)match8(v[u], key_tok) << (8 * u);
+        if (__ballot(cand != 0) == 0) continue;  // wave-uniform: no key token in these 64*UNROLL*16 B
         if constexpr (FILTER) {
-            // keep `a` only where the next slot holds `b` or a hole (the next lane's first token via
-            // a shuffle; lane 63 cannot see it and keeps its last candidate for phase 2)
+            // by a: keep a where the next slot holds b or a hole; by b: keep b where the previous slot
+            // holds a or a hole (across lanes by a shuffle; lanes 63 / 0 keep their edge candidate)
             uint64_t f = 0;
 #pragma unroll
             for (int u = 0; u < UNROLL; u++) {
-                const uint32_t nx = (uint32_t)__shfl_down((int)v[u].x, 1) & 0xffffu;
-                uint32_t nb = 0;  // bit k: token k+1 (k < 7) or the next vector's token 0 is b / HOLE
+                uint32_t nb = 0;
+                if (!by_b) {
+                    const uint32_t nx = (uint32_t)__shfl_down((int)v[u].x, 1) & 0xffffu;
 #pragma unroll
-                for (int k = 0; k < 7; k++) {
-                    const uint32_t t = tok_at(v[u], k + 1);
-                    nb |= (t == A.b || t == HOLE ? 1u : 0u) << k;
+                    for (int k = 0; k < 7; k++) {
+                        const uint32_t t = tok_at(v[u], k + 1);
+                        nb |= (t == A.b || t == HOLE ? 1u : 0u) << k;
+                    }
+                    nb |= (lane == 63 || nx == A.b || nx == HOLE ? 1u : 0u) << 7;
+                } else {
+                    const uint32_t pv = (uint32_t)__shfl_up((int)v[u].w, 1) >> 16;
+                    nb |= (lane == 0 || pv == A.a || pv == HOLE ? 1u : 0u);
+#pragma unroll
+                    for (int k = 1; k < 8; k++) {
+                        const uint32_t t = tok_at(v[u], k - 1);
+                        nb |= (t == A.a || t == HOLE ? 1u : 0u) << k;
+                    }
                 }
-                nb |= (lane == 63 || nx == A.b || nx == HOLE ? 1u : 0u) << 7;
                 f |= (uint64_t)nb << (8 * u);
             }
             cand &= f;
@@ -540,14 +613,25 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
         // phase 2 (lanes with candidates): resolve occurrences, stage them per STAGE vectors
 #pragma unroll
         for (int ug = 0; ug < UNROLL; ug += STAGE) {
-            uint32_t occ = 0;  // bit 8(u-ug)+k
+            uint32_t occ = 0;  // bit 8(u-ug)+k (by b: the occurrence's b sits there)
             uint64_t c = (cand >> (8 * ug)) & ((STAGE * 8 >= 64) ? ~0ull : ((1ull << (STAGE * 8)) - 1));
 #pragma unroll 1
             while (c) {
                 const int u = (__ffsll((unsigned long long)c) - 1) >> 3;
-                const uint32_t m = (uint32_t)(c >> (8 * u)) & 0xffu;
+                uint32_t m = (uint32_t)(c >> (8 * u)) & 0xffu;
                 c &= ~(0xffull << (8 * u));
-                occ |= occ_vector(A, H, vbase + (ug + u) * 64 + lane, nvec, m, xx) << (8 * u);
+                const int64_t vi = vbase + (ug + u) * 64 + lane;
+                if (!by_b) {
+                    occ |= occ_vector(A, H, vi, nvec, m, xx) << (8 * u);
+                } else {
+                    while (m) {
+                        const int k = __ffs(m) - 1;
+                        m &= m - 1;
+                        const int64_t q = vi * 8 + k, p = prev_live_h(A, q);
+                        // p < 0: the a is the left shard's, which owns the occurrence
+                        if (p >= 0 && tok[p] == A.a && occ_slow(A, H, p, xx)) occ |= 1u << (8 * u + k);
+                    }
+                }
             }
             const uint32_t cnt = __popc(occ);
             const uint32_t incl = wave_incl_scan(cnt);
@@ -561,29 +645,68 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
                 wave_lds_sync();
             }
             uint32_t o = nbuf + incl - cnt;
+            const uint64_t tile_blk = (uint64_t)vbase * 8 / PRES_BLK;
             while (occ) {
                 const int bit = __ffs(occ) - 1;
                 occ &= occ - 1;
-                wrec[o++] = (uint32_t)((vbase + (ug + (bit >> 3)) * 64 + lane) * 8 + (bit & 7));
+                int64_t p = (vbase + (ug + (bit >> 3)) * 64 + lane) * 8 + (bit & 7);
+                if (by_b) {
+                    p = prev_live(tok, p);
+                    if (A.pres && (uint64_t)p / PRES_BLK != tile_blk) pres_set(A, p);
+                }
+                wrec[o++] = (uint32_t)p;
             }
             nbuf += total;
+            if (A.pres && lane == 0) pres_set(A, vbase * 8);
         }
+      }
     }
     if (nbuf) {
         wave_lds_sync();
         wave_flush_records(A, wrec, nbuf);
     }
-    // flush LDS neighbour histograms and the xx count
+    // flush LDS neighbour histograms, the xx count and the streamed-slot count
     xx = wave_sum(xx);
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     if (lane == 0 && any) s_any = 1;
+    if (lane == 0 && tiles) atomicAdd(&s_scanned, (unsigned long long)tiles * WT_VEC * 8);
     __syncthreads();
+    if (threadIdx.x == 0 && s_scanned) atomicAdd(&A.st->scanned_slots, s_scanned);
     if (s_any) {
         for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) {
             uint32_t l = s_left[i], r = s_right[i];
             if (l) atomicAdd(&A.left[i], l);
             if (r) atomicAdd(&A.right[i], r);
         }
+    }
+}
+
+// Presence bitmap from the stream: one workgroup per PRES_GROUP blocks, a bitset per block in LDS
+// (tokens < vp <= 32768), then one coalesced row of words pres[g * vp + t].
+constexpr int PRES_THREADS = 1024;
+__global__ void __launch_bounds__(PRES_THREADS) zbpe_pres_build(const uint16_t *__restrict__ tok, int64_t n, uint32_t vp,
+                                                                 uint32_t *__restrict__ pres) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t bits[];  // PRES_GROUP x (vp / 32) words
+    const uint32_t W = vp / 32;
+    for (uint32_t i = threadIdx.x; i < PRES_GROUP * W; i += PRES_THREADS) bits[i] = 0;
+    __syncthreads();
+    const int64_t g = blockIdx.x;
+    const int64_t beg = g * (int64_t)PRES_GROUP * PRES_BLK, end = min(n, beg + (int64_t)PRES_GROUP * PRES_BLK);
+    for (int64_t p = beg + 8 * threadIdx.x; p < end; p += 8 * PRES_THREADS) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(tok + p);
+        const uint32_t j = (uint32_t)((p - beg) / PRES_BLK);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t t = tok_at(v, k);
+            if (t < vp && p + k < end) atomicOr(&bits[j * W + (t >> 5)], 1u << (t & 31));
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < vp; t += PRES_THREADS) {
+        uint32_t w = 0;
+#pragma unroll 8
+        for (int j = 0; j < PRES_GROUP; j++) w |= ((bits[j * W + (t >> 5)] >> (t & 31)) & 1u) << j;
+        pres[g * vp + t] = w;
     }
 }
 
@@ -602,51 +725,45 @@ __global__ void __launch_bounds__(256) zbpe_apply(uint16_t *tok, int64_t n, cons
     }
 }
 
-// Count update after merge X = (a, b). Four independent chains per neighbour token t < X so
-// each thread waits on one hash-table walk: group 0 decrements (t, a) by left[t], group 1 creates
-// (t, X) = left[t], group 2 decrements (b, t) by right[t], group 3 creates (X, t) = right[t];
-// one extra thread handles (b, a) -> (X, X) and the merged pair itself. Groups are padded to whole
-// waves so the wave-aggregated id / hot-list appends see uniform control flow.
-__device__ inline void update_body(const Tables &T, DevState *st, const uint32_t *__restrict__ left,
-                                   const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
-                                   uint32_t b, uint32_t X, uint32_t top_key, uint32_t gid) {
-    const uint32_t nX = (X + 63) & ~63u;
-    const uint32_t g = gid / nX, t = gid - g * nX;
-    int live_delta = 0;
-    if (g == 0 || g == 2) {
-        const uint32_t c = t < X ? (g == 0 ? left[t] : right[t]) : 0;
-        if (c) {
-            const uint32_t key = g == 0 ? pair_key(t, a) : pair_key(b, t);
-            const uint32_t id = ht_find(T, key);
-            if (id == NO_ID) atomicOr(&st->error, 4u);
-            else {
-                const uint32_t old = atomicSub(&T.id_cnt[id], c);
-                if (old < c) atomicOr(&st->error, 2u);
-                if (old == c) { live_delta--; home_add(T, st, key, false); }
-            }
-        }
-    } else if (g == 1 || g == 3) {
-        const uint32_t c = t < X ? (g == 1 ? left[t] : right[t]) : 0;
-        const uint32_t id = wave_append(&st->num_ids, c != 0);
-        const bool ok = c != 0 && id < T.id_cap;
-        if (c != 0 && !ok) atomicOr(&st->error, 1u);
-        const uint32_t key = g == 1 ? pair_key(t, X) : pair_key(X, t);
-        if (ok) {
-            T.id_key[id] = key;
-            T.id_cnt[id] = c;
-            ht_insert_new(T, key, id);
-            home_add(T, st, key, true);
-            live_delta++;
-        }
-        const bool hot = ok && c >= st->theta;
-        const uint32_t j = wave_append(&st->hot_len, hot);
-        if (hot && j < T.hot_cap) T.hot[j] = id;
-    } else if (gid >= 4 * nX && gid < 4 * nX + 3) {  // three independent chains for the specials (xx, occ: all ranks)
-        const uint32_t which = gid - 4 * nX;
+// Count update after merge X = (a, b), per neighbour token t < X: group 0 decrements (t, a) by
+// left[t], group 1 creates (t, X) = left[t], group 2 decrements (b, t) by right[t], group 3 creates
+// (X, t) = right[t]; the last block handles (b, a) -> (X, X) and the merged pair itself. A block
+// owns UPD_THREADS * per consecutive t of one group: it gathers the nonzero deltas into LDS, then
+// every shared counter (ids, live pairs, hot list, dirty home blocks) takes one atomic per block.
+constexpr int UPD_THREADS = 256;
+constexpr int UPD_MAX_PER = 8;
+__host__ __device__ inline uint32_t update_chunks(uint32_t X, uint32_t per) { return (X + UPD_THREADS * per - 1) / (UPD_THREADS * per); }
+__host__ __device__ inline uint32_t update_blocks(uint32_t X, uint32_t per) { return 4 * update_chunks(X, per) + 1; }
+// t per thread: about 16 blocks per group (fewer, fatter blocks cut the shared atomics)
+__host__ __device__ inline uint32_t update_per(uint32_t X) {
+    const uint32_t p = X / (16 * UPD_THREADS);
+    return p < 1 ? 1 : (p > UPD_MAX_PER ? UPD_MAX_PER : p);
+}
+// home_add without the dirty-list append: returns the block to append (or ~0u)
+__device__ inline uint32_t home_add_nd(const Tables &T, DevState *st, uint32_t key, bool add) {
+    if (!T.home_cnt) return ~0u;
+    const uint32_t s = (uint32_t)(zig_pair_hash(key) & T.home_mask), sh = 8 * (s & 3);
+    const uint32_t old = add ? atomicAdd(&T.home_cnt[s >> 2], 1u << sh) : atomicSub(&T.home_cnt[s >> 2], 1u << sh);
+    if (((old >> sh) & 0xffu) == (add ? 0xffu : 0u)) atomicOr(&st->error, 16u);
+    const uint32_t blk = s / SUMM_SLOTS, bit = 1u << (blk & 31);
+    return (atomicOr(&T.home_dirty[blk >> 5], bit) & bit) ? ~0u : blk;
+}
+__device__ inline void update_block(const Tables &T, DevState *st, const uint32_t *__restrict__ left,
+                                    const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
+                                    uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per) {
+    __shared__ uint32_t s_t[UPD_THREADS * UPD_MAX_PER], s_c[UPD_THREADS * UPD_MAX_PER];
+    __shared__ uint32_t s_hot[UPD_THREADS * UPD_MAX_PER], s_dirty[UPD_THREADS * UPD_MAX_PER];
+    __shared__ uint32_t s_n, s_nhot, s_ndirty, s_base;
+    __shared__ int s_live;
+    const uint32_t nch = update_chunks(X, per);
+    const uint32_t tid = threadIdx.x;
+    if (ublk >= 4 * nch) {  // specials: three independent chains
+        if (tid >= 3) return;
+        int live_delta = 0;
         const uint32_t xx = tail[0];
-        if (which == 0 && xx) pair_dec(T, st, pair_key(b, a), xx);
-        if (which == 1 && xx) pair_new(T, st, pair_key(X, X), xx);
-        if (which == 2) {
+        if (tid == 0 && xx) pair_dec(T, st, pair_key(b, a), xx);
+        if (tid == 1 && xx) pair_new(T, st, pair_key(X, X), xx);
+        if (tid == 2) {
             const uint32_t occ = tail[1];
             const uint32_t top_id = ht_find(T, top_key);
             if (top_id == NO_ID) atomicOr(&st->error, 4u);
@@ -655,16 +772,82 @@ __device__ inline void update_body(const Tables &T, DevState *st, const uint32_t
                 if (old < occ) atomicOr(&st->error, 2u);
                 if (old == occ) { live_delta--; home_add(T, st, top_key, false); }
             }
+            if (T.tok_cnt) {
+                T.tok_cnt[X] += (int32_t)occ;
+                T.tok_cnt[a] -= (int32_t)occ;
+                T.tok_cnt[b] -= (int32_t)occ;
+            }
+        }
+        if (live_delta) atomicAdd(&st->live, live_delta);
+        return;
+    }
+    const uint32_t g = ublk / nch, beg = (ublk - g * nch) * UPD_THREADS * per;
+    const uint32_t *delta = (g < 2) ? left : right;
+    if (tid == 0) { s_n = 0; s_nhot = 0; s_ndirty = 0; s_live = 0; }
+    __syncthreads();
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t t = beg + k * UPD_THREADS + tid;
+        const uint32_t c = t < X ? delta[t] : 0;
+        if (c) {
+            const uint32_t j = atomicAdd(&s_n, 1u);
+            s_t[j] = t;
+            s_c[j] = c;
         }
     }
-    if (g < 4) {
-        const uint32_t sum = wave_sum((uint32_t)live_delta);
-        if ((threadIdx.x & 63) == 0 && sum) atomicAdd((uint32_t *)&st->live, sum);
-    } else if (live_delta) {
-        atomicAdd(&st->live, live_delta);
+    __syncthreads();
+    const uint32_t n = s_n;
+    if (n == 0) return;
+    const bool create = g == 1 || g == 3;
+    if (create && tid == 0) {
+        s_base = atomicAdd(&st->num_ids, n);
+        atomicAdd(&st->live, (int)n);
+    }
+    __syncthreads();
+    const uint32_t theta = st->theta;
+    int live_delta = 0;
+    for (uint32_t i = tid; i < n; i += UPD_THREADS) {
+        const uint32_t t = s_t[i], c = s_c[i];
+        uint32_t dblk = ~0u;
+        if (!create) {
+            const uint32_t key = g == 0 ? pair_key(t, a) : pair_key(b, t);
+            const uint32_t id = ht_find(T, key);
+            if (id == NO_ID) atomicOr(&st->error, 4u);
+            else {
+                const uint32_t old = atomicSub(&T.id_cnt[id], c);
+                if (old < c) atomicOr(&st->error, 2u);
+                if (old == c) { live_delta--; dblk = home_add_nd(T, st, key, false); }
+            }
+        } else {
+            const uint32_t id = s_base + i;
+            const uint32_t key = g == 1 ? pair_key(t, X) : pair_key(X, t);
+            if (id >= T.id_cap) atomicOr(&st->error, 1u);
+            else {
+                T.id_key[id] = key;
+                T.id_cnt[id] = c;
+                ht_insert_new(T, key, id);
+                dblk = home_add_nd(T, st, key, true);
+                if (c >= theta) s_hot[atomicAdd(&s_nhot, 1u)] = id;
+            }
+        }
+        if (dblk != ~0u) s_dirty[atomicAdd(&s_ndirty, 1u)] = dblk;
+    }
+    if (live_delta) atomicAdd(&s_live, live_delta);
+    __syncthreads();
+    if (tid == 0) {
+        if (s_live) atomicAdd(&st->live, s_live);
+        s_base = s_nhot ? atomicAdd(&st->hot_len, s_nhot) : 0;
+        const uint32_t nd = s_ndirty;
+        s_n = nd ? atomicAdd(&st->dirty_len, nd) : 0;  // reuse: base of this block's dirty entries
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < s_nhot; i += UPD_THREADS)
+        if (s_base + i < T.hot_cap) T.hot[s_base + i] = s_hot[i];
+    for (uint32_t i = tid; i < s_ndirty; i += UPD_THREADS) {
+        const uint32_t j = s_n + i;
+        if (j < T.dirty_cap) T.dirty_list[j] = s_dirty[i];
+        else atomicOr(&st->error, 32u);
     }
 }
-__host__ __device__ inline uint32_t update_blocks(uint32_t X) { return (4 * ((X + 63) & ~63u) + 3 + 255) / 256; }
 
 // replaceTopPairWithNewToken in one launch: blocks [0, apply_blocks) rewrite the stream at the
 // recorded occurrences (X at the start, a hole at the consumed b), the rest update the counts
@@ -680,8 +863,17 @@ struct ReplaceArgs {
     uint32_t apply_blocks;
     Halo halo;
     const uint8_t *x0;  // self pairs: parity of the run of a's entering the shard (nullptr: none)
+    int dyn;            // batch mode (see ScanArgs::dyn)
+    const Halo *dhalo;
 };
 __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, DevState *st) {
+    if (R.dyn) {
+        if (st->halt) return;
+        R.top_key = st->cur_key;
+        R.a = R.top_key & 0xFFFF;
+        R.b = R.top_key >> 16;
+        if (R.dhalo) R.halo = *R.dhalo;
+    }
     if (blockIdx.x < R.apply_blocks) {
         const uint32_t cnt = min(st->rec_count, R.rec_cap);
         uint32_t made = 0;  // an occurrence whose b lies in the next shard makes no hole here
@@ -714,12 +906,14 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
         }
         return;
     }
-    update_body(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, (blockIdx.x - R.apply_blocks) * 256 + threadIdx.x);
+    const uint32_t ublk = blockIdx.x - R.apply_blocks;
+    if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != st->top_count) atomicOr(&st->error, 64u);  // occurrences != count
+    update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, update_per(R.X));
 }
 
 // this shard's boundary record: first 3 / last 2 live tokens (holes skipped) and its live count
-__global__ void zbpe_boundary(const uint16_t *__restrict__ tok, int64_t n, int64_t nlive, Boundary *out) {
-    if (threadIdx.x || blockIdx.x) return;
+__global__ void zbpe_boundary(const uint16_t *__restrict__ tok, int64_t n, int64_t nlive, Boundary *out, const DevState *st) {
+    if (threadIdx.x || blockIdx.x || (st && st->halt)) return;
     Boundary B{};
     for (int k = 0; k < 3; k++) B.first[k] = HOLE;
     B.last[0] = B.last[1] = HOLE;
@@ -729,6 +923,18 @@ __global__ void zbpe_boundary(const uint16_t *__restrict__ tok, int64_t n, int64
         if (tok[p] != HOLE) B.last[B.nlast++] = tok[p];
     B.nlive = (uint32_t)nlive;
     *out = B;
+}
+// batch mode: this rank's halo from the gathered boundary records (Engine::halo_from_boundaries)
+__global__ void zbpe_halo_build(const Boundary *__restrict__ bnd, int rank, int world, Halo *out, const DevState *st) {
+    if (threadIdx.x || blockIdx.x || st->halt) return;
+    Halo H{};
+    H.left[0] = H.left[1] = HOLE;
+    H.right[0] = H.right[1] = H.right[2] = HOLE;
+    for (int r = rank - 1; r >= 0 && H.nleft < 2; r--)
+        for (int k = 0; k < bnd[r].nlast && H.nleft < 2; k++) H.left[H.nleft++] = bnd[r].last[k];
+    for (int r = rank + 1; r < world && H.nright < 3; r++)
+        for (int k = 0; k < bnd[r].nfirst && H.nright < 3; k++) H.right[H.nright++] = bnd[r].first[k];
+    *out = H;
 }
 // end of merge: clear the neighbour histograms [0, X) and roll the per-merge counters
 __global__ void __launch_bounds__(256) zbpe_reset_merge(DevState *st, uint32_t *left, uint32_t *right, uint32_t X) {
@@ -751,6 +957,7 @@ __global__ void __launch_bounds__(256) zbpe_reset_merge(DevState *st, uint32_t *
 constexpr int SELF_THREADS = 256;
 constexpr int SELF_PER_THREAD = 32;
 constexpr int SELF_TILE = SELF_THREADS * SELF_PER_THREAD;  // 8192
+static_assert(SELF_TILE == PRES_BLK, "a self-pair tile is one presence block");
 __global__ void __launch_bounds__(SELF_THREADS) zbpe_self_tiles(const uint16_t *__restrict__ tok, int64_t n, uint32_t a,
                                                                 uint8_t *__restrict__ tile_fn) {
     // tile_fn bit0: tile is all a; bit1: parity of the trailing a-run (if not all a)
@@ -885,6 +1092,7 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A, const
         if (threadIdx.x == 0) {
             s_base = atomicAdd(&A.st->rec_count, nrec);
             atomicAdd(A.occ_out, nrec);
+            if (A.pres) pres_set(A, beg);  // SELF_TILE == PRES_BLK: the tile is one presence block
         }
         __syncthreads();
         const uint32_t base = s_base;
@@ -1027,6 +1235,7 @@ __global__ void __launch_bounds__(256) zbpe_hot_build(Tables T, DevState *st) {
 __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState *st, MaxRec *__restrict__ partial,
                                                               const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
                                                               uint32_t X, int roll, const Boundary *__restrict__ bnd, int world) {
+    if (st->halt) return;
     for (uint32_t t = blockIdx.x * ARGMAX_THREADS + threadIdx.x; t < 2 * X; t += gridDim.x * ARGMAX_THREADS) delta[t] = 0;
     const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
     MaxRec r{0, 0, NO_ID};
@@ -1083,6 +1292,7 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
             st->total_occ += st->rec_count;
             st->last_gocc = tail[1];
             st->last_holes = st->holes_made;
+            st->live_tokens -= st->holes_made;
             st->holes_made = 0;
             st->rec_count = 0;
             tail[0] = tail[1] = 0;
@@ -1108,8 +1318,11 @@ __device__ inline Summ summ_slot(uint32_t k) {
 }
 __device__ inline uint32_t home_at(const uint32_t *hc, uint32_t s) { return (hc[s >> 2] >> (8 * (s & 3))) & 0xffu; }
 
+__device__ inline bool tie_skip(const DevState *st, int dyn) { return dyn && (st->halt || !st->tie_on); }
 __global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, uint32_t top, uint32_t cap_mask,
-                                                        uint64_t *__restrict__ tie_list, uint32_t tie_cap) {
+                                                        uint64_t *__restrict__ tie_list, uint32_t tie_cap, int dyn) {
+    if (tie_skip(st, dyn)) return;
+    if (dyn) top = st->top_count;
     const uint32_t n = min(st->hot_len, T.hot_cap);
     const uint32_t stride = gridDim.x * 256;
     for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
@@ -1130,7 +1343,8 @@ __global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, 
 // block summaries of the home histogram (block b covers slots [b*SUMM_SLOTS, ...)): every block
 // when all_nb > 0 (after a rebuild), otherwise only the blocks listed dirty since the last tie
 __global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st, uint32_t nslots, uint32_t all_nb,
-                                                         Summ *__restrict__ out) {
+                                                         Summ *__restrict__ out, int dyn) {
+    if (tie_skip(st, dyn)) return;
     constexpr int PER = SUMM_SLOTS / 256;  // 16 slots = 4 words per thread
     __shared__ Summ sm[256];
     const uint32_t nwork = all_nb ? all_nb : min(st->dirty_len, T.dirty_cap);
@@ -1159,7 +1373,9 @@ __global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st,
     }
 }
 // super-block summaries: one wave composes SUPER_BLOCKS block summaries
-__global__ void __launch_bounds__(256) zbpe_super_summary(const Summ *__restrict__ summ, uint32_t nb, Summ *__restrict__ sup) {
+__global__ void __launch_bounds__(256) zbpe_super_summary(const Summ *__restrict__ summ, uint32_t nb, Summ *__restrict__ sup,
+                                                          const DevState *st, int dyn) {
+    if (tie_skip(st, dyn)) return;
     const uint32_t nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
     const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (w >= nsb) return;
@@ -1247,7 +1463,8 @@ __device__ inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_
 }
 constexpr int DECIDE_THREADS = 256;
 __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, const uint64_t *__restrict__ tie_list,
-                                                                  uint32_t tie_cap, HomeView V) {
+                                                                  uint32_t tie_cap, HomeView V, MergeLog *log, int dyn) {
+    if (tie_skip(st, dyn)) return;
     __shared__ uint64_t s1[DECIDE_THREADS], s2[DECIDE_THREADS];
     __shared__ uint32_t sh[DECIDE_THREADS];
     __shared__ long long s_c1, s_c0, s_cw, s_last;
@@ -1301,6 +1518,54 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
     st->tie_verdict = verdict;
     st->tie_winner = (uint32_t)m1;
     st->dirty_len = 0;
+    if (dyn) {
+        if (st->tie_len != st->tie_count) atomicOr(&st->error, 128u);
+        const uint32_t key = (uint32_t)m1;
+        if (verdict) {
+            st->halt = HALT_TIE;
+            st->halt_at = st->cur_x;
+        } else if ((key & 0xFFFF) == (key >> 16)) {
+            st->halt = HALT_SELF;
+            st->halt_at = st->cur_x;
+        } else {
+            st->cur_key = key;
+            log[st->cur_x - 256] = MergeLog{key, st->top_count, (uint32_t)st->live_tokens, st->tie_count};
+        }
+    }
+}
+
+// Zig map final capacity for D live pairs (zig_order.hpp zig_final_capacity, on the device)
+__device__ inline uint64_t dev_zig_final_capacity(uint64_t D, bool call_after) {
+    uint64_t cap = 8;
+    while (cap * 80 / 100 < D) cap *= 2;
+    if (cap * 80 / 100 == D && call_after) cap *= 2;
+    return cap;
+}
+// batch mode, first kernel of merge X: decide whether the device can run this merge by itself
+__global__ void zbpe_merge_begin(Tables T, DevState *st, uint32_t X, uint64_t home_cap, uint32_t rec_cap, MergeLog *log) {
+    if (threadIdx.x || blockIdx.x || st->halt) return;
+    st->cur_x = X;
+    uint32_t h = HALT_NONE;
+    if (st->live <= 0) h = HALT_DONE;
+    else if (st->hot_len > T.hot_cap || st->top_count == 0) h = HALT_SELECT;
+    else if (st->top_count > rec_cap) h = HALT_RECORDS;
+    else if (st->tie_count > 1) {
+        if (dev_zig_final_capacity((uint64_t)st->live, st->lastpair_count >= 2) != home_cap) h = HALT_HOME;
+        st->tie_on = 1;
+        st->tie_len = 0;
+    } else {
+        st->tie_on = 0;
+        const uint32_t key = st->top_key;
+        if ((key & 0xFFFF) == (key >> 16)) h = HALT_SELF;
+        else {
+            st->cur_key = key;
+            log[X - 256] = MergeLog{key, st->top_count, (uint32_t)st->live_tokens, st->tie_count};
+        }
+    }
+    if (h) {
+        st->halt = h;
+        st->halt_at = X;
+    }
 }
 // rebuild the home histogram for a new Zig capacity
 __global__ void __launch_bounds__(256) zbpe_home_build(Tables T, DevState *st) {

@@ -15,6 +15,8 @@ constexpr int SCAN_TILE = SCAN_THREADS * SCAN_UNROLL * 8;            // tokens p
 constexpr int SCAN_REC_CAP = SCAN_TILE / 2;                          // occurrences per tile (non-overlapping)
 constexpr int LDS_BINS = 1024;                                       // neighbour tokens counted in LDS
 constexpr int COMPACT_TILE = 8192;                                   // tokens per compaction tile
+constexpr int PRES_BLK = 8192;       // stream slots per presence block (a multiple of every wave-tile)
+constexpr int PRES_GROUP = 32;       // presence blocks per bitmap word
 
 __host__ __device__ constexpr inline uint32_t pair_key(uint32_t first, uint32_t second) { return first | (second << 16); }
 
@@ -45,6 +47,32 @@ struct DevState {
     uint32_t consumed;       // 1: this shard's first live token was the b of the left rank's last occurrence
     uint32_t holes_made;     // slots of this shard turned into holes by the current merge
     uint32_t last_holes;     // holes_made of the last merge (rolled by zbpe_select)
+    int32_t pad_by_b;
+    uint32_t pad3;
+    unsigned long long scanned_slots;  // stream slots the scans actually streamed (block skipping)
+    // device-resident merge loop (Engine::run_batch): the host enqueues a batch of merges whose
+    // kernels read the pair from here; a merge the device cannot finish alone halts the batch
+    uint32_t halt;           // HaltReason; every merge-loop kernel returns at once while set
+    uint32_t halt_at;        // merge token X of the halted merge
+    uint32_t cur_x;          // merge token X being processed
+    uint32_t cur_key;        // the pair this merge replaces (after the tie-break)
+    uint32_t tie_on;         // 1: this merge's top count is tied (the tie kernels run)
+    uint32_t pad4;
+    long long live_tokens;   // live tokens of this shard (rolled by zbpe_select)
+};
+// why a device-resident batch stopped (the host finishes that merge on the synchronous path)
+enum HaltReason : uint32_t {
+    HALT_NONE = 0,
+    HALT_DONE = 1,        // no live pairs
+    HALT_SELECT = 2,      // hot-list argmax not valid (overflow / exhausted): rebuild on the host
+    HALT_HOME = 3,        // the Zig map capacity changed: rebuild the home histogram
+    HALT_TIE = 4,         // tie not decided by the cluster test: exact emulation on the host
+    HALT_SELF = 5,        // self pair (a, a): compaction + run-parity path
+    HALT_RECORDS = 6,     // occurrence buffer too small
+};
+// per-merge log written by the device in batch mode
+struct MergeLog {
+    uint32_t key, count, live, ties;
 };
 
 struct Tables {
@@ -60,6 +88,7 @@ struct Tables {
     uint32_t *home_dirty;  // 1 bit per SUMM_SLOTS block: summary stale
     uint32_t *dirty_list;  // stale block indices (each listed once)
     uint32_t dirty_cap;
+    int32_t *tok_cnt;      // [65536] live occurrences per token id (global; picks the scan's key token)
 };
 
 constexpr int COUNT_BINS = 64 + 26 * 32;  // count histogram for choosing theta: exact < 64, then 32 per octave

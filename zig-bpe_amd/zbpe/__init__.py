@@ -127,6 +127,8 @@ class Stats(ctypes.Structure):
         ("distinct_pairs", ctypes.c_uint64),
         ("pair_ids", ctypes.c_uint64),
         ("sum_tokens", ctypes.c_uint64),
+        ("scan_timed_launches", ctypes.c_uint64),
+        ("scan_timed_alg_bytes", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -136,8 +138,10 @@ class Stats(ctypes.Structure):
 EXPORTS = (
     "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_create_dist_host", "zbpe_destroy", "zbpe_last_error",
     "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts",
-    "zbpe_set_option", "zbpe_bench_scan", "zbpe_zig_order_winner", "zbpe_version",
+    "zbpe_set_option", "zbpe_bench_scan", "zbpe_trace", "zbpe_zig_order_winner", "zbpe_version",
 )
+TRACE_COLUMNS = ("merge", "count", "live", "slots", "streamed", "scan_ms", "replace_ms", "select_ms", "wall_ms",
+                 "self_pair", "ties")
 
 _lib = None
 COLLECTIVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t)
@@ -197,6 +201,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
     L.zbpe_bench_scan.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double)]
+    L.zbpe_trace.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.zbpe_zig_order_winner.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
     L.zbpe_version.restype = ctypes.c_char_p
     for name in EXPORTS:
@@ -293,6 +298,17 @@ class Engine:
         ms, gbps = ctypes.c_double(0), ctypes.c_double(0)
         self._check(self._L.zbpe_bench_scan(self._ctx, a, b, reps, ctypes.byref(ms), ctypes.byref(gbps)), "zbpe_bench_scan")
         return ms.value, gbps.value
+
+    def trace(self):
+        """Per-merge rows of the last train (option "trace" = 1): float32 array [merges, len(TRACE_COLUMNS)]."""
+        import numpy as np
+
+        n = ctypes.c_size_t(0)
+        self._check(self._L.zbpe_trace(self._ctx, None, 0, ctypes.byref(n)), "zbpe_trace")
+        out = np.zeros((n.value, len(TRACE_COLUMNS)), dtype=np.float32)
+        if n.value:
+            self._check(self._L.zbpe_trace(self._ctx, _ptr(out), n.value, ctypes.byref(n)), "zbpe_trace")
+        return out
 
     def verify_counts(self) -> int:
         mm = ctypes.c_uint64(0)
@@ -522,5 +538,5 @@ __all__ = [
     "BasicTokenizer", "CharPair", "Merge", "Merges", "Engine", "Stats", "TrainError", "InvalidVocabSize", "InvalidUtf8",
     "OutOfMemory", "DeviceError", "InvalidToken", "InvalidFormat", "InvalidCharacter", "Overflow", "StreamTooLong",
     "InvalidArgument", "InternalError", "load_library", "synth_corpus", "comm_unique_id", "zig_order_winner",
-    "merges_to_text", "vocabStart", "EXPORTS", "torch_collective", "COLLECTIVE_FN",
+    "merges_to_text", "vocabStart", "EXPORTS", "TRACE_COLUMNS", "torch_collective", "COLLECTIVE_FN",
 ]
