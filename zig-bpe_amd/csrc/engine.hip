@@ -56,7 +56,7 @@ void Engine::release() {
     f(T.ht); f(T.id_key); f(T.id_cnt);
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.sup_pending);
     for (auto &e : bev) if (e) (void)hipEventDestroy(e);
     bev.clear();
     if (h_st) (void)hipHostFree(h_st);
@@ -138,12 +138,10 @@ zbpe_status Engine::upload(const uint8_t *text, size_t n, bool shard) {
     n_text = e - s;
     shard_offset = (uint32_t)s;
     next_byte = e < n && shard ? (int)text[e] : -1;
-    Halo H{};
-    H.left[0] = H.left[1] = HOLE;
-    H.right[0] = H.right[1] = H.right[2] = HOLE;
+    Halo H = halo_empty();
     if (shard) {
-        for (size_t i = s; i > 0 && H.nleft < 2; i--) H.left[H.nleft++] = text[i - 1];
-        for (size_t i = e; i < n && H.nright < 3; i++) H.right[H.nright++] = text[i];
+        for (size_t i = s; i > 0 && H.nleft < 2; i--) halo_push_left(H, text[i - 1]);
+        for (size_t i = e; i < n && H.nright < 3; i++) halo_push_right(H, text[i]);
     }
     halo0 = H;
     sharded = shard;
@@ -181,7 +179,7 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     Tables N{};
     N.hot = T.hot; N.hot_cap = T.hot_cap; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
     N.home_dirty = T.home_dirty; N.dirty_list = T.dirty_list; N.dirty_cap = T.dirty_cap;
-    N.tok_cnt = T.tok_cnt;
+    N.tok_cnt = T.tok_cnt; N.sup_pending = T.sup_pending;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
     if (hipMalloc(&N.ht, ht_cap_new * 8) != hipSuccess || hipMalloc(&N.id_key, id_cap_new * 4) != hipSuccess ||
@@ -338,7 +336,8 @@ zbpe_status Engine::select_ready() {
 }
 
 zbpe_status Engine::rebuild_home(uint64_t cap) {
-    const size_t words = cap / 4 + 1;
+    // whole 4096-slot blocks (the tie kernels read a block's slots as 16-B vectors)
+    const size_t words = (std::max<uint64_t>(cap, SUMM_SLOTS) + SUMM_SLOTS - 1) / SUMM_SLOTS * (SUMM_SLOTS / 4);
     if (!T.home_cnt || home_words_cap < words) {
         if (T.home_cnt) (void)hipFree(T.home_cnt);
         T.home_cnt = nullptr;
@@ -355,6 +354,7 @@ zbpe_status Engine::rebuild_home(uint64_t cap) {
     CHECK(ensure(&d_sup, sup_cap, nb / SUPER_BLOCKS + 1, "home super-block summaries"));
     CHECK(ensure(&T.dirty_list, dirty_list_cap, nb, "home dirty list"));
     CHECK(ensure(&T.home_dirty, dirty_bits_cap, nb / 32 + 1, "home dirty bits"));
+    CHECK(ensure(&T.sup_pending, sup_pending_cap, nb / SUPER_BLOCKS + 1, "home super-block pending counts"));
     T.dirty_cap = (uint32_t)dirty_list_cap;
     HIP_OK(hipMemsetAsync(T.home_cnt, 0, words * 4, stream));
     HIP_OK(hipMemsetAsync(T.home_dirty, 0, (nb / 32 + 1) * 4, stream));
@@ -365,7 +365,10 @@ zbpe_status Engine::rebuild_home(uint64_t cap) {
     LAUNCH_OK();
     HIP_OK(hipMemsetAsync(T.home_dirty, 0, (nb / 32 + 1) * 4, stream));
     HIP_OK(hipMemsetAsync(&d_st->dirty_len, 0, 4, stream));
-    zbpe_home_summary<<<(unsigned)std::min<size_t>(nb, 4096), 256, 0, stream>>>(T, d_st, (uint32_t)cap, (uint32_t)nb, d_summ, 0);
+    HIP_OK(hipMemsetAsync(T.sup_pending, 0, (nb / SUPER_BLOCKS + 1) * 4, stream));
+    zbpe_home_summary<<<(unsigned)std::min<size_t>(nb, 4096), 256, 0, stream>>>(T, d_st, (uint32_t)cap, (uint32_t)nb, d_summ, d_sup, 0);
+    LAUNCH_OK();
+    zbpe_super_summary<<<(unsigned)((nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS + 3) / 4, 256, 0, stream>>>(d_summ, (uint32_t)nb, d_sup, d_st, 0);
     LAUNCH_OK();
     home_slots = cap;
     home_rebuilds++;
@@ -384,13 +387,11 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     HIP_OK(hipMemsetAsync(&d_st->tie_len, 0, 4, stream));
     const uint32_t hl = std::min<uint32_t>(h_st->hot_len, T.hot_cap);
     zbpe_tie_collect<<<std::min<uint32_t>(1024, hl / 256 + 1), 256, 0, stream>>>(T, d_st, top, (uint32_t)(cap - 1), d_tie_list,
-                                                                                  (uint32_t)tie_list_cap, 0);
+                                                                                  (uint32_t)tie_list_cap, 0, BeginArgs{});
     LAUNCH_OK();
-    zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)cap, 0, d_summ, 0);
+    zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)cap, 0, d_summ, d_sup, 0);
     LAUNCH_OK();
     const uint32_t nb = (uint32_t)((cap + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
-    zbpe_super_summary<<<(nsb + 3) / 4, 256, 0, stream>>>(d_summ, nb, d_sup, d_st, 0);
-    LAUNCH_OK();
     HomeView V{T.home_cnt, d_summ, d_sup, (uint32_t)cap, nb, nsb};
     zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 0);
     LAUNCH_OK();
@@ -447,8 +448,8 @@ using ScanFn = void (*)(ScanArgs);
 // 0 is the default (unroll 4, non-temporal loads, next-token filter); the others for A/B runs
 static const ScanFn kScanVariants[] = {zbpe_scan_pairs_t<4, true, true>,  zbpe_scan_pairs_t<8, true, true>,
                                        zbpe_scan_pairs_t<4, false, true>, zbpe_scan_pairs_t<4, true, false>,
-                                       zbpe_scan_pairs_t<2, true, true>};
-static const int kScanUnroll[] = {4, 8, 4, 4, 2};
+                                       zbpe_scan_pairs_t<2, true, true>,  zbpe_scan_pairs_t<4, true, true, false>};
+static const int kScanUnroll[] = {4, 8, 4, 4, 2, 4};
 
 zbpe_status Engine::set_scan_variant(int v) {
     if (v < 0 || v >= (int)(sizeof(kScanVariants) / sizeof(kScanVariants[0])))
@@ -540,13 +541,11 @@ zbpe_status Engine::alloc_stream(size_t n) {
 
 // halo of this rank from the gathered boundary records (walks past shards with too few live tokens)
 void Engine::halo_from_boundaries() {
-    Halo H{};
-    H.left[0] = H.left[1] = HOLE;
-    H.right[0] = H.right[1] = H.right[2] = HOLE;
+    Halo H = halo_empty();
     for (int r = rank - 1; r >= 0 && H.nleft < 2; r--)
-        for (int k = 0; k < h_bnd[r].nlast && H.nleft < 2; k++) H.left[H.nleft++] = h_bnd[r].last[k];
+        for (int k = 0; k < h_bnd[r].nlast && H.nleft < 2; k++) halo_push_left(H, h_bnd[r].last[k]);
     for (int r = rank + 1; r < world && H.nright < 3; r++)
-        for (int k = 0; k < h_bnd[r].nfirst && H.nright < 3; k++) H.right[H.nright++] = h_bnd[r].first[k];
+        for (int k = 0; k < h_bnd[r].nfirst && H.nright < 3; k++) halo_push_right(H, h_bnd[r].first[k]);
     halo = H;
 }
 
@@ -589,6 +588,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     T.home_mask = 0;
     if (T.home_cnt) { (void)hipFree(T.home_cnt); T.home_cnt = nullptr; home_words_cap = 0; }
     if (T.home_dirty) { (void)hipFree(T.home_dirty); T.home_dirty = nullptr; dirty_bits_cap = 0; }
+    if (T.sup_pending) { (void)hipFree(T.sup_pending); T.sup_pending = nullptr; sup_pending_cap = 0; }
     if (T.dirty_list) { (void)hipFree(T.dirty_list); T.dirty_list = nullptr; dirty_list_cap = 0; T.dirty_cap = 0; }
     hot_stale = true;
     halo = halo0;
@@ -726,14 +726,12 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         const bool timed = merge_timing && X % merge_timing == 0;
         if (timed) HIP_OK(hipEventRecord(bev[4 * i], stream));
         uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
-        zbpe_merge_begin<<<1, 64, 0, stream>>>(T, d_st, X, C, (uint32_t)rec_cap, d_log);
+        // merge start (halt checks, tie_on) fused into the tie collection
+        zbpe_tie_collect<<<64, 256, 0, stream>>>(T, d_st, 0, (uint32_t)(C ? C - 1 : 0), d_tie_list, (uint32_t)tie_list_cap, 1,
+                                                 BeginArgs{X, C, (uint32_t)rec_cap, d_log});
         LAUNCH_OK();
         if (C) {
-            zbpe_tie_collect<<<64, 256, 0, stream>>>(T, d_st, 0, (uint32_t)(C - 1), d_tie_list, (uint32_t)tie_list_cap, 1);
-            LAUNCH_OK();
-            zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)C, 0, d_summ, 1);
-            LAUNCH_OK();
-            zbpe_super_summary<<<(nsb + 3) / 4, 256, 0, stream>>>(d_summ, nb, d_sup, d_st, 1);
+            zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)C, 0, d_summ, d_sup, 1);
             LAUNCH_OK();
             zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 1);
             LAUNCH_OK();

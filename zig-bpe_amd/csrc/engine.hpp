@@ -74,7 +74,7 @@ struct Engine {
     size_t recount_cap = 0;
     uint32_t *d_count_hist = nullptr, *h_count_hist = nullptr;
     size_t hot_cap_alloc = 0;
-    size_t home_words_cap = 0, dirty_list_cap = 0, dirty_bits_cap = 0;
+    size_t home_words_cap = 0, dirty_list_cap = 0, dirty_bits_cap = 0, sup_pending_cap = 0;
     uint64_t home_slots = 0;    // Zig capacity the home histogram is kept for (0: none)
     Summ *d_summ = nullptr, *d_sup = nullptr;
     size_t summ_cap = 0, sup_cap = 0;

@@ -79,6 +79,7 @@ __device__ inline void home_add(const Tables &T, DevState *st, uint32_t key, boo
         const uint32_t j = atomicAdd(&st->dirty_len, 1u);
         if (j < T.dirty_cap) T.dirty_list[j] = blk;
         else atomicOr(&st->error, 32u);
+        if (T.sup_pending) atomicAdd(&T.sup_pending[blk / SUPER_BLOCKS], 1u);
     }
 }
 // Wave-aggregated append: one atomic per wave. Every lane of the wave must call it.
@@ -342,8 +343,8 @@ __device__ inline bool scan_args_resolve(ScanArgs &A) {
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
 constexpr int64_t NONE_POS = INT64_MIN;
 __device__ inline uint32_t tok_h(const ScanArgs &A, int64_t p) {
-    if (p >= A.n) return A.halo.right[p - A.n];
-    if (p < 0) return A.halo.left[-p - 1];
+    if (p >= A.n) return halo_right(A.halo, p - A.n);
+    if (p < 0) return halo_left(A.halo, -p - 1);
     return A.tok[p];
 }
 __device__ inline int64_t next_live_h(const ScanArgs &A, int64_t p) {
@@ -503,9 +504,21 @@ __device__ inline void pres_set(const ScanArgs &A, int64_t pos) {
     atomicOr(&A.pres[(blk / PRES_GROUP) * A.vp + A.X], 1u << (blk % PRES_GROUP));
 }
 
-template <int UNROLL, bool NT, bool FILTER>
-__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
-    if (!scan_args_resolve(A)) return;
+template <int UNROLL, bool NT, bool FILTER, bool PIPE>
+__device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A);
+template <int UNROLL, bool NT, bool FILTER, bool PIPE = true>
+__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
+    if (!A0.dyn) return scan_pairs_body<UNROLL, NT, FILTER, PIPE>(A0);
+    if (A0.st->halt) return;
+    const uint32_t k = A0.st->cur_key;
+    Halo h = A0.halo;
+    if (A0.dhalo) h = *A0.dhalo;
+    const ScanArgs A{A0.tok, A0.n, k & 0xFFFF, k >> 16, A0.left, A0.right, A0.st, A0.rec, A0.rec_cap, A0.count_deltas,
+                     A0.xx_out, A0.occ_out, h, A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr};
+    scan_pairs_body<UNROLL, NT, FILTER, PIPE>(A);
+}
+template <int UNROLL, bool NT, bool FILTER, bool PIPE>
+__device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A) {
     constexpr int STAGE = 4;                      // vectors per lane per record-staging step
     constexpr uint32_t WREC = 64 * STAGE * 8 / 2;  // at most one occurrence per 2 tokens
     static_assert(UNROLL % STAGE == 0 || UNROLL < STAGE, "UNROLL must be a multiple of 4 (or < 4)");
@@ -530,7 +543,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
     uint32_t *wrec = s_rec[wib];
     uint32_t nbuf = 0;  // wave-uniform: records staged in wrec
     uint32_t xx = 0, any = 0, tiles = 0;
-    if (by_b && blockIdx.x == 0 && threadIdx.x == 0 && A.halo.nright > 0 && A.halo.right[0] == A.b) {
+    if (by_b && blockIdx.x == 0 && threadIdx.x == 0 && A.halo.nright > 0 && halo_right(A.halo, 0) == A.b) {
         // the occurrence leaving the shard: its b is the next shard's, so no tile here holds it
         const int64_t p = prev_live(tok, A.n);
         if (p >= 0 && tok[p] == A.a && occ_slow(A, H, p, xx)) {
@@ -555,34 +568,37 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
           }
           todo = __ballot(pr);
       }
-      while (todo) {
-        const int64_t wt = wt0 + (int64_t)__builtin_ctzll(todo) * wstride;
-        todo &= todo - 1;
+      if (!todo) continue;
+      // phase 1: stream UNROLL x 16 B per lane, keep only the positions holding the key token
+      uint4 v[UNROLL];
+      auto load_tile = [&](int64_t vb) {
+#pragma unroll
+          for (int u = 0; u < UNROLL; u++) {
+              const int64_t vi = vb + u * 64 + lane;
+              if (vi < nvec) {
+                  const uint4 *src = reinterpret_cast<const uint4 *>(tok) + vi;
+                  if constexpr (NT) {
+                      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
+                      v[u] = make_uint4(x.x, x.y, x.z, x.w);
+                  } else {
+                      v[u] = *src;
+                  }
+              } else {
+                  v[u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+              }
+          }
+      };
+      int64_t wt = wt0 + (int64_t)__builtin_ctzll(todo) * wstride;
+      todo &= todo - 1;
+      load_tile(wt * WT_VEC);
+      for (;;) {
         const int64_t vbase = wt * WT_VEC;
         tiles++;
-        // phase 1: stream UNROLL x 16 B per lane, keep only the positions holding the key token
-        uint4 v[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++) {
-            const int64_t vi = vbase + u * 64 + lane;
-            if (vi < nvec) {
-                const uint4 *src = reinterpret_cast<const uint4 *>(tok) + vi;
-                if constexpr (NT) {
-                    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
-                    v[u] = make_uint4(x.x, x.y, x.z, x.w);
-                } else {
-                    v[u] = *src;
-                }
-            } else {
-                v[u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-            }
-        }
         uint64_t cand = 0;  // bit 8u+k: token k of vector u is the key token
 #pragma unroll
         for (int u = 0; u < UNROLL; u++) cand |= (uint64_t)match8(v[u], key_tok) << (8 * u);
-        if (__ballot(cand != 0) == 0) continue;  // wave-uniform: no key token in these 64*UNROLL*16 B
-        if constexpr (FILTER) {
+        if (FILTER && __ballot(cand != 0) != 0) {
             // by a: keep a where the next slot holds b or a hole; by b: keep b where the previous slot
             // holds a or a hole (across lanes by a shuffle; lanes 63 / 0 keep their edge candidate)
             uint64_t f = 0;
@@ -610,6 +626,16 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
             }
             cand &= f;
         }
+        // the tile's vectors are dead: start streaming the next present tile (its loads overlap
+        // this tile's phase 2)
+        const bool more = todo != 0;
+        int64_t wt_next = 0;
+        if (more) {
+            wt_next = wt0 + (int64_t)__builtin_ctzll(todo) * wstride;
+            todo &= todo - 1;
+            if (PIPE) load_tile(wt_next * WT_VEC);
+        }
+        if (__ballot(cand != 0) != 0) {
         // phase 2 (lanes with candidates): resolve occurrences, stage them per STAGE vectors
 #pragma unroll
         for (int ug = 0; ug < UNROLL; ug += STAGE) {
@@ -659,6 +685,10 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A) {
             nbuf += total;
             if (A.pres && lane == 0) pres_set(A, vbase * 8);
         }
+        }  // tile has candidates
+        if (!more) break;
+        wt = wt_next;
+        if (!PIPE) load_tile(wt * WT_VEC);
       }
     }
     if (nbuf) {
@@ -746,7 +776,9 @@ __device__ inline uint32_t home_add_nd(const Tables &T, DevState *st, uint32_t k
     const uint32_t old = add ? atomicAdd(&T.home_cnt[s >> 2], 1u << sh) : atomicSub(&T.home_cnt[s >> 2], 1u << sh);
     if (((old >> sh) & 0xffu) == (add ? 0xffu : 0u)) atomicOr(&st->error, 16u);
     const uint32_t blk = s / SUMM_SLOTS, bit = 1u << (blk & 31);
-    return (atomicOr(&T.home_dirty[blk >> 5], bit) & bit) ? ~0u : blk;
+    if (atomicOr(&T.home_dirty[blk >> 5], bit) & bit) return ~0u;
+    if (T.sup_pending) atomicAdd(&T.sup_pending[blk / SUPER_BLOCKS], 1u);
+    return blk;
 }
 __device__ inline void update_block(const Tables &T, DevState *st, const uint32_t *__restrict__ left,
                                     const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
@@ -872,7 +904,6 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
         R.top_key = st->cur_key;
         R.a = R.top_key & 0xFFFF;
         R.b = R.top_key >> 16;
-        if (R.dhalo) R.halo = *R.dhalo;
     }
     if (blockIdx.x < R.apply_blocks) {
         const uint32_t cnt = min(st->rec_count, R.rec_cap);
@@ -890,11 +921,13 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
         if ((threadIdx.x & 63) == 0 && made) atomicAdd(&st->holes_made, made);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->consumed = 0;
-            if (R.halo.nleft > 0 || R.x0) {
+            if (R.dhalo) R.halo = *R.dhalo;
+            const Halo &Hl = R.halo;
+            if (Hl.nleft > 0 || R.x0) {
                 const int64_t f = next_live(R.tok, R.n, -1);
                 if (f >= 0) {
                     const uint32_t tf = R.tok[f];
-                    const bool c = R.a != R.b ? (R.halo.nleft > 0 && R.halo.left[0] == R.a && tf == R.b)
+                    const bool c = R.a != R.b ? (Hl.nleft > 0 && halo_left(Hl, 0) == R.a && tf == R.b)
                                               : (tf == R.a && R.x0 && (*R.x0 & 1));
                     if (c) {
                         R.tok[f] = HOLE;
@@ -927,13 +960,11 @@ __global__ void zbpe_boundary(const uint16_t *__restrict__ tok, int64_t n, int64
 // batch mode: this rank's halo from the gathered boundary records (Engine::halo_from_boundaries)
 __global__ void zbpe_halo_build(const Boundary *__restrict__ bnd, int rank, int world, Halo *out, const DevState *st) {
     if (threadIdx.x || blockIdx.x || st->halt) return;
-    Halo H{};
-    H.left[0] = H.left[1] = HOLE;
-    H.right[0] = H.right[1] = H.right[2] = HOLE;
+    Halo H = halo_empty();
     for (int r = rank - 1; r >= 0 && H.nleft < 2; r--)
-        for (int k = 0; k < bnd[r].nlast && H.nleft < 2; k++) H.left[H.nleft++] = bnd[r].last[k];
+        for (int k = 0; k < bnd[r].nlast && H.nleft < 2; k++) halo_push_left(H, bnd[r].last[k]);
     for (int r = rank + 1; r < world && H.nright < 3; r++)
-        for (int k = 0; k < bnd[r].nfirst && H.nright < 3; k++) H.right[H.nright++] = bnd[r].first[k];
+        for (int k = 0; k < bnd[r].nfirst && H.nright < 3; k++) halo_push_right(H, bnd[r].first[k]);
     *out = H;
 }
 // end of merge: clear the neighbour histograms [0, X) and roll the per-merge counters
@@ -1066,8 +1097,8 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A, const
         if (off_par) continue;
         // the shard is compacted: positions past its end continue in the right halo, before it in the left
         auto at = [&](int64_t q) -> uint32_t {
-            if (q < n) return q >= 0 ? tok[q] : (-q - 1 < A.halo.nleft ? A.halo.left[-q - 1] : HOLE);
-            return q - n < A.halo.nright ? A.halo.right[q - n] : HOLE;
+            if (q < n) return q >= 0 ? tok[q] : (-q - 1 < A.halo.nleft ? halo_left(A.halo, -q - 1) : HOLE);
+            return q - n < A.halo.nright ? halo_right(A.halo, q - n) : HOLE;
         };
         if (at(p + 1) != a) continue;
         // occurrence at p
@@ -1250,20 +1281,21 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < ARGMAX_THREADS / WAVE; w++) r = max_combine(r, sm[w]);
-        partial[blockIdx.x] = r;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // write-through (sc1) partial, drained before the ticket; the last block reads the partials
+        // with sc1 loads (no release / acquire fences: cdna_hip_programming.md section 6 G16, R1)
+        __hip_atomic_store(&partial[blockIdx.x].cnt, r.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&partial[blockIdx.x].ties, r.ties, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&partial[blockIdx.x].id, r.id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         s_last = atomicAdd(&st->ticket, 1u) == gridDim.x - 1;
     }
     __syncthreads();
     if (!s_last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
     MaxRec q{0, 0, NO_ID};
-    for (uint32_t i = threadIdx.x; i < gridDim.x; i += ARGMAX_THREADS) q = max_combine(q, partial[i]);
+    for (uint32_t i = threadIdx.x; i < gridDim.x; i += ARGMAX_THREADS)
+        q = max_combine(q, MaxRec{__hip_atomic_load(&partial[i].cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                  __hip_atomic_load(&partial[i].ties, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                  __hip_atomic_load(&partial[i].id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)});
     q = wave_max(q);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = q;
@@ -1293,6 +1325,7 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
             st->last_gocc = tail[1];
             st->last_holes = st->holes_made;
             st->live_tokens -= st->holes_made;
+            st->tie_len = 0;
             st->holes_made = 0;
             st->rec_count = 0;
             tail[0] = tail[1] = 0;
@@ -1319,10 +1352,59 @@ __device__ inline Summ summ_slot(uint32_t k) {
 __device__ inline uint32_t home_at(const uint32_t *hc, uint32_t s) { return (hc[s >> 2] >> (8 * (s & 3))) & 0xffu; }
 
 __device__ inline bool tie_skip(const DevState *st, int dyn) { return dyn && (st->halt || !st->tie_on); }
+// Zig map final capacity for D live pairs (zig_order.hpp zig_final_capacity, on the device)
+__device__ inline uint64_t dev_zig_final_capacity(uint64_t D, bool call_after) {
+    uint64_t cap = 8;
+    while (cap * 80 / 100 < D) cap *= 2;
+    if (cap * 80 / 100 == D && call_after) cap *= 2;
+    return cap;
+}
+// Batch mode, start of merge X: can the device run this merge by itself? Every block of the first
+// kernel of the merge evaluates the same predicate on the (read-only here) selection state; block 0
+// records the outcome: the halt, or tie_on / cur_key and the merge log.
+struct BeginArgs {
+    uint32_t X;
+    uint64_t home_cap;  // Zig capacity the home histogram is kept for
+    uint32_t rec_cap;
+    MergeLog *log;
+};
+__device__ inline uint32_t merge_begin_eval(const Tables &T, const DevState *st, const BeginArgs &B, bool *tie) {
+    *tie = false;
+    if (st->live <= 0) return HALT_DONE;
+    if (st->hot_len > T.hot_cap || st->top_count == 0) return HALT_SELECT;
+    if (st->top_count > B.rec_cap) return HALT_RECORDS;
+    if (st->tie_count > 1) {
+        if (dev_zig_final_capacity((uint64_t)st->live, st->lastpair_count >= 2) != B.home_cap) return HALT_HOME;
+        *tie = true;
+        return HALT_NONE;
+    }
+    const uint32_t key = st->top_key;
+    return (key & 0xFFFF) == (key >> 16) ? HALT_SELF : HALT_NONE;
+}
+__device__ inline void merge_begin_commit(DevState *st, const BeginArgs &B, uint32_t h, bool tie) {
+    st->cur_x = B.X;
+    st->tie_on = tie ? 1u : 0u;
+    if (h) {
+        st->halt = h;
+        st->halt_at = B.X;
+    } else if (!tie) {
+        const uint32_t key = st->top_key;
+        st->cur_key = key;
+        B.log[B.X - 256] = MergeLog{key, st->top_count, (uint32_t)st->live_tokens, st->tie_count};
+    }
+}
 __global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, uint32_t top, uint32_t cap_mask,
-                                                        uint64_t *__restrict__ tie_list, uint32_t tie_cap, int dyn) {
-    if (tie_skip(st, dyn)) return;
-    if (dyn) top = st->top_count;
+                                                        uint64_t *__restrict__ tie_list, uint32_t tie_cap, int dyn,
+                                                        BeginArgs B) {
+    if (dyn) {
+        if (st->halt) return;
+        bool tie;
+        const uint32_t h = merge_begin_eval(T, st, B, &tie);
+        __syncthreads();  // every thread has read the state before block 0 updates it
+        if (blockIdx.x == 0 && threadIdx.x == 0) merge_begin_commit(st, B, h, tie);
+        if (h || !tie) return;
+        top = st->top_count;
+    }
     const uint32_t n = min(st->hot_len, T.hot_cap);
     const uint32_t stride = gridDim.x * 256;
     for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
@@ -1343,7 +1425,7 @@ __global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, 
 // block summaries of the home histogram (block b covers slots [b*SUMM_SLOTS, ...)): every block
 // when all_nb > 0 (after a rebuild), otherwise only the blocks listed dirty since the last tie
 __global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st, uint32_t nslots, uint32_t all_nb,
-                                                         Summ *__restrict__ out, int dyn) {
+                                                         Summ *__restrict__ out, Summ *__restrict__ sup, int dyn) {
     if (tie_skip(st, dyn)) return;
     constexpr int PER = SUMM_SLOTS / 256;  // 16 slots = 4 words per thread
     __shared__ Summ sm[256];
@@ -1365,9 +1447,37 @@ __global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st,
             if ((threadIdx.x & (2 * sp - 1)) == 0) sm[threadIdx.x] = summ_cat(sm[threadIdx.x], sm[threadIdx.x + sp]);
             __syncthreads();
         }
+        __shared__ uint32_t s_last;
         if (threadIdx.x == 0) {
-            out[blk] = sm[0];
+            // write-through (sc1) stores drained before the arrival count: the last arriver of the
+            // super-block reads them with sc1 loads, no release / acquire fence (cdna_hip_programming.md
+            // section 6 Guideline 16, R1)
+            __hip_atomic_store(&out[blk].q, sm[0].q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&out[blk].m, sm[0].m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             atomicAnd(&T.home_dirty[blk >> 5], ~(1u << (blk & 31)));
+            s_last = 0;
+            if (!all_nb && T.sup_pending) {  // the last dirty block of its super-block recomputes the super summary
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                s_last = atomicSub(&T.sup_pending[blk / SUPER_BLOCKS], 1u) == 1u;
+            }
+        }
+        __syncthreads();
+        if (s_last && threadIdx.x < 64) {
+            const uint32_t nb = (nslots + SUMM_SLOTS - 1) / SUMM_SLOTS, sb = blk / SUPER_BLOCKS, lane = threadIdx.x;
+            const uint32_t bi = sb * SUPER_BLOCKS + lane;
+            Summ x{0, 0};
+            if (bi < nb) {
+                x.q = __hip_atomic_load(&out[bi].q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                x.m = __hip_atomic_load(&out[bi].m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                Summ y;
+                y.q = __shfl_down(x.q, off);
+                y.m = __shfl_down(x.m, off);
+                if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
+            }
+            if (lane == 0) sup[sb] = x;
         }
         __syncthreads();
     }
@@ -1416,27 +1526,147 @@ struct HomeView {
     const Summ *summ, *sup;
     uint32_t C, nb, nsb;
 };
-// carry into slot s = m of the composition over slots s+1 .. s-1 (circular), by one wave:
-// partial block, blocks to the end of the super-block, the other super-blocks, blocks up to s's
-// block, partial block
+// ordered composition by one wave of the slots [lo, hi) inside the summary block starting at
+// `base`: lane L owns slots base + 64L .. +63 and reads them as four 16-B vectors (the histogram
+// is allocated in whole 4096-slot blocks)
+__device__ __attribute__((always_inline)) inline Summ wave_compose_slots(const uint32_t *hc, uint32_t base, uint32_t lo, uint32_t hi) {
+    const uint32_t lane = threadIdx.x & 63, s0 = base + 64 * lane;
+    Summ x{0, 0};
+    if (hi > lo && s0 < hi && s0 + 64 > lo) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(hc + s0 / 4);
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const uint4 w4 = p[v];
+            const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint32_t s = s0 + 16 * v + k;
+                if (s >= lo && s < hi) x = summ_cat(x, summ_slot((w[k >> 2] >> (8 * (k & 3))) & 0xffu));
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        Summ y;
+        y.q = __shfl_down(x.q, off);
+        y.m = __shfl_down(x.m, off);
+        if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
+    }
+    Summ r;
+    r.q = __shfl(x.q, 0);
+    r.m = __shfl(x.m, 0);
+    return r;
+}
+// ordered reduction over the lanes of one wave (lane i absorbs lane i + off), result broadcast
+__device__ inline Summ wave_reduce_summ(Summ x) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        Summ y;
+        y.q = __shfl_down(x.q, off);
+        y.m = __shfl_down(x.m, off);
+        if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
+    }
+    Summ r;
+    r.q = __shfl(x.q, 0);
+    r.m = __shfl(x.m, 0);
+    return r;
+}
+// carry into slot s = m of the composition over slots s+1 .. s-1 (circular), by one wave: the
+// slots after s in its block, the blocks after it in its super-block, the other super-blocks, the
+// blocks before it in its super-block, the slots before s. Every load is issued before the first
+// reduction (one memory latency, not five).
 __device__ inline int64_t wave_carry_into(const HomeView &V, uint32_t s) {
-    const uint32_t b = s / SUMM_SLOTS, sb = b / SUPER_BLOCKS;
-    auto slot = [&](uint32_t i) { return summ_slot(home_at(V.hc, i)); };
-    auto blk = [&](uint32_t i) { return V.summ[i]; };
-    auto sup = [&](uint32_t i) { return V.sup[i % V.nsb]; };
-    Summ x = wave_compose(s + 1, min(V.C, (b + 1) * SUMM_SLOTS), slot);
-    x = summ_cat(x, wave_compose(b + 1, min(V.nb, (sb + 1) * SUPER_BLOCKS), blk));
-    x = summ_cat(x, wave_compose(sb + 1, sb + V.nsb, sup));
-    x = summ_cat(x, wave_compose(sb * SUPER_BLOCKS, b, blk));
-    x = summ_cat(x, wave_compose(b * SUMM_SLOTS, s, slot));
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t b = s / SUMM_SLOTS, sb = b / SUPER_BLOCKS, bbase = b * SUMM_SLOTS;
+    const uint32_t s0 = bbase + 64 * lane, bend = min(V.C, bbase + SUMM_SLOTS);
+    uint32_t w[16];
+    if (s0 < bend) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(V.hc + s0 / 4);
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const uint4 q = p[v];
+            w[4 * v] = q.x; w[4 * v + 1] = q.y; w[4 * v + 2] = q.z; w[4 * v + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = 0;
+    }
+    const uint32_t bi = sb * SUPER_BLOCKS + lane;
+    const Summ bs = bi < V.nb ? V.summ[bi] : Summ{0, 0};
+    const uint32_t nsup = V.nsb - 1, per = (nsup + 63) / 64, i0 = min(nsup, lane * per), i1 = min(nsup, i0 + per);
+    Summ x3{0, 0};
+    for (uint32_t i = i0; i < i1; i++) x3 = summ_cat(x3, V.sup[(sb + 1 + i) % V.nsb]);
+    Summ x1{0, 0}, x5{0, 0};
+#pragma unroll
+    for (int k = 0; k < 64; k++) {
+        const uint32_t t = s0 + k;
+        const Summ e = summ_slot((w[k >> 2] >> (8 * (k & 3))) & 0xffu);
+        if (t > s && t < bend) x1 = summ_cat(x1, e);
+        if (t < s) x5 = summ_cat(x5, e);
+    }
+    const Summ x2 = (bi > b && bi < V.nb) ? bs : Summ{0, 0};
+    const Summ x4 = bi < b ? bs : Summ{0, 0};
+    Summ x = wave_reduce_summ(x1);
+    x = summ_cat(x, wave_reduce_summ(x2));
+    x = summ_cat(x, wave_reduce_summ(x3));
+    x = summ_cat(x, wave_reduce_summ(x4));
+    x = summ_cat(x, wave_reduce_summ(x5));
     return x.m;
 }
-// last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none)
-__device__ inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int64_t carry_in) {
+// first free slot at or after h given the carry into h, by one wave, 64 slots per step; -1 when
+// the run reaches slot C-1 (wraps) or is absurdly long
+__device__ inline int64_t wave_first_free(const HomeView &V, uint32_t h, int64_t carry_in) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t per = (hi - lo + 63) / 64, b = lo + min(hi - lo, lane * per), e = min(hi, b + per);
+    int64_t c = carry_in;
+    for (uint32_t base = h; base < V.C && base - h <= (1u << 20); base += 64) {
+        const uint32_t s = base + lane;
+        const bool valid = s < V.C;
+        const int64_t k = valid ? (int64_t)home_at(V.hc, s) : 0;
+        // carry into slot s: composition of the slots [base, s) applied to c (exclusive scan)
+        Summ inc = summ_slot((uint32_t)k);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            Summ y;
+            y.q = __shfl_up(inc.q, off);
+            y.m = __shfl_up(inc.m, off);
+            if ((int)lane >= off) inc = summ_cat(y, inc);
+        }
+        Summ ex;
+        ex.q = __shfl_up(inc.q, 1);
+        ex.m = __shfl_up(inc.m, 1);
+        if (lane == 0) ex = Summ{0, 0};
+        const int64_t cin = max(ex.m, c + ex.q);
+        const uint64_t fr = __ballot(valid && cin + k == 0);
+        if (fr) return (int64_t)base + __builtin_ctzll(fr);
+        if (base + 64 >= V.C) return -1;
+        const int64_t tq = __shfl(inc.q, 63), tm = __shfl(inc.m, 63);
+        c = max(tm, c + tq);
+    }
+    return -1;
+}
+// last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none)
+// last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none); lo is a multiple
+// of 64 and hi - lo <= 4096: lane L owns slots lo + 64L .. +63, read once as four 16-B vectors
+__device__ inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int64_t carry_in) {
+    const uint32_t lane = threadIdx.x & 63, s0 = lo + 64 * lane;
+    uint32_t w[16];
+    const bool mine = s0 < hi;
+    if (mine) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(V.hc + s0 / 4);
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const uint4 q = p[v];
+            w[4 * v] = q.x; w[4 * v + 1] = q.y; w[4 * v + 2] = q.z; w[4 * v + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = 0;
+    }
     Summ x{0, 0};
-    for (uint32_t i = b; i < e; i++) x = summ_cat(x, summ_slot(home_at(V.hc, i)));
+#pragma unroll
+    for (int k = 0; k < 64; k++)
+        if (s0 + k < hi) x = summ_cat(x, summ_slot((w[k >> 2] >> (8 * (k & 3))) & 0xffu));
     // exclusive ordered scan over lanes
     Summ inc = x;
 #pragma unroll
@@ -1452,10 +1682,13 @@ __device__ inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_
     if (lane == 0) ex = Summ{0, 0};
     int64_t c = max(ex.m, carry_in + ex.q);
     long long last = -1;
-    for (uint32_t i = b; i < e; i++) {
-        const int64_t k = home_at(V.hc, i);
-        if (c + k == 0) last = i;
-        else c = c + k - 1;
+#pragma unroll
+    for (int k = 0; k < 64; k++) {
+        if (s0 + k < hi) {
+            const int64_t kk = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+            if (c + kk == 0) last = s0 + k;
+            else c = c + kk - 1;
+        }
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) last = max(last, (long long)__shfl_xor(last, off));
@@ -1467,7 +1700,7 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
     if (tie_skip(st, dyn)) return;
     __shared__ uint64_t s1[DECIDE_THREADS], s2[DECIDE_THREADS];
     __shared__ uint32_t sh[DECIDE_THREADS];
-    __shared__ long long s_c1, s_c0, s_cw, s_last;
+    __shared__ long long s_c1, s_c0, s_cw, s_last, s_free;
     const uint32_t len = min(st->tie_len, tie_cap);
     uint64_t m1 = ~0ull, m2 = ~0ull;
     uint32_t hmax = 0;
@@ -1496,7 +1729,12 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
     if (w == 1) { const int64_t c = wave_carry_into(V, 0); if ((threadIdx.x & 63) == 0) s_c0 = c; }
     if (w == 2) { const int64_t c = ws ? wave_carry_into(V, ws) : 0; if ((threadIdx.x & 63) == 0) s_cw = c; }
     __syncthreads();
-    // the run wrapping past slot C-1 (if any) starts after the last free slot of [ws, C)
+    // wave 0: end of h1's run; wave 2: the run wrapping past slot C-1 (if any) starts after the
+    // last free slot of [ws, C)
+    if (w == 0) {
+        const int64_t f = wave_first_free(V, h1, s_c1);
+        if ((threadIdx.x & 63) == 0) s_free = f;
+    }
     if (w == 2) {
         const int64_t lf = s_c0 > 0 ? wave_last_free(V, ws, V.C, ws ? s_cw : s_c0) : -2;
         if ((threadIdx.x & 63) == 0) s_last = lf;
@@ -1504,15 +1742,9 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
     __syncthreads();
     if (threadIdx.x) return;
     uint32_t verdict = st->tie_len > tie_cap ? 1u : 0u;
-    int64_t c = s_c1;  // first free slot at or after h1
-    uint32_t s = h1;
-    for (;; s++) {
-        if (s >= V.C || s - h1 > (1u << 20)) { verdict = 1; break; }  // the run of h1 wraps (or is absurdly long)
-        const int64_t k = home_at(V.hc, s);
-        if (c + k == 0) break;
-        c = c + k - 1;
-    }
-    if (m2 != ~0ull && s > (uint32_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
+    const int64_t s = s_free;  // first free slot at or after h1
+    if (s < 0) verdict = 1;     // the run of h1 wraps (or is absurdly long)
+    if (m2 != ~0ull && s > (int64_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
     const long long lf = s_last;
     if (lf != -2 && (lf < 0 || (long long)hmax >= lf + 1)) verdict = 1;  // a tied pair may have wrapped
     st->tie_verdict = verdict;
@@ -1534,39 +1766,6 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
     }
 }
 
-// Zig map final capacity for D live pairs (zig_order.hpp zig_final_capacity, on the device)
-__device__ inline uint64_t dev_zig_final_capacity(uint64_t D, bool call_after) {
-    uint64_t cap = 8;
-    while (cap * 80 / 100 < D) cap *= 2;
-    if (cap * 80 / 100 == D && call_after) cap *= 2;
-    return cap;
-}
-// batch mode, first kernel of merge X: decide whether the device can run this merge by itself
-__global__ void zbpe_merge_begin(Tables T, DevState *st, uint32_t X, uint64_t home_cap, uint32_t rec_cap, MergeLog *log) {
-    if (threadIdx.x || blockIdx.x || st->halt) return;
-    st->cur_x = X;
-    uint32_t h = HALT_NONE;
-    if (st->live <= 0) h = HALT_DONE;
-    else if (st->hot_len > T.hot_cap || st->top_count == 0) h = HALT_SELECT;
-    else if (st->top_count > rec_cap) h = HALT_RECORDS;
-    else if (st->tie_count > 1) {
-        if (dev_zig_final_capacity((uint64_t)st->live, st->lastpair_count >= 2) != home_cap) h = HALT_HOME;
-        st->tie_on = 1;
-        st->tie_len = 0;
-    } else {
-        st->tie_on = 0;
-        const uint32_t key = st->top_key;
-        if ((key & 0xFFFF) == (key >> 16)) h = HALT_SELF;
-        else {
-            st->cur_key = key;
-            log[X - 256] = MergeLog{key, st->top_count, (uint32_t)st->live_tokens, st->tie_count};
-        }
-    }
-    if (h) {
-        st->halt = h;
-        st->halt_at = X;
-    }
-}
 // rebuild the home histogram for a new Zig capacity
 __global__ void __launch_bounds__(256) zbpe_home_build(Tables T, DevState *st) {
     const uint32_t n = min(st->num_ids, T.id_cap);

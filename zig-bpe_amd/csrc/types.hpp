@@ -1,5 +1,6 @@
 // Types and constants shared by the device code (kernels.hpp) and the host engine.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace zbpe {
@@ -89,6 +90,7 @@ struct Tables {
     uint32_t *dirty_list;  // stale block indices (each listed once)
     uint32_t dirty_cap;
     int32_t *tok_cnt;      // [65536] live occurrences per token id (global; picks the scan's key token)
+    uint32_t *sup_pending; // per super-block: listed dirty blocks whose summaries are not yet recomputed
 };
 
 constexpr int COUNT_BINS = 64 + 26 * 32;  // count histogram for choosing theta: exact < 64, then 32 per octave
@@ -96,13 +98,26 @@ constexpr int SUMM_SLOTS = 4096;          // home-histogram slots per max-plus b
 constexpr int SUPER_BLOCKS = 64;          // block summaries per super-block summary
 struct Summ { int64_t q, m; };            // carry function c -> max(m, c + q) of a run of slots
 
-// Live tokens just outside this rank's shard (multi-GPU): left[0] is the last live token before the
-// shard, left[1] the one before it; right[0..2] the first live tokens after it.
+// Live tokens just outside this rank's shard (multi-GPU): left token 0 is the last live token before
+// the shard, left 1 the one before it; right 0..2 the first live tokens after it. Packed 16 bits per
+// token so that a run-time index is a shift, not an indexed load from a private copy.
 struct Halo {
-    uint16_t left[2];
-    uint16_t right[3];
+    uint64_t right;  // token i in bits [16i, 16i+16)
+    uint32_t left;
     uint8_t nleft, nright;
+    uint16_t pad;
 };
+__host__ __device__ inline Halo halo_empty() { return Halo{0xFFFFFFFFFFFFull, 0xFFFFFFFFu, 0, 0, 0}; }
+__host__ __device__ inline uint32_t halo_left(const Halo &h, int64_t i) { return (uint32_t)(h.left >> (16 * i)) & 0xFFFFu; }
+__host__ __device__ inline uint32_t halo_right(const Halo &h, int64_t i) { return (uint32_t)(h.right >> (16 * i)) & 0xFFFFu; }
+__host__ __device__ inline void halo_push_left(Halo &h, uint32_t t) {
+    h.left = (h.left & ~(0xFFFFu << (16 * h.nleft))) | (t << (16 * h.nleft));
+    h.nleft++;
+}
+__host__ __device__ inline void halo_push_right(Halo &h, uint32_t t) {
+    h.right = (h.right & ~(0xFFFFull << (16 * h.nright))) | ((uint64_t)t << (16 * h.nright));
+    h.nright++;
+}
 // Per-rank boundary record exchanged after every merge (16 B): first 3 / last 2 live tokens and
 // the live-token count of the shard.
 struct Boundary {
