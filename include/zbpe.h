@@ -61,6 +61,8 @@ typedef struct zbpe_stats {
      * every merge on the synchronous path) and their algorithmic bytes: scan_kernel_s covers these */
     uint64_t scan_timed_launches;
     uint64_t scan_timed_alg_bytes;
+    uint64_t list_scans;      /* pair scans that walked a token occurrence list instead of the stream */
+    uint64_t list_builds;     /* occurrence-list rebuilds (after compactions) */
 } zbpe_stats;
 
 /* Create a single-GPU context on HIP device `device`. */
@@ -115,7 +117,10 @@ zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches);
  * "block_skip" (0/1: stream only the 8192-slot blocks that hold the pair's rarer token),
  * "trace" (0/1: record per-merge timings, see zbpe_trace), "merge_batch" (merges enqueued per host
  * sync, 1 = synchronous loop), "merge_timing" (time every N-th merge of a batch with HIP events;
- * 0 = none), "replace_split" (profiling: apply and count update as separate launches). */
+ * 0 = none), "replace_split" (profiling: apply and count update as separate launches), "list_mode"
+ * (0: always stream the token stream; 1: token occurrence lists once counts are small), "list_ratio"
+ * (list scan when list length * ratio < stream slots), "list_start" (build the lists at a compaction
+ * once top count * list_start < live tokens). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* Benchmark diagnostic: time `reps` launches of the pair-scan kernel for pair (a, b), a != b, over

@@ -112,13 +112,19 @@ def test_debug_checks_hot_list_and_compaction(kind, n, vocab, seed):
 
 
 @pytest.mark.parametrize("g", synth_goldens(), ids=lambda g: g["name"])
-@pytest.mark.parametrize("batch,skip", [(1, 1), (3, 0), (256, 1)])
-def test_merge_batch_and_block_skip_agree(g, batch, skip):
+@pytest.mark.parametrize("batch,skip,lists", [(1, 1, 1), (3, 0, 0), (256, 1, 1), (32, 1, 2), (1, 0, 2)])
+def test_merge_batch_and_block_skip_agree(g, batch, skip, lists):
     """The synchronous loop (merge_batch 1), short and long device-resident batches (halting at self
-    pairs, undecided ties and capacity changes), with and without block skipping: same merges."""
+    pairs, undecided ties and capacity changes), with and without block skipping and occurrence
+    lists (2: lists from the first compaction on, every scan that can use one does): same merges."""
     e = zbpe.Engine(0)
     e.set_option("merge_batch", batch)
     e.set_option("block_skip", skip)
+    e.set_option("list_mode", min(lists, 1))
+    if lists == 2:
+        e.set_option("list_start", 0)
+        e.set_option("list_ratio", 1)
+        e.set_option("compact_den", 2)
     m, c, st = e.train(synth_text(g), g["vocab_size"])
     assert m.tolist() == g["merges"]
     assert c.tolist() == g["counts"]

@@ -56,7 +56,7 @@ void Engine::release() {
     f(T.ht); f(T.id_key); f(T.id_cnt);
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.sup_pending);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.sup_pending); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt);
     for (auto &e : bev) if (e) (void)hipEventDestroy(e);
     bev.clear();
     if (h_st) (void)hipHostFree(h_st);
@@ -90,6 +90,11 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&T.tok_cnt, 65536 * sizeof(int32_t)));
     HIP_OK(hipMalloc(&d_log, 65536 * sizeof(MergeLog)));
+    HIP_OK(hipMalloc(&T.lst_off, 65536 * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&T.lst_len, 65536 * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_list_total, 65536 * sizeof(uint32_t)));
+    HIP_OK(hipFuncSetAttribute((const void *)zbpe_list_hist, hipFuncAttributeMaxDynamicSharedMemorySize, PRES_MAX_VP * 4));
+    HIP_OK(hipFuncSetAttribute((const void *)zbpe_list_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, PRES_MAX_VP * 4));
     HIP_OK(hipMalloc(&d_halo, sizeof(Halo)));
     h_log.resize(65536);
     bev.resize(4 * MAX_BATCH);
@@ -179,7 +184,7 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     Tables N{};
     N.hot = T.hot; N.hot_cap = T.hot_cap; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
     N.home_dirty = T.home_dirty; N.dirty_list = T.dirty_list; N.dirty_cap = T.dirty_cap;
-    N.tok_cnt = T.tok_cnt; N.sup_pending = T.sup_pending;
+    N.tok_cnt = T.tok_cnt; N.sup_pending = T.sup_pending; N.lst_off = T.lst_off; N.lst_len = T.lst_len;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
     if (hipMalloc(&N.ht, ht_cap_new * 8) != hipSuccess || hipMalloc(&N.id_key, id_cap_new * 4) != hipSuccess ||
@@ -243,6 +248,48 @@ zbpe_status Engine::compact() {
         if ((int64_t)total != n_live) return fail(ZBPE_INTERNAL, "compaction kept %llu tokens, expected %lld",
                                                   (unsigned long long)total, (long long)n_live);
     }
+    return ZBPE_OK;
+}
+
+// Compaction during training: positions move, so the occurrence lists are rebuilt (once they are
+// on, or once pair counts have become small against the stream), else the arena is emptied.
+zbpe_status Engine::compact_train() {
+    HIP_OK(hipEventRecord(ev[3], stream));
+    CHECK(compact());
+    const bool want = list_mode && pres_vp <= PRES_MAX_VP && (uint64_t)n_slots < 0xF0000000ull &&
+                      (lists_on || list_start == 0 || (uint64_t)h_st->top_count * list_start < (uint64_t)n_live);
+    if (want) {
+        CHECK(build_lists());
+    } else {
+        HIP_OK(hipMemsetAsync(&d_st->arena_top, 0, 4, stream));
+        HIP_OK(hipMemsetAsync(&d_st->lists_valid, 0, 4, stream));
+    }
+    HIP_OK(hipEventRecord(ev[4], stream));
+    HIP_OK(hipEventSynchronize(ev[4]));
+    float ms;
+    HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
+    run.ev_replace += ms * 1e-3;
+    return sync_state();
+}
+
+// occurrence lists of the compacted stream (no holes): counting sort of positions by token
+zbpe_status Engine::build_lists() {
+    const int64_t n = n_slots;
+    const uint32_t nchunks = (uint32_t)std::max<int64_t>(1, (n + LIST_CHUNK - 1) / LIST_CHUNK);
+    CHECK(ensure(&d_list_cnt, list_cnt_cap, (size_t)nchunks * pres_vp, "list chunk histograms"));
+    zbpe_list_hist<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt);
+    LAUNCH_OK();
+    zbpe_list_colscan<<<(pres_vp + 255) / 256, 256, 0, stream>>>(d_list_cnt, nchunks, pres_vp, d_list_total);
+    LAUNCH_OK();
+    const uint32_t max_len = (uint32_t)std::min<uint64_t>(0xFFFFFFFEu, (uint64_t)n / list_ratio);
+    zbpe_list_offsets<<<1, 1024, 0, stream>>>(d_list_total, pres_vp, max_len, T.lst_off, T.lst_len, d_st);
+    LAUNCH_OK();
+    zbpe_list_scatter<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt, T.lst_off,
+                                                                       T.lst_len, d_lists);
+    LAUNCH_OK();
+    lists_on = true;
+    pres_on = false;  // block skipping is not maintained once scans can bypass the stream
+    stats.list_builds++;
     return ZBPE_OK;
 }
 
@@ -572,6 +619,9 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     pres_vp = ((uint32_t)vocab_size + 63) & ~63u;
     pres_on = block_skip && pres_vp <= PRES_MAX_VP;
     CHECK(build_presence());
+    // arena: the occurrence lists (<= live tokens) + the records appended until the next compaction
+    CHECK(ensure(&d_lists, lists_cap, std::min<size_t>(0xFFFFFFF0u, n + n / 2 + (16u << 20)), "occurrence arena"));
+    lists_on = false;
     if (!T.id_key || T.id_cap < (1u << 20)) {
         if (T.id_key) { (void)hipFree(T.ht); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt); T.ht = nullptr; T.id_key = T.id_cnt = nullptr; }
         CHECK(alloc_tables(1u << 20));
@@ -702,17 +752,10 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // headroom for K merges: ids, occurrence records (counts never grow), tie list; compaction
     CHECK(maybe_grow_tables(X0, K));
     if (hot_stale) CHECK(rebuild_hot());  // a table rebuild renumbered the ids the tie kernels read
-    if ((uint64_t)(n_slots - n_live) * compact_den > (uint64_t)n_slots) {
-        HIP_OK(hipEventRecord(ev[0], stream));
-        CHECK(compact());
-        HIP_OK(hipEventRecord(ev[1], stream));
-        HIP_OK(hipEventSynchronize(ev[1]));
-        float ms;
-        HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
-        run.ev_replace += ms * 1e-3;
-    }
     const uint32_t top0 = h_st->top_count;
-    CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(top0, 1), "occurrence records"));
+    if ((uint64_t)(n_slots - n_live) * compact_den > (uint64_t)n_slots ||
+        (uint64_t)h_st->arena_top + (uint64_t)K * top0 > lists_cap)
+        CHECK(compact_train());
     CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
     if (world > 1) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
     const uint64_t C = home_slots;
@@ -728,7 +771,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
         // merge start (halt checks, tie_on) fused into the tie collection
         zbpe_tie_collect<<<64, 256, 0, stream>>>(T, d_st, 0, (uint32_t)(C ? C - 1 : 0), d_tie_list, (uint32_t)tie_list_cap, 1,
-                                                 BeginArgs{X, C, (uint32_t)rec_cap, d_log});
+                                                 BeginArgs{X, C, (uint32_t)lists_cap, d_log});
         LAUNCH_OK();
         if (C) {
             zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)C, 0, d_summ, d_sup, 1);
@@ -737,13 +780,14 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             LAUNCH_OK();
         }
         if (timed) HIP_OK(hipEventRecord(bev[4 * i + 1], stream));
-        ScanArgs A{d_tok[cur], slots, 0, 0, left, right, d_st, d_rec, (uint32_t)rec_cap, 1, tail, tail + 1, halo,
-                   pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 1, world > 1 ? d_halo : nullptr};
+        ScanArgs A{d_tok[cur], slots, 0, 0, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
+                   pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 1, world > 1 ? d_halo : nullptr,
+                   lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log};
         CHECK(launch_scan(A, top0));
         if (timed) HIP_OK(hipEventRecord(bev[4 * i + 2], stream));
         CHECK(comm_sum(d_delta, 2ull * X + 2));
-        ReplaceArgs R{d_tok[cur], slots, d_rec, (uint32_t)rec_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
-                      1, world > 1 ? d_halo : nullptr};
+        ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
+                      1, world > 1 ? d_halo : nullptr, 1};
         if (!replace_split) {
             zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
         } else {  // profiling: apply and count update as two launches
@@ -791,14 +835,17 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         stats.count_pairs_calls++;
         stats.replace_pair_calls++;
         if (L.ties > 1) stats.tie_iterations++;
+        if (L.mode) stats.list_scans++;
         float ms_sel = 0, ms_scan = 0, ms_rep = 0;
         if (merge_timing && X % merge_timing == 0) {
             HIP_OK(hipEventElapsedTime(&ms_sel, bev[4 * i], bev[4 * i + 1]));
             HIP_OK(hipEventElapsedTime(&ms_scan, bev[4 * i + 1], bev[4 * i + 2]));
             HIP_OK(hipEventElapsedTime(&ms_rep, bev[4 * i + 2], bev[4 * i + 3]));
-            stats.scan_kernel_s += ms_scan * 1e-3;
-            stats.scan_timed_launches++;
-            stats.scan_timed_alg_bytes += 2ull * L.live;
+            if (!L.mode) {  // the roofline covers stream scans (a list scan reads no stream)
+                stats.scan_kernel_s += ms_scan * 1e-3;
+                stats.scan_timed_launches++;
+                stats.scan_timed_alg_bytes += 2ull * L.live;
+            }
             // stage totals are extrapolated from the sampled merges
             run.ev_count += merge_timing * ms_scan * 1e-3;
             run.ev_select += merge_timing * ms_sel * 1e-3;
@@ -839,22 +886,16 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     stats.sum_tokens += (uint64_t)n_live;
 
     CHECK(maybe_grow_tables(X, 1));
-    CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(top, 1), "occurrence records"));
     const bool self = a == b;
-    if (self && n_slots != n_live) {
-        HIP_OK(hipEventRecord(ev[3], stream));
-        CHECK(compact());
-        HIP_OK(hipEventRecord(ev[4], stream));
-        HIP_OK(hipEventSynchronize(ev[4]));
-        float ms;
-        HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
-        run.ev_replace += ms * 1e-3;
-    }
+    // self pairs need a stream without holes; records need room in the arena
+    if ((self && n_slots != n_live) || (uint64_t)h_st->arena_top + top > lists_cap) CHECK(compact_train());
+    if ((uint64_t)h_st->arena_top + top > lists_cap) return fail(ZBPE_OUT_OF_MEMORY, "occurrence arena full");
     // delta layout for this merge: left[0, X) | right[X, 2X) | xx | occurrences
     uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
     // ---- count: scan the stream for (a, b) -----------------------------------------------------
-    ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_rec, (uint32_t)rec_cap, 1, tail, tail + 1, halo,
-               pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt};
+    ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
+               pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 0, nullptr, lists_on ? d_lists : nullptr, T.lst_off,
+               T.lst_len, list_ratio, 1, nullptr};
     HIP_OK(hipEventRecord(ev[0], stream));
     if (!self) {
         CHECK(launch_scan(A, top));
@@ -884,8 +925,8 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     // ---- replace: apply + count update ---------------------------------------------------------
     {
         const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top / 256 + 1);
-        ReplaceArgs R{d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, left, right, tail, a, b, X, key, ab, halo,
-                      (self && world > 1) ? d_x0 : nullptr};
+        ReplaceArgs R{d_tok[cur], n_slots, d_lists, (uint32_t)lists_cap, left, right, tail, a, b, X, key, ab, halo,
+                      (self && world > 1) ? d_x0 : nullptr, 0, nullptr, 1};
         zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
         LAUNCH_OK();
     }
@@ -907,10 +948,14 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         float ms_r, ms_s;
         HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1])); run.ev_count += ms * 1e-3;
         if (!self) {
-            stats.scan_kernel_s += ms * 1e-3;
             stats.scan_alg_bytes += 2ull * (uint64_t)n_live;
-            stats.scan_timed_launches++;
-            stats.scan_timed_alg_bytes += 2ull * (uint64_t)n_live;
+            if (h_st->scan_mode) {
+                stats.list_scans++;
+            } else {
+                stats.scan_kernel_s += ms * 1e-3;
+                stats.scan_timed_launches++;
+                stats.scan_timed_alg_bytes += 2ull * (uint64_t)n_live;
+            }
         }
         HIP_OK(hipEventElapsedTime(&ms_r, ev[1], ev[2])); run.ev_replace += ms_r * 1e-3;
         HIP_OK(hipEventElapsedTime(&ms_s, ev[2], ev[3])); run.ev_select += ms_s * 1e-3;
@@ -938,15 +983,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     const uint64_t gone = h_st->last_holes;  // slots of this shard that became holes
     n_live -= gone;
     (void)gone;
-    if ((uint64_t)(n_slots - n_live) * compact_den > (uint64_t)n_slots) {
-        HIP_OK(hipEventRecord(ev[0], stream));
-        CHECK(compact());
-        HIP_OK(hipEventRecord(ev[1], stream));
-        HIP_OK(hipEventSynchronize(ev[1]));
-        float ms;
-        HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
-        run.ev_replace += ms * 1e-3;
-    }
+    if ((uint64_t)(n_slots - n_live) * compact_den > (uint64_t)n_slots) CHECK(compact_train());
     return ZBPE_OK;
 }
 

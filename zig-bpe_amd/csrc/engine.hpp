@@ -85,6 +85,15 @@ struct Engine {
     uint32_t pres_vp = 0, pres_groups = 0;
     bool pres_on = false, block_skip = true;
     uint64_t stats_pres_builds = 0;
+    // token occurrence lists + this merge's records, in one arena (see kernels.hpp list kernels)
+    uint32_t *d_lists = nullptr;
+    size_t lists_cap = 0;
+    uint32_t *d_list_cnt = nullptr, *d_list_total = nullptr;
+    size_t list_cnt_cap = 0;
+    bool lists_on = false;
+    int list_mode = 1;          // 0: never build lists, 1: once pair counts are small against the stream
+    uint32_t list_ratio = 32;   // list scan when list length * ratio < stream slots
+    uint64_t list_start = 64;   // build lists at a compaction once top count * list_start < live tokens (0: always)
     // per-merge trace (option "trace"), ZBPE_TRACE_COLS floats per merge
     bool trace_on = false;
     std::vector<float> trace;
@@ -143,6 +152,8 @@ struct Engine {
     zbpe_status alloc_stream(size_t n);
     zbpe_status build_presence();
     zbpe_status compact();
+    zbpe_status compact_train();
+    zbpe_status build_lists();
     zbpe_status launch_argmax(uint32_t X, int roll);
     int scan_grid(int64_t slots) const;
     zbpe_status launch_scan(const ScanArgs &A, uint64_t expected_occ);

@@ -328,16 +328,36 @@ struct ScanArgs {
     const int32_t *tokcnt;  // token counts: the rarer of a, b keys the scan (nullptr: a)
     int dyn;                // batch mode: a, b from st->cur_key, halo from *dhalo (if set); no-op when halted
     const Halo *dhalo;
+    // token occurrence lists (Engine::build_lists): positions of token t at lst_off[t] .. + lst_len[t]
+    // in the arena (NO_LIST: none); a scan keyed by the shorter list when it is short enough
+    const uint32_t *lists;
+    const uint32_t *lst_off, *lst_len;
+    uint32_t list_ratio;    // list scan when list length * list_ratio < stream slots
+    int rec_arena;          // records at rec + st->arena_top (they become the new token's list)
+    MergeLog *log;          // batch mode: the scan records its mode in log[X - 256]
 };
-// batch mode: resolve the device-held parts of the arguments (false: the batch is halted)
-__device__ inline bool scan_args_resolve(ScanArgs &A) {
-    if (!A.dyn) return true;
-    if (A.st->halt) return false;
-    const uint32_t k = A.st->cur_key;
-    A.a = k & 0xFFFF;
-    A.b = k >> 16;
-    if (A.dhalo) A.halo = *A.dhalo;
-    return true;
+constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
+// the device-held parts of the arguments: pair (batch mode), halo (batch mode, multi-GPU), record
+// window in the arena
+__device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
+    uint32_t a = A0.a, b = A0.b;
+    Halo h = A0.halo;
+    if (A0.dyn) {
+        const uint32_t k = A0.st->cur_key;
+        a = k & 0xFFFF;
+        b = k >> 16;
+        if (A0.dhalo) h = *A0.dhalo;
+    }
+    uint32_t *rec = A0.rec;
+    uint32_t cap = A0.rec_cap;
+    if (A0.rec_arena) {
+        const uint32_t top = A0.st->arena_top;
+        rec += top;
+        cap = cap > top ? cap - top : 0;
+    }
+    return ScanArgs{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
+                    A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
+                    A0.log};
 }
 
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
@@ -506,16 +526,100 @@ __device__ inline void pres_set(const ScanArgs &A, int64_t pos) {
 
 template <int UNROLL, bool NT, bool FILTER, bool PIPE>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A);
+__device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
+                                                                     uint32_t len);
 template <int UNROLL, bool NT, bool FILTER, bool PIPE = true>
 __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
-    if (!A0.dyn) return scan_pairs_body<UNROLL, NT, FILTER, PIPE>(A0);
-    if (A0.st->halt) return;
-    const uint32_t k = A0.st->cur_key;
-    Halo h = A0.halo;
-    if (A0.dhalo) h = *A0.dhalo;
-    const ScanArgs A{A0.tok, A0.n, k & 0xFFFF, k >> 16, A0.left, A0.right, A0.st, A0.rec, A0.rec_cap, A0.count_deltas,
-                     A0.xx_out, A0.occ_out, h, A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr};
+    if (A0.dyn && A0.st->halt) return;
+    const ScanArgs A = scan_args_resolve(A0);
+    // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
+    if (A.lists && A.a != A.b && A.st->lists_valid) {
+        const uint32_t la = A.lst_len[A.a], lb = A.lst_len[A.b];
+        const bool by_b = lb < la;
+        const uint32_t len = by_b ? lb : la;
+        if (len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                A.st->scan_mode = 1;
+                if (A.log) A.log[A.X - 256].mode = 1;
+            }
+            scan_list_body(A, by_b, A.lists + A.lst_off[by_b ? A.b : A.a], len);
+            return;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
     scan_pairs_body<UNROLL, NT, FILTER, PIPE>(A);
+}
+// List scan: every entry of the key token's list is a position that held the key when it was
+// listed; entries overwritten since (merged or turned into holes) fail the token check.
+__device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
+                                                                     uint32_t len) {
+    __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
+    __shared__ uint32_t s_any;
+    for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
+    NeighbourHist H{s_left, s_right, A.left, A.right};
+    const uint16_t *tok = A.tok;
+    const uint32_t key = by_b ? A.b : A.a;
+    uint32_t xx = 0, any = 0;
+    const int lane = threadIdx.x & 63;
+    if (by_b && blockIdx.x == 0 && threadIdx.x == 0 && A.halo.nright > 0 && halo_right(A.halo, 0) == A.b) {
+        // the occurrence leaving the shard: its b is the next shard's, in no list here
+        const int64_t p = prev_live(tok, A.n);
+        if (p >= 0 && tok[p] == A.a && occ_slow(A, H, p, xx)) {
+            const uint32_t j = atomicAdd(&A.st->rec_count, 1u);
+            atomicAdd(A.occ_out, 1u);
+            if (j < A.rec_cap) A.rec[j] = (uint32_t)p;
+            else atomicOr(&A.st->error, 8u);
+            any = 1;
+        }
+    }
+    const uint32_t stride = gridDim.x * SCAN_THREADS;
+    const uint32_t len64 = (len + 63) & ~63u;  // wave-uniform trip count (wave_append)
+    for (uint32_t i = blockIdx.x * SCAN_THREADS + threadIdx.x; i - lane < len64; i += stride) {
+        bool hit = false;
+        uint32_t pr = 0;
+        if (i < len) {
+            const int64_t p = L[i];
+            if (tok[p] == key) {
+                if (!by_b) {
+                    hit = occ_slow(A, H, p, xx);
+                    pr = (uint32_t)p;
+                } else {
+                    const int64_t q = prev_live_h(A, p);  // q < 0: the a is the left shard's, which owns it
+                    if (q >= 0 && tok[q] == A.a && occ_slow(A, H, q, xx)) {
+                        hit = true;
+                        pr = (uint32_t)q;
+                    }
+                }
+            }
+        }
+        const uint64_t m = __ballot(hit);
+        if (!m) continue;
+        any = 1;
+        uint32_t base = 0;
+        if (lane == 0) {
+            base = atomicAdd(&A.st->rec_count, (uint32_t)__popcll(m));
+            atomicAdd(A.occ_out, (uint32_t)__popcll(m));
+        }
+        base = (uint32_t)__shfl((int)base, 0);
+        if (hit) {
+            const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (j < A.rec_cap) A.rec[j] = pr;
+            else atomicOr(&A.st->error, 8u);
+        }
+    }
+    xx = wave_sum(xx);
+    if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
+    if (lane == 0 && any) s_any = 1;
+    __syncthreads();
+    if (s_any) {
+        for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) {
+            uint32_t l = s_left[i], r = s_right[i];
+            if (l) atomicAdd(&A.left[i], l);
+            if (r) atomicAdd(&A.right[i], r);
+        }
+    }
 }
 template <int UNROLL, bool NT, bool FILTER, bool PIPE>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A) {
@@ -740,6 +844,97 @@ __global__ void __launch_bounds__(PRES_THREADS) zbpe_pres_build(const uint16_t *
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Token occurrence lists (counting sort of the compacted stream by token): per chunk histograms,
+// per-token exclusive scan over chunks, offsets over tokens (tokens too frequent to ever key a
+// list scan get none), scatter of positions. Rebuilt after every compaction while lists are on.
+// ------------------------------------------------------------------------------------------
+constexpr int LIST_CHUNK = 1 << 20;
+constexpr int LIST_THREADS = 1024;
+__global__ void __launch_bounds__(LIST_THREADS) zbpe_list_hist(const uint16_t *__restrict__ tok, int64_t n, uint32_t vp,
+                                                               uint32_t *__restrict__ cnt) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];
+    for (uint32_t i = threadIdx.x; i < vp; i += LIST_THREADS) h[i] = 0;
+    __syncthreads();
+    const int64_t beg = (int64_t)blockIdx.x * LIST_CHUNK, end = min(n, beg + (int64_t)LIST_CHUNK);
+    for (int64_t p = beg + 8 * threadIdx.x; p < end; p += 8 * LIST_THREADS) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(tok + p);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t t = tok_at(v, k);
+            if (t < vp && p + k < end) atomicAdd(&h[t], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < vp; t += LIST_THREADS) cnt[(uint64_t)blockIdx.x * vp + t] = h[t];
+}
+// in place: cnt[c][t] -> sum of cnt[c'][t] for c' < c; total[t] = column sum
+__global__ void __launch_bounds__(256) zbpe_list_colscan(uint32_t *__restrict__ cnt, uint32_t nchunks, uint32_t vp,
+                                                         uint32_t *__restrict__ total) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= vp) return;
+    uint32_t run = 0;
+#pragma unroll 8
+    for (uint32_t c = 0; c < nchunks; c++) {
+        const uint32_t v = cnt[(uint64_t)c * vp + t];
+        cnt[(uint64_t)c * vp + t] = run;
+        run += v;
+    }
+    total[t] = run;
+}
+// one block: list offsets over tokens; tokens with total > max_len get NO_LIST
+__global__ void __launch_bounds__(1024) zbpe_list_offsets(const uint32_t *__restrict__ total, uint32_t vp, uint32_t max_len,
+                                                          uint32_t *__restrict__ lst_off, uint32_t *__restrict__ lst_len,
+                                                          DevState *st) {
+    __shared__ uint32_t s_part[1024];
+    const uint32_t per = (vp + 1023) / 1024, t0 = threadIdx.x * per, t1 = min(vp, t0 + per);
+    uint32_t sum = 0;
+    for (uint32_t t = t0; t < t1; t++) sum += total[t] <= max_len ? total[t] : 0;
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
+        const uint32_t v = threadIdx.x >= (uint32_t)off ? s_part[threadIdx.x - off] : 0;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = s_part[threadIdx.x] - sum;
+    for (uint32_t t = t0; t < t1; t++) {
+        const uint32_t c = total[t];
+        if (c <= max_len) {
+            lst_off[t] = run;
+            lst_len[t] = c;
+            run += c;
+        } else {
+            lst_off[t] = 0;
+            lst_len[t] = NO_LIST;
+        }
+    }
+    if (threadIdx.x == 1023) {
+        st->arena_top = s_part[1023];
+        st->lists_valid = 1;
+    }
+}
+__global__ void __launch_bounds__(LIST_THREADS) zbpe_list_scatter(const uint16_t *__restrict__ tok, int64_t n, uint32_t vp,
+                                                                  const uint32_t *__restrict__ colpre,
+                                                                  const uint32_t *__restrict__ lst_off,
+                                                                  const uint32_t *__restrict__ lst_len,
+                                                                  uint32_t *__restrict__ lists) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
+    for (uint32_t t = threadIdx.x; t < vp; t += LIST_THREADS)
+        cur[t] = lst_len[t] == NO_LIST ? NO_LIST : lst_off[t] + colpre[(uint64_t)blockIdx.x * vp + t];
+    __syncthreads();
+    const int64_t beg = (int64_t)blockIdx.x * LIST_CHUNK, end = min(n, beg + (int64_t)LIST_CHUNK);
+    for (int64_t p = beg + 8 * threadIdx.x; p < end; p += 8 * LIST_THREADS) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(tok + p);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t t = tok_at(v, k);
+            if (t < vp && p + k < end && cur[t] != NO_LIST) lists[atomicAdd(&cur[t], 1u)] = (uint32_t)(p + k);
+        }
+    }
+}
+
 // default variant and the alternatives selectable for A/B runs (option "scan_variant")
 #define zbpe_scan_pairs zbpe_scan_pairs_t<SCAN_UNROLL, true, true>
 
@@ -897,6 +1092,7 @@ struct ReplaceArgs {
     const uint8_t *x0;  // self pairs: parity of the run of a's entering the shard (nullptr: none)
     int dyn;            // batch mode (see ScanArgs::dyn)
     const Halo *dhalo;
+    int rec_arena;      // records at rec + st->arena_top (ScanArgs::rec_arena)
 };
 __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, DevState *st) {
     if (R.dyn) {
@@ -906,6 +1102,11 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
         R.b = R.top_key >> 16;
     }
     if (blockIdx.x < R.apply_blocks) {
+        if (R.rec_arena) {
+            const uint32_t top = st->arena_top;
+            R.rec += top;
+            R.rec_cap = R.rec_cap > top ? R.rec_cap - top : 0;
+        }
         const uint32_t cnt = min(st->rec_count, R.rec_cap);
         uint32_t made = 0;  // an occurrence whose b lies in the next shard makes no hole here
         for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += R.apply_blocks * 256) {
@@ -1060,7 +1261,8 @@ __global__ void zbpe_self_x0(const uint32_t *__restrict__ fns, int rank, uint8_t
     }
     *x0 = x;
 }
-__global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A, const uint8_t *__restrict__ carry_in) {
+__global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, const uint8_t *__restrict__ carry_in) {
+    const ScanArgs A = scan_args_resolve(A0);
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
     __shared__ uint32_t s_rec[SELF_TILE / 2];
     __shared__ int32_t s_last[SELF_THREADS];
@@ -1326,6 +1528,11 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
             st->last_holes = st->holes_made;
             st->live_tokens -= st->holes_made;
             st->tie_len = 0;
+            if (T.lst_off) {  // this merge's records (positions of X) are X's occurrence list
+                T.lst_off[X] = st->arena_top;
+                T.lst_len[X] = st->rec_count;
+                st->arena_top += st->rec_count;
+            }
             st->holes_made = 0;
             st->rec_count = 0;
             tail[0] = tail[1] = 0;
@@ -1365,14 +1572,14 @@ __device__ inline uint64_t dev_zig_final_capacity(uint64_t D, bool call_after) {
 struct BeginArgs {
     uint32_t X;
     uint64_t home_cap;  // Zig capacity the home histogram is kept for
-    uint32_t rec_cap;
+    uint32_t rec_cap;   // arena entries (records go at st->arena_top)
     MergeLog *log;
 };
 __device__ inline uint32_t merge_begin_eval(const Tables &T, const DevState *st, const BeginArgs &B, bool *tie) {
     *tie = false;
     if (st->live <= 0) return HALT_DONE;
     if (st->hot_len > T.hot_cap || st->top_count == 0) return HALT_SELECT;
-    if (st->top_count > B.rec_cap) return HALT_RECORDS;
+    if ((uint64_t)st->arena_top + st->top_count > B.rec_cap) return HALT_RECORDS;
     if (st->tie_count > 1) {
         if (dev_zig_final_capacity((uint64_t)st->live, st->lastpair_count >= 2) != B.home_cap) return HALT_HOME;
         *tie = true;

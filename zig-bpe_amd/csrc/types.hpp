@@ -58,8 +58,10 @@ struct DevState {
     uint32_t cur_x;          // merge token X being processed
     uint32_t cur_key;        // the pair this merge replaces (after the tie-break)
     uint32_t tie_on;         // 1: this merge's top count is tied (the tie kernels run)
-    uint32_t pad4;
+    uint32_t lists_valid;    // 1: token occurrence lists describe the current stream
     long long live_tokens;   // live tokens of this shard (rolled by zbpe_select)
+    uint32_t arena_top;      // arena entries in use (lists, then this merge's records)
+    uint32_t scan_mode;      // last pair scan: 0 streamed the token stream, 1 walked an occurrence list
 };
 // why a device-resident batch stopped (the host finishes that merge on the synchronous path)
 enum HaltReason : uint32_t {
@@ -74,6 +76,8 @@ enum HaltReason : uint32_t {
 // per-merge log written by the device in batch mode
 struct MergeLog {
     uint32_t key, count, live, ties;
+    uint32_t mode;     // 0: stream scan, 1: list scan
+    uint32_t pad[3];
 };
 
 struct Tables {
@@ -91,6 +95,7 @@ struct Tables {
     uint32_t dirty_cap;
     int32_t *tok_cnt;      // [65536] live occurrences per token id (global; picks the scan's key token)
     uint32_t *sup_pending; // per super-block: listed dirty blocks whose summaries are not yet recomputed
+    uint32_t *lst_off, *lst_len;  // [65536] token occurrence lists in the arena (nullptr: not kept)
 };
 
 constexpr int COUNT_BINS = 64 + 26 * 32;  // count histogram for choosing theta: exact < 64, then 32 per octave

@@ -129,6 +129,8 @@ class Stats(ctypes.Structure):
         ("sum_tokens", ctypes.c_uint64),
         ("scan_timed_launches", ctypes.c_uint64),
         ("scan_timed_alg_bytes", ctypes.c_uint64),
+        ("list_scans", ctypes.c_uint64),
+        ("list_builds", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
