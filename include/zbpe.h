@@ -120,7 +120,8 @@ zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches);
  * 0 = none), "replace_split" (profiling: apply and count update as separate launches), "list_mode"
  * (0: always stream the token stream; 1: token occurrence lists once counts are small), "list_ratio"
  * (list scan when list length * ratio < stream slots), "list_start" (build the lists at a compaction
- * once top count * list_start < live tokens). */
+ * once top count * list_start < live tokens; 0: at the first compaction), "compact_den_lists" (compact_den
+ * once lists are on). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* Benchmark diagnostic: time `reps` launches of the pair-scan kernel for pair (a, b), a != b, over

@@ -125,6 +125,7 @@ def test_merge_batch_and_block_skip_agree(g, batch, skip, lists):
         e.set_option("list_start", 0)
         e.set_option("list_ratio", 1)
         e.set_option("compact_den", 2)
+        e.set_option("compact_den_lists", 4)
     m, c, st = e.train(synth_text(g), g["vocab_size"])
     assert m.tolist() == g["merges"]
     assert c.tolist() == g["counts"]
@@ -139,6 +140,7 @@ def test_compaction_policies_agree(engine):
     for den in (1, 2, 64, 1 << 40):
         e = zbpe.Engine(0)
         e.set_option("compact_den", den)
+        e.set_option("compact_den_lists", den)
         m, c, st = e.train(text, 700)
         assert m.tolist() == r.merges.tolist(), den
         assert e.verify_counts() == 0

@@ -56,7 +56,7 @@ void Engine::release() {
     f(T.ht); f(T.id_key); f(T.id_cnt);
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(T.dirty_list); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.sup_pending); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt);
     for (auto &e : bev) if (e) (void)hipEventDestroy(e);
     bev.clear();
     if (h_st) (void)hipHostFree(h_st);
@@ -72,7 +72,7 @@ void Engine::release() {
     d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr;
     d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
     d_summ = nullptr; d_count_hist = nullptr; h_count_hist = nullptr; hot_cap_alloc = home_words_cap = 0; home_slots = 0;
-    dirty_list_cap = dirty_bits_cap = 0; d_sup = nullptr; sup_cap = 0; d_pres = nullptr; pres_cap = 0;
+    dirty_bits_cap = 0; d_sup = nullptr; sup_cap = 0; d_pres = nullptr; pres_cap = 0;
     for (auto &e : ev) e = nullptr;
 }
 
@@ -98,7 +98,7 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipMalloc(&d_halo, sizeof(Halo)));
     h_log.resize(65536);
     bev.resize(4 * MAX_BATCH);
-    for (auto &e : bev) HIP_OK(hipEventCreate(&e));
+    for (auto &e : bev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no L2 writeback
     HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
     HIP_OK(hipMalloc(&d_count_hist, COUNT_BINS * sizeof(uint32_t)));
     HIP_OK(hipHostMalloc((void **)&h_count_hist, COUNT_BINS * sizeof(uint32_t), hipHostMallocDefault));
@@ -183,8 +183,8 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     while (ht_cap_new < 2 * id_cap_new) ht_cap_new <<= 1;
     Tables N{};
     N.hot = T.hot; N.hot_cap = T.hot_cap; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
-    N.home_dirty = T.home_dirty; N.dirty_list = T.dirty_list; N.dirty_cap = T.dirty_cap;
-    N.tok_cnt = T.tok_cnt; N.sup_pending = T.sup_pending; N.lst_off = T.lst_off; N.lst_len = T.lst_len;
+    N.home_dirty = T.home_dirty;
+    N.tok_cnt = T.tok_cnt; N.lst_off = T.lst_off; N.lst_len = T.lst_len;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
     if (hipMalloc(&N.ht, ht_cap_new * 8) != hipSuccess || hipMalloc(&N.id_key, id_cap_new * 4) != hipSuccess ||
@@ -338,11 +338,15 @@ zbpe_status Engine::rebuild_hot() {
     return ZBPE_OK;
 }
 
+int Engine::argmax_blocks(uint32_t X) const {
+    const uint64_t work = std::max<uint64_t>(T.hot_cap / 4, X);
+    const int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, (work + ARGMAX_THREADS - 1) / ARGMAX_THREADS);
+    return std::max(blocks, 1);
+}
+
 zbpe_status Engine::launch_argmax(uint32_t X, int roll) {
     if (hot_stale) CHECK(rebuild_hot());
-    const uint64_t work = std::max<uint64_t>(T.hot_cap / 4, X);
-    int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, (work + ARGMAX_THREADS - 1) / ARGMAX_THREADS);
-    blocks = std::max(blocks, 1);
+    const int blocks = argmax_blocks(X);
     zbpe_select<<<blocks, ARGMAX_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], n_slots, d_delta, X, roll, d_bnd_all,
                                                        world);
     LAUNCH_OK();
@@ -396,26 +400,20 @@ zbpe_status Engine::rebuild_home(uint64_t cap) {
         }
         home_words_cap = words;
     }
-    const size_t nb = (cap + SUMM_SLOTS - 1) / SUMM_SLOTS;
+    const size_t nb = (cap + SUMM_SLOTS - 1) / SUMM_SLOTS, nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
     CHECK(ensure(&d_summ, summ_cap, nb, "home summaries"));
-    CHECK(ensure(&d_sup, sup_cap, nb / SUPER_BLOCKS + 1, "home super-block summaries"));
-    CHECK(ensure(&T.dirty_list, dirty_list_cap, nb, "home dirty list"));
-    CHECK(ensure(&T.home_dirty, dirty_bits_cap, nb / 32 + 1, "home dirty bits"));
-    CHECK(ensure(&T.sup_pending, sup_pending_cap, nb / SUPER_BLOCKS + 1, "home super-block pending counts"));
-    T.dirty_cap = (uint32_t)dirty_list_cap;
+    CHECK(ensure(&d_sup, sup_cap, nsb, "home super-block summaries"));
+    CHECK(ensure(&T.home_dirty, dirty_bits_cap, 2 * nsb, "home dirty bits"));
     HIP_OK(hipMemsetAsync(T.home_cnt, 0, words * 4, stream));
-    HIP_OK(hipMemsetAsync(T.home_dirty, 0, (nb / 32 + 1) * 4, stream));
-    HIP_OK(hipMemsetAsync(&d_st->dirty_len, 0, 4, stream));  // entries of the previous capacity are void
+    HIP_OK(hipMemsetAsync(T.home_dirty, 0, 2 * nsb * 4, stream));
     T.home_mask = (uint32_t)(cap - 1);
     const uint32_t nid = h_st->num_ids;
     zbpe_home_build<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_st);
     LAUNCH_OK();
-    HIP_OK(hipMemsetAsync(T.home_dirty, 0, (nb / 32 + 1) * 4, stream));
-    HIP_OK(hipMemsetAsync(&d_st->dirty_len, 0, 4, stream));
-    HIP_OK(hipMemsetAsync(T.sup_pending, 0, (nb / SUPER_BLOCKS + 1) * 4, stream));
-    zbpe_home_summary<<<(unsigned)std::min<size_t>(nb, 4096), 256, 0, stream>>>(T, d_st, (uint32_t)cap, (uint32_t)nb, d_summ, d_sup, 0);
+    HIP_OK(hipMemsetAsync(T.home_dirty, 0, 2 * nsb * 4, stream));
+    zbpe_home_summary<<<(unsigned)std::min<size_t>(nb, 4096), 256, 0, stream>>>(T, d_st, (uint32_t)cap, (uint32_t)nb, d_summ);
     LAUNCH_OK();
-    zbpe_super_summary<<<(unsigned)((nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS + 3) / 4, 256, 0, stream>>>(d_summ, (uint32_t)nb, d_sup, d_st, 0);
+    zbpe_super_summary<<<(unsigned)(nsb + 3) / 4, 256, 0, stream>>>(d_summ, (uint32_t)nb, d_sup, d_st, 0);
     LAUNCH_OK();
     home_slots = cap;
     home_rebuilds++;
@@ -436,9 +434,9 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     zbpe_tie_collect<<<std::min<uint32_t>(1024, hl / 256 + 1), 256, 0, stream>>>(T, d_st, top, (uint32_t)(cap - 1), d_tie_list,
                                                                                   (uint32_t)tie_list_cap, 0, BeginArgs{});
     LAUNCH_OK();
-    zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)cap, 0, d_summ, d_sup, 0);
-    LAUNCH_OK();
     const uint32_t nb = (uint32_t)((cap + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
+    zbpe_home_refresh<<<nsb, REFRESH_THREADS, 0, stream>>>(T, d_st, (uint32_t)cap, nb, d_summ, d_sup, 0);
+    LAUNCH_OK();
     HomeView V{T.home_cnt, d_summ, d_sup, (uint32_t)cap, nb, nsb};
     zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 0);
     LAUNCH_OK();
@@ -638,8 +636,6 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     T.home_mask = 0;
     if (T.home_cnt) { (void)hipFree(T.home_cnt); T.home_cnt = nullptr; home_words_cap = 0; }
     if (T.home_dirty) { (void)hipFree(T.home_dirty); T.home_dirty = nullptr; dirty_bits_cap = 0; }
-    if (T.sup_pending) { (void)hipFree(T.sup_pending); T.sup_pending = nullptr; sup_pending_cap = 0; }
-    if (T.dirty_list) { (void)hipFree(T.dirty_list); T.dirty_list = nullptr; dirty_list_cap = 0; T.dirty_cap = 0; }
     hot_stale = true;
     halo = halo0;
     HIP_OK(hipMemsetAsync(d_delta, 0, DELTA_WORDS * 4, stream));
@@ -753,7 +749,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     CHECK(maybe_grow_tables(X0, K));
     if (hot_stale) CHECK(rebuild_hot());  // a table rebuild renumbered the ids the tie kernels read
     const uint32_t top0 = h_st->top_count;
-    if ((uint64_t)(n_slots - n_live) * compact_den > (uint64_t)n_slots ||
+    if ((uint64_t)(n_slots - n_live) * (lists_on ? compact_den_lists : compact_den) > (uint64_t)n_slots ||
         (uint64_t)h_st->arena_top + (uint64_t)K * top0 > lists_cap)
         CHECK(compact_train());
     CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
@@ -774,7 +770,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                                                  BeginArgs{X, C, (uint32_t)lists_cap, d_log});
         LAUNCH_OK();
         if (C) {
-            zbpe_home_summary<<<1024, 256, 0, stream>>>(T, d_st, (uint32_t)C, 0, d_summ, d_sup, 1);
+            zbpe_home_refresh<<<nsb, REFRESH_THREADS, 0, stream>>>(T, d_st, (uint32_t)C, nb, d_summ, d_sup, 1);
             LAUNCH_OK();
             zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 1);
             LAUNCH_OK();
@@ -887,8 +883,8 @@ zbpe_status Engine::merge_sync(uint32_t X) {
 
     CHECK(maybe_grow_tables(X, 1));
     const bool self = a == b;
-    // self pairs need a stream without holes; records need room in the arena
-    if ((self && n_slots != n_live) || (uint64_t)h_st->arena_top + top > lists_cap) CHECK(compact_train());
+    // records need room in the arena (self pairs treat holes as transparent: no compaction needed)
+    if ((uint64_t)h_st->arena_top + top > lists_cap) CHECK(compact_train());
     if ((uint64_t)h_st->arena_top + top > lists_cap) return fail(ZBPE_OUT_OF_MEMORY, "occurrence arena full");
     // delta layout for this merge: left[0, X) | right[X, 2X) | xx | occurrences
     uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
@@ -983,7 +979,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     const uint64_t gone = h_st->last_holes;  // slots of this shard that became holes
     n_live -= gone;
     (void)gone;
-    if ((uint64_t)(n_slots - n_live) * compact_den > (uint64_t)n_slots) CHECK(compact_train());
+    if ((uint64_t)(n_slots - n_live) * (lists_on ? compact_den_lists : compact_den) > (uint64_t)n_slots) CHECK(compact_train());
     return ZBPE_OK;
 }
 

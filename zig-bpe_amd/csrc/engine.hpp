@@ -74,7 +74,7 @@ struct Engine {
     size_t recount_cap = 0;
     uint32_t *d_count_hist = nullptr, *h_count_hist = nullptr;
     size_t hot_cap_alloc = 0;
-    size_t home_words_cap = 0, dirty_list_cap = 0, dirty_bits_cap = 0, sup_pending_cap = 0;
+    size_t home_words_cap = 0, dirty_bits_cap = 0;
     uint64_t home_slots = 0;    // Zig capacity the home histogram is kept for (0: none)
     Summ *d_summ = nullptr, *d_sup = nullptr;
     size_t summ_cap = 0, sup_cap = 0;
@@ -92,7 +92,7 @@ struct Engine {
     size_t list_cnt_cap = 0;
     bool lists_on = false;
     int list_mode = 1;          // 0: never build lists, 1: once pair counts are small against the stream
-    uint32_t list_ratio = 32;   // list scan when list length * ratio < stream slots
+    uint32_t list_ratio = 256;  // list scan when list length * ratio < stream slots
     uint64_t list_start = 64;   // build lists at a compaction once top count * list_start < live tokens (0: always)
     // per-merge trace (option "trace"), ZBPE_TRACE_COLS floats per merge
     bool trace_on = false;
@@ -120,6 +120,7 @@ struct Engine {
 
     // policy knobs
     uint64_t compact_den = 8;     // compact when holes > slots / compact_den
+    uint64_t compact_den_lists = 8;  // the same once occurrence lists are on (a compaction also rebuilds them)
     int scan_blocks_per_cu = 8;
     bool debug_checks = false;    // extra syncs + consistency checks
     bool force_exact_ties = false;  // resolve every tie by the exact emulation and cross-check the fast path
@@ -155,6 +156,7 @@ struct Engine {
     zbpe_status compact_train();
     zbpe_status build_lists();
     zbpe_status launch_argmax(uint32_t X, int roll);
+    int argmax_blocks(uint32_t X) const;
     int scan_grid(int64_t slots) const;
     zbpe_status launch_scan(const ScanArgs &A, uint64_t expected_occ);
     zbpe_status rebuild_hot();

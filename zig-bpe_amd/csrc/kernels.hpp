@@ -70,17 +70,14 @@ __device__ inline void ht_insert_new(const Tables &T, uint32_t key, uint32_t id)
 // Live keys per home slot of the Zig map: kept incrementally once a tie
 // has asked for it, so later ties need no pass over every key.
 __device__ inline void home_add(const Tables &T, DevState *st, uint32_t key, bool add) {
+    // fire-and-forget: the count (u8 per slot; > 255 keys on one home slot of a table loaded <= 80 %
+    // has probability ~1e-500) and the block's dirty bit, both non-returning atomics
     if (!T.home_cnt) return;
     const uint32_t s = (uint32_t)(zig_pair_hash(key) & T.home_mask), sh = 8 * (s & 3);
-    const uint32_t old = add ? atomicAdd(&T.home_cnt[s >> 2], 1u << sh) : atomicSub(&T.home_cnt[s >> 2], 1u << sh);
-    if (((old >> sh) & 0xffu) == (add ? 0xffu : 0u)) atomicOr(&st->error, 16u);
-    const uint32_t blk = s / SUMM_SLOTS, bit = 1u << (blk & 31);
-    if (!(atomicOr(&T.home_dirty[blk >> 5], bit) & bit)) {
-        const uint32_t j = atomicAdd(&st->dirty_len, 1u);
-        if (j < T.dirty_cap) T.dirty_list[j] = blk;
-        else atomicOr(&st->error, 32u);
-        if (T.sup_pending) atomicAdd(&T.sup_pending[blk / SUPER_BLOCKS], 1u);
-    }
+    if (add) atomicAdd(&T.home_cnt[s >> 2], 1u << sh);
+    else atomicSub(&T.home_cnt[s >> 2], 1u << sh);
+    const uint32_t blk = s / SUMM_SLOTS;
+    atomicOr(&T.home_dirty[blk >> 5], 1u << (blk & 31));
 }
 // Wave-aggregated append: one atomic per wave. Every lane of the wave must call it.
 __device__ inline uint32_t wave_append(uint32_t *counter, bool flag) {
@@ -964,23 +961,12 @@ __host__ __device__ inline uint32_t update_per(uint32_t X) {
     const uint32_t p = X / (16 * UPD_THREADS);
     return p < 1 ? 1 : (p > UPD_MAX_PER ? UPD_MAX_PER : p);
 }
-// home_add without the dirty-list append: returns the block to append (or ~0u)
-__device__ inline uint32_t home_add_nd(const Tables &T, DevState *st, uint32_t key, bool add) {
-    if (!T.home_cnt) return ~0u;
-    const uint32_t s = (uint32_t)(zig_pair_hash(key) & T.home_mask), sh = 8 * (s & 3);
-    const uint32_t old = add ? atomicAdd(&T.home_cnt[s >> 2], 1u << sh) : atomicSub(&T.home_cnt[s >> 2], 1u << sh);
-    if (((old >> sh) & 0xffu) == (add ? 0xffu : 0u)) atomicOr(&st->error, 16u);
-    const uint32_t blk = s / SUMM_SLOTS, bit = 1u << (blk & 31);
-    if (atomicOr(&T.home_dirty[blk >> 5], bit) & bit) return ~0u;
-    if (T.sup_pending) atomicAdd(&T.sup_pending[blk / SUPER_BLOCKS], 1u);
-    return blk;
-}
 __device__ inline void update_block(const Tables &T, DevState *st, const uint32_t *__restrict__ left,
                                     const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
                                     uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per) {
     __shared__ uint32_t s_t[UPD_THREADS * UPD_MAX_PER], s_c[UPD_THREADS * UPD_MAX_PER];
-    __shared__ uint32_t s_hot[UPD_THREADS * UPD_MAX_PER], s_dirty[UPD_THREADS * UPD_MAX_PER];
-    __shared__ uint32_t s_n, s_nhot, s_ndirty, s_base;
+    __shared__ uint32_t s_hot[UPD_THREADS * UPD_MAX_PER];
+    __shared__ uint32_t s_n, s_nhot, s_base;
     __shared__ int s_live;
     const uint32_t nch = update_chunks(X, per);
     const uint32_t tid = threadIdx.x;
@@ -1010,7 +996,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
     }
     const uint32_t g = ublk / nch, beg = (ublk - g * nch) * UPD_THREADS * per;
     const uint32_t *delta = (g < 2) ? left : right;
-    if (tid == 0) { s_n = 0; s_nhot = 0; s_ndirty = 0; s_live = 0; }
+    if (tid == 0) { s_n = 0; s_nhot = 0; s_live = 0; }
     __syncthreads();
     for (uint32_t k = 0; k < per; k++) {
         const uint32_t t = beg + k * UPD_THREADS + tid;
@@ -1034,7 +1020,6 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
     int live_delta = 0;
     for (uint32_t i = tid; i < n; i += UPD_THREADS) {
         const uint32_t t = s_t[i], c = s_c[i];
-        uint32_t dblk = ~0u;
         if (!create) {
             const uint32_t key = g == 0 ? pair_key(t, a) : pair_key(b, t);
             const uint32_t id = ht_find(T, key);
@@ -1042,7 +1027,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
             else {
                 const uint32_t old = atomicSub(&T.id_cnt[id], c);
                 if (old < c) atomicOr(&st->error, 2u);
-                if (old == c) { live_delta--; dblk = home_add_nd(T, st, key, false); }
+                if (old == c) { live_delta--; home_add(T, st, key, false); }
             }
         } else {
             const uint32_t id = s_base + i;
@@ -1051,29 +1036,21 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
             else {
                 T.id_key[id] = key;
                 T.id_cnt[id] = c;
+                home_add(T, st, key, true);
                 ht_insert_new(T, key, id);
-                dblk = home_add_nd(T, st, key, true);
                 if (c >= theta) s_hot[atomicAdd(&s_nhot, 1u)] = id;
             }
         }
-        if (dblk != ~0u) s_dirty[atomicAdd(&s_ndirty, 1u)] = dblk;
     }
     if (live_delta) atomicAdd(&s_live, live_delta);
     __syncthreads();
     if (tid == 0) {
         if (s_live) atomicAdd(&st->live, s_live);
         s_base = s_nhot ? atomicAdd(&st->hot_len, s_nhot) : 0;
-        const uint32_t nd = s_ndirty;
-        s_n = nd ? atomicAdd(&st->dirty_len, nd) : 0;  // reuse: base of this block's dirty entries
     }
     __syncthreads();
     for (uint32_t i = tid; i < s_nhot; i += UPD_THREADS)
         if (s_base + i < T.hot_cap) T.hot[s_base + i] = s_hot[i];
-    for (uint32_t i = tid; i < s_ndirty; i += UPD_THREADS) {
-        const uint32_t j = s_n + i;
-        if (j < T.dirty_cap) T.dirty_list[j] = s_dirty[i];
-        else atomicOr(&st->error, 32u);
-    }
 }
 
 // replaceTopPairWithNewToken in one launch: blocks [0, apply_blocks) rewrite the stream at the
@@ -1182,35 +1159,45 @@ __global__ void __launch_bounds__(256) zbpe_reset_merge(DevState *st, uint32_t *
 
 // ------------------------------------------------------------------------------------------
 // Self pair (a, a): left-greedy over runs needs each position's offset parity inside its run
-// of a's (basic_tokenizer.zig:217-226 consumes a run of L a's as floor(L/2) merges). The stream
-// is compacted (no holes) before these kernels run. Per tile: all_a flag + trailing-run parity;
-// a scan composes them into the parity of the run entering each tile.
+// of a's (basic_tokenizer.zig:217-226 consumes a run of L a's as floor(L/2) merges). Runs are runs
+// of LIVE tokens: holes are transparent, so the stream needs no compaction first. A segment of the
+// stream acts on the parity x of the run entering it as x -> has_non_a ? p : x ^ p (p = parity of
+// the live a's after its last live non-a); tiles and threads compose these functions in order.
 // ------------------------------------------------------------------------------------------
 constexpr int SELF_THREADS = 256;
 constexpr int SELF_PER_THREAD = 32;
 constexpr int SELF_TILE = SELF_THREADS * SELF_PER_THREAD;  // 8192
 static_assert(SELF_TILE == PRES_BLK, "a self-pair tile is one presence block");
+// run-parity function of SELF_PER_THREAD slots: bit0 = no live non-a (x -> x ^ p), bit1 = p
+__device__ inline uint8_t self_segment(const uint16_t *tok, int64_t p0, int64_t end, uint32_t a) {
+    uint8_t all = 1, par = 0;
+    for (int i = 0; i < SELF_PER_THREAD; i++) {
+        const int64_t p = p0 + i;
+        if (p >= end) break;
+        const uint32_t t = tok[p];
+        if (t == HOLE) continue;
+        if (t != a) { all = 0; par = 0; }
+        else par ^= 1;
+    }
+    return (uint8_t)(all | (par << 1));
+}
+__device__ inline uint8_t self_apply(uint8_t f, uint8_t x) { return (f & 1) ? (uint8_t)(x ^ ((f >> 1) & 1)) : (uint8_t)((f >> 1) & 1); }
 __global__ void __launch_bounds__(SELF_THREADS) zbpe_self_tiles(const uint16_t *__restrict__ tok, int64_t n, uint32_t a,
                                                                 uint8_t *__restrict__ tile_fn) {
-    // tile_fn bit0: tile is all a; bit1: parity of the trailing a-run (if not all a)
+    // tile_fn bit0: the tile holds no live non-a; bit1: parity of its trailing live a-run
     const int64_t beg = blockIdx.x * (int64_t)SELF_TILE;
     const int64_t end = min(n, beg + SELF_TILE);
-    __shared__ int32_t s_last[SELF_THREADS];
-    int32_t last = -1;  // last index (tile-relative) holding a non-a
-    for (int i = 0; i < SELF_PER_THREAD; i++) {
-        int64_t p = beg + threadIdx.x * SELF_PER_THREAD + i;
-        if (p < end && tok[p] != a) last = threadIdx.x * SELF_PER_THREAD + i;
-    }
-    s_last[threadIdx.x] = last;
+    __shared__ uint8_t s_fn[SELF_THREADS];
+    s_fn[threadIdx.x] = self_segment(tok, beg + threadIdx.x * SELF_PER_THREAD, end, a);
     __syncthreads();
     if (threadIdx.x == 0) {
-        int32_t L = -1;
-        for (int t = 0; t < SELF_THREADS; t++) L = max(L, s_last[t]);
-        int64_t len = end - beg;
-        uint8_t f;
-        if (L < 0) f = 1 | (uint8_t)((len & 1) << 1);  // all a: carry parity += len
-        else f = (uint8_t)(((len - 1 - L) & 1) << 1);
-        tile_fn[blockIdx.x] = f;
+        uint8_t all = 1, par = 0;  // identity
+        for (int t = 0; t < SELF_THREADS; t++) {
+            const uint8_t f = s_fn[t];
+            if (f & 1) par ^= (f >> 1) & 1;
+            else { all = 0; par = (f >> 1) & 1; }
+        }
+        tile_fn[blockIdx.x] = (uint8_t)(all | (par << 1));
     }
 }
 // carry_in[t] = parity of the a-run entering tile t. One block; each thread composes a segment.
@@ -1265,58 +1252,54 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
     const ScanArgs A = scan_args_resolve(A0);
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
     __shared__ uint32_t s_rec[SELF_TILE / 2];
-    __shared__ int32_t s_last[SELF_THREADS];
+    __shared__ uint8_t s_fn[SELF_THREADS];
     __shared__ uint32_t s_nrec, s_base;
     for (int i = threadIdx.x; i < LDS_BINS; i += SELF_THREADS) { s_left[i] = 0; s_right[i] = 0; }
     if (threadIdx.x == 0) s_nrec = 0;
-    __syncthreads();
     NeighbourHist H{s_left, s_right, A.left, A.right};
     const uint16_t *tok = A.tok;
-    const int64_t n = A.n;
     const uint32_t a = A.a;
     const int64_t beg = blockIdx.x * (int64_t)SELF_TILE;
-    const int64_t end = min(n, beg + SELF_TILE);
+    const int64_t end = min(A.n, beg + SELF_TILE);
     const int64_t t0 = beg + threadIdx.x * SELF_PER_THREAD;
-    int32_t last = -1;
-    for (int i = 0; i < SELF_PER_THREAD; i++) {
-        int64_t p = t0 + i;
-        if (p < end && tok[p] != a) last = (int32_t)(threadIdx.x * SELF_PER_THREAD + i);
-    }
-    s_last[threadIdx.x] = last;
+    s_fn[threadIdx.x] = self_segment(tok, t0, end, a);
     __syncthreads();
-    // exclusive max over threads before me (sequential: 256 entries, cheap relative to the tile)
-    int32_t prev = -1;
-    for (int t = 0; t < (int)threadIdx.x; t++) prev = max(prev, s_last[t]);
-    const uint32_t carry = carry_in[blockIdx.x] & 1;
+    // parity of the live a-run entering my segment: the tile's carry through the segments before mine
+    uint8_t x = carry_in[blockIdx.x] & 1;
+    for (int t = 0; t < (int)threadIdx.x; t++) x = self_apply(s_fn[t], x);
     uint32_t xx = 0;
-    int32_t lastna = prev;  // tile-relative index of the last non-a before the current position
     for (int i = 0; i < SELF_PER_THREAD; i++) {
         const int64_t p = t0 + i;
         if (p >= end) break;
-        const int32_t rel = (int32_t)(threadIdx.x * SELF_PER_THREAD + i);
-        if (tok[p] != a) { lastna = rel; continue; }
-        uint32_t off_par = lastna >= 0 ? (uint32_t)((rel - lastna - 1) & 1) : ((carry + (uint32_t)rel) & 1);
-        if (off_par) continue;
-        // the shard is compacted: positions past its end continue in the right halo, before it in the left
-        auto at = [&](int64_t q) -> uint32_t {
-            if (q < n) return q >= 0 ? tok[q] : (-q - 1 < A.halo.nleft ? halo_left(A.halo, -q - 1) : HOLE);
-            return q - n < A.halo.nright ? halo_right(A.halo, q - n) : HOLE;
-        };
-        if (at(p + 1) != a) continue;
-        // occurrence at p
+        const uint32_t tp = tok[p];
+        if (tp == HOLE) continue;
+        if (tp != a) { x = 0; continue; }
+        const uint8_t off_par = x;
+        x ^= 1;
+        if (off_par) continue;  // odd offset in its run: the b of an occurrence (or a lone trailing a)
+        const int64_t q = next_live_h(A, p);
+        if (q == NONE_POS || tok_h(A, q) != a) continue;
+        // occurrence (p, q)
         if (A.count_deltas) {
-            // offset 0 in the run: the left neighbour is not the end of a previous occurrence
-            const bool run_start = lastna >= 0 ? (rel - lastna - 1 == 0) : (rel == 0 && at(p - 1) != a);
-            const uint32_t tl = at(p - 1);
-            if (run_start && tl != HOLE) H.left((uint16_t)tl);
-            const uint32_t tr = at(p + 2);
-            if (tr != HOLE) {
-                const bool r_occ = (tr == a) && (at(p + 3) == a);
+            // first a of its run: the left neighbour is not the end of a previous occurrence
+            const int64_t l = prev_live_h(A, p);
+            if (l != NONE_POS) {
+                const uint32_t tl = tok_h(A, l);
+                if (tl != a) H.left((uint16_t)tl);
+            }
+            const int64_t r = next_live_h(A, q);
+            if (r != NONE_POS) {
+                const uint32_t tr = tok_h(A, r);
+                bool r_occ = false;
+                if (tr == a) {
+                    const int64_t r2 = next_live_h(A, r);
+                    r_occ = r2 != NONE_POS && tok_h(A, r2) == a;
+                }
                 if (r_occ) xx++;
                 else H.right((uint16_t)tr);
             }
         }
-        uint32_t slot = atomicAdd(&s_nrec, 1u);
+        const uint32_t slot = atomicAdd(&s_nrec, 1u);
         s_rec[slot] = (uint32_t)p;
     }
     __syncthreads();
@@ -1465,6 +1448,8 @@ __global__ void __launch_bounds__(256) zbpe_hot_build(Tables T, DevState *st) {
 // (agent-scope release/acquire around the ticket, cdna_hip_programming.md Guideline 16), the
 // stream's last-pair count, and the end-of-merge resets (neighbour histograms, counters) when
 // roll != 0. One launch per merge instead of three.
+__device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, const uint16_t *tok, int64_t n,
+                                     uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world);
 __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState *st, MaxRec *__restrict__ partial,
                                                               const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
                                                               uint32_t X, int roll, const Boundary *__restrict__ bnd, int world) {
@@ -1504,6 +1489,14 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < ARGMAX_THREADS / WAVE; w++) q = max_combine(q, sm[w]);
+        select_finish(T, st, q, tok, n, delta, X, roll, bnd, world);
+    }
+}
+// the selection's state update (one thread): top pair, tie count, the stream's last pair (ties),
+// and at roll the end-of-merge bookkeeping (occurrence list of X, counters, deltas' tail)
+__device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, const uint16_t *tok, int64_t n,
+                                     uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world) {
+    {
         st->top_count = q.cnt;
         st->tie_count = q.cnt ? q.ties : 0;
         st->top_id = q.id;
@@ -1629,16 +1622,13 @@ __global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, 
         }
     }
 }
-// block summaries of the home histogram (block b covers slots [b*SUMM_SLOTS, ...)): every block
-// when all_nb > 0 (after a rebuild), otherwise only the blocks listed dirty since the last tie
-__global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st, uint32_t nslots, uint32_t all_nb,
-                                                         Summ *__restrict__ out, Summ *__restrict__ sup, int dyn) {
-    if (tie_skip(st, dyn)) return;
+// block summaries of the home histogram (block b covers slots [b*SUMM_SLOTS, ...)), every block
+// (after a rebuild for a new capacity)
+__global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st, uint32_t nslots, uint32_t nb,
+                                                         Summ *__restrict__ out) {
     constexpr int PER = SUMM_SLOTS / 256;  // 16 slots = 4 words per thread
     __shared__ Summ sm[256];
-    const uint32_t nwork = all_nb ? all_nb : min(st->dirty_len, T.dirty_cap);
-    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
-        const uint32_t blk = all_nb ? w : T.dirty_list[w];
+    for (uint32_t blk = blockIdx.x; blk < nb; blk += gridDim.x) {
         const uint32_t beg = blk * SUMM_SLOTS + threadIdx.x * PER;
         Summ acc{0, 0};
         if (beg < nslots) {
@@ -1654,40 +1644,91 @@ __global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st,
             if ((threadIdx.x & (2 * sp - 1)) == 0) sm[threadIdx.x] = summ_cat(sm[threadIdx.x], sm[threadIdx.x + sp]);
             __syncthreads();
         }
-        __shared__ uint32_t s_last;
-        if (threadIdx.x == 0) {
-            // write-through (sc1) stores drained before the arrival count: the last arriver of the
-            // super-block reads them with sc1 loads, no release / acquire fence (cdna_hip_programming.md
-            // section 6 Guideline 16, R1)
-            __hip_atomic_store(&out[blk].q, sm[0].q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&out[blk].m, sm[0].m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            atomicAnd(&T.home_dirty[blk >> 5], ~(1u << (blk & 31)));
-            s_last = 0;
-            if (!all_nb && T.sup_pending) {  // the last dirty block of its super-block recomputes the super summary
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                s_last = atomicSub(&T.sup_pending[blk / SUPER_BLOCKS], 1u) == 1u;
-            }
-        }
-        __syncthreads();
-        if (s_last && threadIdx.x < 64) {
-            const uint32_t nb = (nslots + SUMM_SLOTS - 1) / SUMM_SLOTS, sb = blk / SUPER_BLOCKS, lane = threadIdx.x;
-            const uint32_t bi = sb * SUPER_BLOCKS + lane;
-            Summ x{0, 0};
-            if (bi < nb) {
-                x.q = __hip_atomic_load(&out[bi].q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                x.m = __hip_atomic_load(&out[bi].m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                Summ y;
-                y.q = __shfl_down(x.q, off);
-                y.m = __shfl_down(x.m, off);
-                if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
-            }
-            if (lane == 0) sup[sb] = x;
-        }
+        if (threadIdx.x == 0) out[blk] = sm[0];
         __syncthreads();
     }
+}
+// Refresh after merges: one workgroup per super-block (SUPER_BLOCKS = 64 blocks = two dirty-bitmap
+// words). Each wave recomputes dirty blocks (a lane composes 64 slots read as four 16-B vectors,
+// then an ordered wave reduction); wave 0 then recomposes the super-block. No cross-workgroup data.
+constexpr int REFRESH_THREADS = 1024;
+// one super-block (all threads of the block call it). wt: write-through (sc1) stores, for a reader
+// in another workgroup of the same launch
+__device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslots, uint32_t nb, Summ *__restrict__ summ,
+                                     Summ *__restrict__ sup, bool wt) {
+    static_assert(SUPER_BLOCKS == 64, "two dirty-bitmap words per super-block");
+    const uint64_t bits = (uint64_t)T.home_dirty[2 * sb] | ((uint64_t)T.home_dirty[2 * sb + 1] << 32);
+    if (!bits) return;
+    __shared__ Summ s_new[SUPER_BLOCKS];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
+    const int ndirty = __popcll(bits);
+    for (int k = wave; k < ndirty; k += nwaves) {
+        uint64_t m = bits;  // k-th set bit
+        for (int j = 0; j < k; j++) m &= m - 1;
+        const uint32_t bi = (uint32_t)__builtin_ctzll(m), blk = sb * SUPER_BLOCKS + bi;
+        const uint32_t s0 = blk * SUMM_SLOTS + 64 * lane;
+        Summ x{0, 0};
+        if (s0 < nslots) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(T.home_cnt + s0 / 4);
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const uint4 q = p[v];
+                const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int kk = 0; kk < 16; kk++)
+                    if (s0 + 16 * v + kk < nslots) x = summ_cat(x, summ_slot((w[kk >> 2] >> (8 * (kk & 3))) & 0xffu));
+            }
+        }
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            Summ y;
+            y.q = __shfl_down(x.q, off);
+            y.m = __shfl_down(x.m, off);
+            if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
+        }
+        if (lane == 0) {
+            if (wt) {
+                __hip_atomic_store(&summ[blk].q, x.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&summ[blk].m, x.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                summ[blk] = x;
+            }
+            s_new[bi] = x;
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const uint32_t bi = lane, blk = sb * SUPER_BLOCKS + bi;
+        Summ x{0, 0};
+        if (blk < nb) x = ((bits >> bi) & 1) ? s_new[bi] : summ[blk];
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            Summ y;
+            y.q = __shfl_down(x.q, off);
+            y.m = __shfl_down(x.m, off);
+            if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
+        }
+        if (lane == 0) {
+            if (wt) {
+                __hip_atomic_store(&sup[sb].q, x.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&sup[sb].m, x.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                sup[sb] = x;
+            }
+            T.home_dirty[2 * sb] = 0;
+            T.home_dirty[2 * sb + 1] = 0;
+        }
+    }
+    __syncthreads();
+}
+// Refresh after merges: one workgroup per super-block (SUPER_BLOCKS = 64 blocks = two dirty-bitmap
+// words). Each wave recomputes dirty blocks (a lane composes 64 slots read as four 16-B vectors,
+// then an ordered wave reduction); wave 0 then recomposes the super-block. No cross-workgroup data.
+__global__ void __launch_bounds__(REFRESH_THREADS) zbpe_home_refresh(Tables T, DevState *st, uint32_t nslots, uint32_t nb,
+                                                                     Summ *__restrict__ summ, Summ *__restrict__ sup,
+                                                                     int dyn) {
+    if (tie_skip(st, dyn)) return;
+    refresh_super(T, blockIdx.x, nslots, nb, summ, sup, false);
 }
 // super-block summaries: one wave composes SUPER_BLOCKS block summaries
 __global__ void __launch_bounds__(256) zbpe_super_summary(const Summ *__restrict__ summ, uint32_t nb, Summ *__restrict__ sup,
@@ -1902,17 +1943,17 @@ __device__ inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_
     return last;
 }
 constexpr int DECIDE_THREADS = 256;
-__global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, const uint64_t *__restrict__ tie_list,
-                                                                  uint32_t tie_cap, HomeView V, MergeLog *log, int dyn) {
-    if (tie_skip(st, dyn)) return;
+// Zig-order decision over the tied keys `list` (home << 32 | key; `len` of `total` collected: a
+// shortfall decides nothing). Needs DECIDE_THREADS threads. dyn: batch mode (halt / commit).
+__device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
+                                   MergeLog *log, int dyn) {
     __shared__ uint64_t s1[DECIDE_THREADS], s2[DECIDE_THREADS];
     __shared__ uint32_t sh[DECIDE_THREADS];
     __shared__ long long s_c1, s_c0, s_cw, s_last, s_free;
-    const uint32_t len = min(st->tie_len, tie_cap);
     uint64_t m1 = ~0ull, m2 = ~0ull;
     uint32_t hmax = 0;
     for (uint32_t i = threadIdx.x; i < len; i += DECIDE_THREADS) {
-        const uint64_t e = tie_list[i];
+        const uint64_t e = list[i];
         if (e < m1) { m2 = m1; m1 = e; } else if (e < m2) m2 = e;
         hmax = max(hmax, (uint32_t)(e >> 32));
     }
@@ -1948,7 +1989,7 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
     }
     __syncthreads();
     if (threadIdx.x) return;
-    uint32_t verdict = st->tie_len > tie_cap ? 1u : 0u;
+    uint32_t verdict = total > len ? 1u : 0u;
     const int64_t s = s_free;  // first free slot at or after h1
     if (s < 0) verdict = 1;     // the run of h1 wraps (or is absurdly long)
     if (m2 != ~0ull && s > (int64_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
@@ -1956,9 +1997,8 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
     if (lf != -2 && (lf < 0 || (long long)hmax >= lf + 1)) verdict = 1;  // a tied pair may have wrapped
     st->tie_verdict = verdict;
     st->tie_winner = (uint32_t)m1;
-    st->dirty_len = 0;
     if (dyn) {
-        if (st->tie_len != st->tie_count) atomicOr(&st->error, 128u);
+        if (total != st->tie_count) atomicOr(&st->error, 128u);
         const uint32_t key = (uint32_t)m1;
         if (verdict) {
             st->halt = HALT_TIE;
@@ -1971,6 +2011,12 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
             log[st->cur_x - 256] = MergeLog{key, st->top_count, (uint32_t)st->live_tokens, st->tie_count};
         }
     }
+}
+__global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, const uint64_t *__restrict__ tie_list,
+                                                                  uint32_t tie_cap, HomeView V, MergeLog *log, int dyn) {
+    if (tie_skip(st, dyn)) return;
+    const uint32_t total = st->tie_len;
+    decide_body(st, tie_list, min(total, tie_cap), total, V, log, dyn);
 }
 
 // rebuild the home histogram for a new Zig capacity

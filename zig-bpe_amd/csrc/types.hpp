@@ -42,7 +42,7 @@ struct DevState {
     uint32_t total_occ;      // running sum of last_occ (encode bookkeeping)
     uint32_t theta;          // hot-list threshold: every live id with count >= theta is in the hot list
     uint32_t hot_len;        // ids appended to the hot list (may exceed its capacity -> rebuild)
-    uint32_t dirty_len;      // home-histogram blocks changed since their summaries were computed
+    uint32_t pad_dirty;
     uint32_t ticket;         // zbpe_select: blocks done (the last one reduces), reset by it
     uint32_t last_gocc;      // occurrences merged by the last merge on all ranks
     uint32_t consumed;       // 1: this shard's first live token was the b of the left rank's last occurrence
@@ -90,11 +90,8 @@ struct Tables {
     uint32_t hot_cap;
     uint32_t *home_cnt; // u8 x 4 per word: live keys per home slot of the Zig map (nullptr: not kept)
     uint32_t home_mask; // Zig map capacity - 1 the histogram is kept for
-    uint32_t *home_dirty;  // 1 bit per SUMM_SLOTS block: summary stale
-    uint32_t *dirty_list;  // stale block indices (each listed once)
-    uint32_t dirty_cap;
+    uint32_t *home_dirty;  // 1 bit per SUMM_SLOTS block: summary stale (2 words per super-block)
     int32_t *tok_cnt;      // [65536] live occurrences per token id (global; picks the scan's key token)
-    uint32_t *sup_pending; // per super-block: listed dirty blocks whose summaries are not yet recomputed
     uint32_t *lst_off, *lst_len;  // [65536] token occurrence lists in the arena (nullptr: not kept)
 };
 
