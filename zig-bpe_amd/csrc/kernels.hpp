@@ -490,23 +490,45 @@ __device__ inline uint32_t occ_vector(const ScanArgs &A, NeighbourHist &H, int64
         uint64_t q = i < 4 ? W0 : i < 8 ? W1 : i < 12 ? W2 : W3;
         return (uint32_t)(q >> ((i & 3) * 16)) & 0xffffu;
     };
+    // live-slot mask of the window (bit i: window token i is not a hole); slots outside the stream
+    // read as holes, so a walk that leaves the window falls back to occ_slow (halo, stream ends)
+    uint32_t live = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) live |= (win(i) != HOLE ? 1u : 0u) << i;
     uint32_t hits = 0;
     while (m) {
         const int k = __ffs(m) - 1;
         m &= m - 1;
+        const int i = k + 2;  // window index of p
         const int64_t p = vi * 8 + k;
-        const uint32_t t0 = win(k), t1 = win(k + 1), t3 = win(k + 3), t4 = win(k + 4), t5 = win(k + 5);
-        // fast path: tok[p-2 .. p+3] all live and inside the stream
-        const bool fast = p >= 2 && p + 3 < n && t0 != HOLE && t1 != HOLE && t3 != HOLE && t4 != HOLE && t5 != HOLE;
+        // next / previous live window slots around p (14 = none)
+        const uint32_t after = live >> (i + 1), before = live & ((1u << i) - 1u);
+        const int q = after ? i + 1 + __builtin_ctz(after) : 14;
         int hit;
+        bool fast = q < 14 && before != 0 && p >= 2 && p + 3 < n;
+        int l = 0, ll = -1, r = 14, rn = 14;
         if (fast) {
-            hit = t3 == A.b;
+            l = 31 - __builtin_clz(before);
+            const uint32_t aq = live >> (q + 1);
+            r = aq ? q + 1 + __builtin_ctz(aq) : 14;
+            const uint32_t bl = live & ((1u << l) - 1u);
+            ll = bl ? 31 - __builtin_clz(bl) : -1;
+            if (r < 14) {
+                const uint32_t ar = live >> (r + 1);
+                rn = ar ? r + 1 + __builtin_ctz(ar) : 14;
+            }
+            // every token the delta rules may look at must be inside the window
+            fast = r < 14 && (win(r) != A.a || rn < 14) && (win(l) != A.b || ll >= 0);
+        }
+        if (fast) {
+            hit = win(q) == A.b;
             if (hit && A.count_deltas) {
-                const bool merged_end = (t1 == A.b) && (t0 == A.a);
-                if (!merged_end) H.left((uint16_t)t1);
-                const bool r_occ = (t4 == A.a) && (t5 == A.b);
+                const uint32_t tl = win(l), tr = win(r);
+                const bool merged_end = (tl == A.b) && (win(ll < 0 ? 0 : ll) == A.a);
+                if (!merged_end) H.left((uint16_t)tl);
+                const bool r_occ = (tr == A.a) && (win(rn > 13 ? 13 : rn) == A.b);
                 if (r_occ) xx++;
-                else H.right((uint16_t)t4);
+                else H.right((uint16_t)tr);
             }
         } else {
             hit = occ_slow(A, H, p, xx);
