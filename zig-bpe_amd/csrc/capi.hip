@@ -125,6 +125,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "replace_split") e.replace_split = value != 0;
     else if (k == "list_mode" && value >= 0 && value <= 1) e.list_mode = (int)value;
     else if (k == "compact_den_lists" && value >= 1) e.compact_den_lists = (uint64_t)value;
+    else if (k == "list_grid" && value >= 0) e.list_grid = (int)value;
     else if (k == "list_ratio" && value >= 1) e.list_ratio = (uint32_t)value;
     else if (k == "list_start" && value >= 0) e.list_start = (uint64_t)value;
     else if (k == "hot_target" && value > 0) e.hot_target = (uint64_t)value;

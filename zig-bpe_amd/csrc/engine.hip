@@ -491,10 +491,13 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
 
 using ScanFn = void (*)(ScanArgs);
 // 0 is the default (unroll 4, non-temporal loads, next-token filter); the others for A/B runs
+// 2 (dense matches, chosen by scan_auto): candidates compacted per wave before phase 2
+// (`tools/scan_variants.py`: +22 % at 1/75 density, -14 % at 1/400, so only above 1/128)
 static const ScanFn kScanVariants[] = {zbpe_scan_pairs_t<4, true, true>,  zbpe_scan_pairs_t<8, true, true>,
-                                       zbpe_scan_pairs_t<4, false, true>, zbpe_scan_pairs_t<4, true, false>,
-                                       zbpe_scan_pairs_t<2, true, true>,  zbpe_scan_pairs_t<4, true, true, false>};
-static const int kScanUnroll[] = {4, 8, 4, 4, 2, 4};
+                                       zbpe_scan_pairs_t<4, true, true, true, true>, zbpe_scan_pairs_t<4, true, false>,
+                                       zbpe_scan_pairs_t<2, true, true>,  zbpe_scan_pairs_t<4, true, true, false>,
+                                       zbpe_scan_pairs_t<4, false, true>};
+static const int kScanUnroll[] = {4, 8, 4, 4, 2, 4, 4};
 
 zbpe_status Engine::set_scan_variant(int v) {
     if (v < 0 || v >= (int)(sizeof(kScanVariants) / sizeof(kScanVariants[0])))
@@ -506,12 +509,11 @@ zbpe_status Engine::set_scan_variant(int v) {
     return ZBPE_OK;
 }
 
-zbpe_status Engine::launch_scan(const ScanArgs &A, uint64_t expected_occ) {
-    // default variant: non-temporal loads pay when matches are rare; when they are dense the
-    // phase-2 window re-reads want the lines cached (variant 2: plain loads)
+zbpe_status Engine::launch_scan(const ScanArgs &A, uint64_t expected_occ, int grid) {
+    // default variant 0; when matches are dense (> 1/128 of the stream) the compacted phase 2
     int v = scan_variant;
-    if (v == 0 && scan_auto && expected_occ * 64 > (uint64_t)A.n) v = 2;
-    hipLaunchKernelGGL(kScanVariants[v], dim3(scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, A);
+    if (v == 0 && scan_auto && expected_occ * 128 > (uint64_t)A.n) v = 2;
+    hipLaunchKernelGGL(kScanVariants[v], dim3(grid > 0 ? grid : scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, A);
     LAUNCH_OK();
     return ZBPE_OK;
 }
@@ -620,6 +622,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     // arena: the occurrence lists (<= live tokens) + the records appended until the next compaction
     CHECK(ensure(&d_lists, lists_cap, std::min<size_t>(0xFFFFFFF0u, n + n / 2 + (16u << 20)), "occurrence arena"));
     lists_on = false;
+    list_streak = false;
     if (!T.id_key || T.id_cap < (1u << 20)) {
         if (T.id_key) { (void)hipFree(T.ht); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt); T.ht = nullptr; T.id_key = T.id_cnt = nullptr; }
         CHECK(alloc_tables(1u << 20));
@@ -779,7 +782,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         ScanArgs A{d_tok[cur], slots, 0, 0, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
                    pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 1, world > 1 ? d_halo : nullptr,
                    lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log};
-        CHECK(launch_scan(A, top0));
+        // a batch that follows one of list scans only launches a smaller grid (fewer idle workgroups
+        // to dispatch); a stream scan still completes on it, only slower
+        CHECK(launch_scan(A, top0, list_streak ? list_grid : 0));
         if (timed) HIP_OK(hipEventRecord(bev[4 * i + 2], stream));
         CHECK(comm_sum(d_delta, 2ull * X + 2));
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
@@ -853,6 +858,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             trace.insert(trace.end(), row, row + ZBPE_TRACE_COLS);
         }
     }
+    uint32_t nlist = 0;
+    for (uint32_t i = 0; i < m; i++) nlist += h_log[X0 - 256 + i].mode;
+    list_streak = m > 0 && nlist == m;
     n_live = h_st->live_tokens;
     if (world > 1) halo_from_boundaries();
     *done = m;

@@ -91,6 +91,8 @@ struct Engine {
     uint32_t *d_list_cnt = nullptr, *d_list_total = nullptr;
     size_t list_cnt_cap = 0;
     bool lists_on = false;
+    bool list_streak = false;   // the last batch used list scans only
+    int list_grid = 0;          // scan grid after such a batch (option "list_grid"; 0 = the full grid)
     int list_mode = 1;          // 0: never build lists, 1: once pair counts are small against the stream
     uint32_t list_ratio = 256;  // list scan when list length * ratio < stream slots
     uint64_t list_start = 64;   // build lists at a compaction once top count * list_start < live tokens (0: always)
@@ -158,7 +160,7 @@ struct Engine {
     zbpe_status launch_argmax(uint32_t X, int roll);
     int argmax_blocks(uint32_t X) const;
     int scan_grid(int64_t slots) const;
-    zbpe_status launch_scan(const ScanArgs &A, uint64_t expected_occ);
+    zbpe_status launch_scan(const ScanArgs &A, uint64_t expected_occ, int grid = 0);
     zbpe_status rebuild_hot();
     zbpe_status rebuild_home(uint64_t cap);
     zbpe_status select_ready();

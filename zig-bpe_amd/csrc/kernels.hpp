@@ -473,19 +473,33 @@ __device__ inline void wave_flush_records(const ScanArgs &A, const uint32_t *rec
 
 // occurrences of (a, b) starting in vector vi (8 tokens) whose bits are set in m; returns the hit mask.
 // Window = vectors vi-1, vi, vi+1 re-read from cache (they were just streamed by this wave).
+// occurrences of (a, b) starting in vector vi (8 tokens) whose bits are set in m, from the window
+// tok[p0-2 .. p0+11] (p0 = 8*vi) given as the previous vector's last dword pw, the vector cv and the
+// next vector's first two dwords nx, ny (holes outside the stream); returns the hit mask.
+__device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64_t vi, uint32_t m, uint32_t &xx,
+                                      uint32_t pw, uint4 cv, uint32_t nx, uint32_t ny);
 __device__ inline uint32_t occ_vector(const ScanArgs &A, NeighbourHist &H, int64_t vi, int64_t nvec, uint32_t m,
                                       uint32_t &xx) {
     const uint16_t *tok = A.tok;
+    const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
+    const uint32_t pw = vi > 0 ? tv[vi - 1].w : 0xffffffffu;
+    const uint4 cv = tv[vi];
+    uint32_t nx = 0xffffffffu, ny = 0xffffffffu;
+    if (vi + 1 < nvec) {
+        const uint4 nv = tv[vi + 1];
+        nx = nv.x;
+        ny = nv.y;
+    }
+    return occ_window(A, H, vi, m, xx, pw, cv, nx, ny);
+}
+__device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64_t vi, uint32_t m, uint32_t &xx,
+                                      uint32_t pw, uint4 cv, uint32_t nx, uint32_t ny) {
     const int64_t n = A.n;
-    const uint4 HOLES = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-    const uint4 pv = vi > 0 ? reinterpret_cast<const uint4 *>(tok)[vi - 1] : HOLES;
-    const uint4 cv = reinterpret_cast<const uint4 *>(tok)[vi];
-    const uint4 nv = vi + 1 < nvec ? reinterpret_cast<const uint4 *>(tok)[vi + 1] : HOLES;
     // window of 14 tokens tok[p0-2 .. p0+11], p0 = 8*vi, in four u64 (no scratch)
-    const uint64_t W0 = (uint64_t)pv.w | ((uint64_t)cv.x << 32);
+    const uint64_t W0 = (uint64_t)pw | ((uint64_t)cv.x << 32);
     const uint64_t W1 = (uint64_t)cv.y | ((uint64_t)cv.z << 32);
-    const uint64_t W2 = (uint64_t)cv.w | ((uint64_t)nv.x << 32);
-    const uint64_t W3 = (uint64_t)nv.y;
+    const uint64_t W2 = (uint64_t)cv.w | ((uint64_t)nx << 32);
+    const uint64_t W3 = (uint64_t)ny;
     auto win = [&](int i) -> uint32_t {
         uint64_t q = i < 4 ? W0 : i < 8 ? W1 : i < 12 ? W2 : W3;
         return (uint32_t)(q >> ((i & 3) * 16)) & 0xffffu;
@@ -543,11 +557,40 @@ __device__ inline void pres_set(const ScanArgs &A, int64_t pos) {
     atomicOr(&A.pres[(blk / PRES_GROUP) * A.vp + A.X], 1u << (blk % PRES_GROUP));
 }
 
-template <int UNROLL, bool NT, bool FILTER, bool PIPE>
+// One candidate position p holding the scan's key token (a, or b when by_b): is it (part of) an
+// occurrence of (a, b)? On a hit *pr = the occurrence's start and the deltas are counted. The
+// window around p comes from one 16-B vector (+ its cached neighbours in occ_vector).
+__device__ inline bool resolve_candidate(const ScanArgs &A, NeighbourHist &H, int64_t p, bool by_b, int64_t nvec,
+                                         uint32_t &xx, uint32_t &pr) {
+    const uint16_t *tok = A.tok;
+    const int64_t vi = p >> 3;
+    const int k = (int)(p & 7);
+    if (!by_b) {
+        pr = (uint32_t)p;
+        return occ_vector(A, H, vi, nvec, 1u << k, xx) != 0;
+    }
+    const uint4 cv = reinterpret_cast<const uint4 *>(tok)[vi];
+    int64_t q = -1;  // the live token before p (q < 0: the left shard's, which owns the occurrence)
+    uint32_t tq = HOLE;
+    for (int j = k - 1; j >= 0 && q < 0; j--) {
+        const uint32_t t = tok_at(cv, j);
+        if (t != HOLE) { q = vi * 8 + j; tq = t; }
+    }
+    if (q < 0) {
+        q = prev_live_h(A, p);
+        if (q >= 0) tq = tok[q];
+    }
+    if (q >= 0 && tq == A.a && occ_vector(A, H, q >> 3, nvec, 1u << (q & 7), xx)) {
+        pr = (uint32_t)q;
+        return true;
+    }
+    return false;
+}
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A);
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
                                                                      uint32_t len);
-template <int UNROLL, bool NT, bool FILTER, bool PIPE = true>
+template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false>
 __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
     if (A0.dyn && A0.st->halt) return;
     const ScanArgs A = scan_args_resolve(A0);
@@ -566,7 +609,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
-    scan_pairs_body<UNROLL, NT, FILTER, PIPE>(A);
+    scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT>(A);
 }
 // List scan: every entry of the key token's list is a position that held the key when it was
 // listed; entries overwritten since (merged or turned into holes) fail the token check.
@@ -594,24 +637,15 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
         }
     }
     const uint32_t stride = gridDim.x * SCAN_THREADS;
+    const int64_t nvec = (A.n + 7) / 8;
     const uint32_t len64 = (len + 63) & ~63u;  // wave-uniform trip count (wave_append)
     for (uint32_t i = blockIdx.x * SCAN_THREADS + threadIdx.x; i - lane < len64; i += stride) {
         bool hit = false;
         uint32_t pr = 0;
         if (i < len) {
+            // the entry still holds the key token: resolve it from a cached window around it
             const int64_t p = L[i];
-            if (tok[p] == key) {
-                if (!by_b) {
-                    hit = occ_slow(A, H, p, xx);
-                    pr = (uint32_t)p;
-                } else {
-                    const int64_t q = prev_live_h(A, p);  // q < 0: the a is the left shard's, which owns it
-                    if (q >= 0 && tok[q] == A.a && occ_slow(A, H, q, xx)) {
-                        hit = true;
-                        pr = (uint32_t)q;
-                    }
-                }
-            }
+            if (tok[p] == key) hit = resolve_candidate(A, H, p, by_b, nvec, xx, pr);
         }
         const uint64_t m = __ballot(hit);
         if (!m) continue;
@@ -640,7 +674,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
         }
     }
 }
-template <int UNROLL, bool NT, bool FILTER, bool PIPE>
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A) {
     constexpr int STAGE = 4;                      // vectors per lane per record-staging step
     constexpr uint32_t WREC = 64 * STAGE * 8 / 2;  // at most one occurrence per 2 tokens
@@ -648,6 +682,8 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
     static_assert(PRES_BLK % (64 * UNROLL * 8) == 0, "presence blocks hold whole wave-tiles");
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
     __shared__ uint32_t s_rec[SCAN_THREADS / 64][WREC];
+    constexpr uint32_t CAND_CAP = COMPACT ? 512 : 1;  // dense form: candidates resolved per round per wave
+    __shared__ uint32_t s_cand[SCAN_THREADS / 64][CAND_CAP];
     __shared__ uint32_t s_any;
     __shared__ unsigned long long s_scanned;
     for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
@@ -759,6 +795,52 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             if (PIPE) load_tile(wt_next * WT_VEC);
         }
         if (__ballot(cand != 0) != 0) {
+        if constexpr (COMPACT) {
+            // phase 2, dense form: the tile's candidates are compacted into a per-wave LDS list and
+            // resolved one per lane (a lane-per-vector loop would iterate as often as the busiest lane)
+            const uint32_t cnt = (uint32_t)__popcll(cand);
+            const uint32_t incl = wave_incl_scan(cnt);
+            const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+            const uint64_t tile_blk = (uint64_t)vbase * 8 / PRES_BLK;
+            bool tile_hit = false;
+            uint32_t *wc = s_cand[wib];
+            for (uint32_t r0 = 0; r0 < total; r0 += CAND_CAP) {
+                uint32_t idx = incl - cnt;
+                uint64_t cc = cand;
+                while (cc) {
+                    const int bit = __builtin_ctzll(cc);
+                    cc &= cc - 1;
+                    if (idx >= r0 && idx < r0 + CAND_CAP)
+                        wc[idx - r0] = (uint32_t)((vbase + (bit >> 3) * 64 + lane) * 8 + (bit & 7));
+                    idx++;
+                }
+                wave_lds_sync();
+                const uint32_t nr = min(total - r0, (uint32_t)CAND_CAP);
+                for (uint32_t j = lane; j - lane < nr; j += 64) {
+                    bool hit = false;
+                    uint32_t pr = 0;
+                    if (j < nr) hit = resolve_candidate(A, H, wc[j], by_b, nvec, xx, pr);
+                    const uint64_t hm = __ballot(hit);
+                    if (!hm) continue;
+                    any = 1;
+                    const uint32_t nh = (uint32_t)__popcll(hm);
+                    if (nbuf + nh > WREC) {
+                        wave_lds_sync();
+                        wave_flush_records(A, wrec, nbuf);
+                        nbuf = 0;
+                        wave_lds_sync();
+                    }
+                    if (hit) {
+                        wrec[nbuf + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = pr;
+                        if (A.pres && pr / PRES_BLK != tile_blk) pres_set(A, pr);
+                    }
+                    nbuf += nh;
+                    tile_hit = true;
+                }
+                wave_lds_sync();
+            }
+            if (A.pres && tile_hit && lane == 0) pres_set(A, vbase * 8);
+        } else {
         // phase 2 (lanes with candidates): resolve occurrences, stage them per STAGE vectors
 #pragma unroll
         for (int ug = 0; ug < UNROLL; ug += STAGE) {
@@ -808,6 +890,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             nbuf += total;
             if (A.pres && lane == 0) pres_set(A, vbase * 8);
         }
+        }  // per-vector phase 2
         }  // tile has candidates
         if (!more) break;
         wt = wt_next;
