@@ -155,6 +155,21 @@ def test_encode_vs_oracle(engine):
         assert np.array_equal(engine.encode(m, t), O.encode(m, t))
 
 
+@pytest.mark.parametrize("list_mode,ratio", [(0, 256), (1, 1)])
+def test_encode_list_and_stream_scans_vs_oracle(list_mode, ratio):
+    """Encode with occurrence lists off, and on for every merge that can use one (ratio 1)."""
+    e = zbpe.Engine(0)
+    e.set_option("list_mode", list_mode)
+    e.set_option("list_ratio", ratio)
+    for kind, seed, n, vocab in (("words_utf8", 44, 300000, 800), ("runs", 45, 80000, 500), ("uniform", 46, 20000, 600)):
+        text = zbpe.synth_corpus(kind, seed, n)
+        m, _, _ = e.train(text, vocab)
+        other = zbpe.synth_corpus(kind, seed + 100, n)
+        for t in (text, other):
+            assert np.array_equal(e.encode(m, t), O.encode(m, t)), (kind, list_mode)
+    e.close()
+
+
 def test_encode_runs_vs_oracle(engine):
     text = zbpe.synth_corpus("runs", 43, 100000)
     m, _, _ = _train(engine, text, 600)

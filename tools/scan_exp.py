@@ -9,6 +9,8 @@ text = zbpe.synth_corpus("words_utf8", 0x5EED0004, 1 << 30, threads=16)
 e = zbpe.Engine(0)
 e.upload(text)
 pairs = {"rare": (1, 2), "e_sp": (101, 32), "sp_t": (32, 116), "t_h": (116, 104), "i_n": (105, 110)}
+if os.environ.get("PAIRS"):  # name=a:b,...
+    pairs = {kv.split("=")[0]: tuple(int(x) for x in kv.split("=")[1].split(":")) for kv in os.environ["PAIRS"].split(",")}
 variants = [int(x) for x in os.environ.get("VARIANTS", "0,2,6,7").split(",")]
 res = {}
 for rnd in range(3):

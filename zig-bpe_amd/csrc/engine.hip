@@ -1060,23 +1060,43 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
     trained = false;
     CHECK(alloc_stream(n));
     HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
-    CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(n / 2 + 1, 1), "occurrence records"));
+    // token occurrence lists (as in train): a merge's scan walks the shorter of its tokens' lists
+    // when that is short; every merge's records become the list of its new token. Needs distinct
+    // new tokens that are not bytes (they would overwrite a list) and vocab ids that fit the build.
+    uint32_t max_tok = 255;
+    bool distinct = true;
+    {
+        std::vector<uint8_t> seen(65536, 0);
+        for (size_t k = 0; k < n_merges; k++) {
+            const uint32_t X = triples[3 * k + 2];
+            max_tok = std::max<uint32_t>(max_tok, std::max<uint32_t>(X, std::max(triples[3 * k], triples[3 * k + 1])));
+            if (X < 256 || seen[X]) distinct = false;
+            seen[X] = 1;
+        }
+    }
+    const uint32_t vp = (max_tok + 1 + 63) & ~63u;
+    const bool use_lists = list_mode && distinct && vp <= PRES_MAX_VP && n < 0x70000000u && n_merges > 0;
+    pres_on = false;
+    if (use_lists) {
+        CHECK(ensure(&d_lists, lists_cap, 2 * n + 1024, "occurrence arena"));  // lists <= n, records <= n
+        pres_vp = vp;
+        CHECK(build_lists());
+    } else {
+        lists_on = false;
+        CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(n / 2 + 1, 1), "occurrence records"));
+    }
+    uint32_t *recbuf = use_lists ? d_lists : d_rec;
+    const uint32_t reccap = (uint32_t)(use_lists ? lists_cap : rec_cap);
+    uint32_t *tail = d_delta + DELTA_WORDS - 32;  // scratch: encode keeps no counts
     uint64_t holes = 0;
     for (size_t k = 0; k < n_merges; k++) {
         const uint32_t a = triples[3 * k], b = triples[3 * k + 1], X = triples[3 * k + 2];
-        if (a == b) {
-            CHECK(sync_state());
-            holes += h_st->total_occ;
-            HIP_OK(hipMemsetAsync(&d_st->total_occ, 0, 4, stream));
-            n_live -= h_st->total_occ;
-            if (holes) { CHECK(compact()); holes = 0; }
-        }
-        uint32_t *tail = d_delta + DELTA_WORDS - 32;  // scratch: encode keeps no counts
-        ScanArgs A{d_tok[cur], n_slots, a, b, d_delta, d_delta + 65536, d_st, d_rec, (uint32_t)rec_cap, 0, tail, tail + 1, Halo{}};
+        ScanArgs A{d_tok[cur], n_slots, a, b, d_delta, d_delta + 65536, d_st, recbuf, reccap, 0, tail, tail + 1, Halo{},
+                   nullptr, vp, X, nullptr, 0, nullptr, use_lists ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio,
+                   use_lists ? 1 : 0, nullptr};
         if (a != b) {
-            CHECK(launch_scan(A, (uint64_t)n_slots / 64));
-            LAUNCH_OK();
-        } else {
+            CHECK(launch_scan(A, 0));
+        } else {  // holes are transparent to the self-pair path
             const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);
             CHECK(ensure(&d_tile_fn, tile_fn_cap, ntiles, "self tiles"));
             CHECK(ensure(&d_carry, carry_cap, ntiles, "self carry"));
@@ -1087,11 +1107,9 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
             zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
             LAUNCH_OK();
         }
-        zbpe_apply<<<2048, 256, 0, stream>>>(d_tok[cur], n_slots, d_rec, (uint32_t)rec_cap, d_st, X);
+        zbpe_encode_apply<<<512, 256, 0, stream>>>(d_tok[cur], n_slots, recbuf, reccap, use_lists ? 1 : 0, X, d_st, T, tail);
         LAUNCH_OK();
-        zbpe_reset_merge<<<1, 256, 0, stream>>>(d_st, d_delta, d_delta + 65536, 0);
-        LAUNCH_OK();
-        if ((k & 63) == 63) {
+        if (!use_lists && (k & 255) == 255) {  // without lists: squeeze the holes now and then
             CHECK(sync_state());
             holes += h_st->total_occ;
             n_live -= h_st->total_occ;

@@ -1250,6 +1250,35 @@ __global__ void zbpe_halo_build(const Boundary *__restrict__ bnd, int rank, int 
         for (int k = 0; k < bnd[r].nfirst && H.nright < 3; k++) halo_push_right(H, bnd[r].first[k]);
     *out = H;
 }
+// encode: apply one merge at the recorded occurrences, then (last block to finish) roll the
+// counters; with occurrence lists the records, kept in the arena, become X's list
+__global__ void __launch_bounds__(256) zbpe_encode_apply(uint16_t *tok, int64_t n, uint32_t *rec, uint32_t rec_cap, int rec_arena,
+                                                         uint32_t X, DevState *st, Tables T, uint32_t *scratch) {
+    const uint32_t top = rec_arena ? st->arena_top : 0;
+    const uint32_t cap = rec_cap > top ? rec_cap - top : 0;
+    const uint32_t cnt = min(st->rec_count, cap);
+    const uint32_t *r = rec + top;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
+        const int64_t p = r[i];
+        tok[p] = (uint16_t)X;
+        const int64_t q = next_live(tok, n, p);
+        if (q >= 0) tok[q] = HOLE;
+    }
+    __shared__ uint32_t s_last;
+    __syncthreads();  // every thread of the block has read rec_count / arena_top
+    if (threadIdx.x == 0) s_last = atomicAdd(&st->ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last || threadIdx.x) return;
+    st->total_occ += cnt;
+    if (rec_arena && T.lst_off) {
+        T.lst_off[X] = top;
+        T.lst_len[X] = cnt;
+        st->arena_top = top + cnt;
+    }
+    st->rec_count = 0;
+    st->ticket = 0;
+    scratch[0] = scratch[1] = 0;  // the scan's xx / occurrence tallies (encode keeps no counts)
+}
 // end of merge: clear the neighbour histograms [0, X) and roll the per-merge counters
 __global__ void __launch_bounds__(256) zbpe_reset_merge(DevState *st, uint32_t *left, uint32_t *right, uint32_t X) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
