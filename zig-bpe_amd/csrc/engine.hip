@@ -56,7 +56,7 @@ void Engine::release() {
     f(T.ht); f(T.id_key); f(T.id_cnt);
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand);
     for (auto &e : bev) if (e) (void)hipEventDestroy(e);
     bev.clear();
     if (h_st) (void)hipHostFree(h_st);
@@ -69,7 +69,7 @@ void Engine::release() {
     if (h_bnd) (void)hipHostFree(h_bnd);
     h_bnd = nullptr;
     comm.reset();
-    d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr;
+    d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr; d_cand = nullptr;
     d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
     d_summ = nullptr; d_count_hist = nullptr; h_count_hist = nullptr; hot_cap_alloc = home_words_cap = 0; home_slots = 0;
     dirty_bits_cap = 0; d_sup = nullptr; sup_cap = 0; d_pres = nullptr; pres_cap = 0;
@@ -100,6 +100,7 @@ zbpe_status Engine::init(int dev) {
     bev.resize(4 * MAX_BATCH);
     for (auto &e : bev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no L2 writeback
     HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
+    HIP_OK(hipMalloc(&d_cand, (size_t)NEXT_MAX_SEL * NEXT_CAND * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_count_hist, COUNT_BINS * sizeof(uint32_t)));
     HIP_OK(hipHostMalloc((void **)&h_count_hist, COUNT_BINS * sizeof(uint32_t), hipHostMallocDefault));
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
@@ -674,6 +675,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         stats.count_pairs_calls++;
     }
     run = RunCtx{};
+    begun = false;
     run.out_triples = out_triples;
     run.out_counts = out_counts;
     run.verbose = verbose;
@@ -768,15 +770,18 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         const bool timed = merge_timing && X % merge_timing == 0;
         if (timed) HIP_OK(hipEventRecord(bev[4 * i], stream));
         uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
-        // merge start (halt checks, tie_on) fused into the tie collection
-        zbpe_tie_collect<<<64, 256, 0, stream>>>(T, d_st, 0, (uint32_t)(C ? C - 1 : 0), d_tie_list, (uint32_t)tie_list_cap, 1,
-                                                 BeginArgs{X, C, (uint32_t)lists_cap, d_log});
-        LAUNCH_OK();
-        if (C) {
-            zbpe_home_refresh<<<nsb, REFRESH_THREADS, 0, stream>>>(T, d_st, (uint32_t)C, nb, d_summ, d_sup, 1);
+        // merge start (halt checks, tie_on, ties): done by the previous merge's zbpe_select_next,
+        // else fused into the tie collection + refresh + decide
+        if (!fused_select || (i == 0 && !begun)) {
+            zbpe_tie_collect<<<64, 256, 0, stream>>>(T, d_st, 0, (uint32_t)(C ? C - 1 : 0), d_tie_list, (uint32_t)tie_list_cap, 1,
+                                                     BeginArgs{X, C, (uint32_t)lists_cap, d_log});
             LAUNCH_OK();
-            zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 1);
-            LAUNCH_OK();
+            if (C) {
+                zbpe_home_refresh<<<nsb, REFRESH_THREADS, 0, stream>>>(T, d_st, (uint32_t)C, nb, d_summ, d_sup, 1);
+                LAUNCH_OK();
+                zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 1);
+                LAUNCH_OK();
+            }
         }
         if (timed) HIP_OK(hipEventRecord(bev[4 * i + 1], stream));
         ScanArgs A{d_tok[cur], slots, 0, 0, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
@@ -805,7 +810,21 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             zbpe_halo_build<<<1, 1, 0, stream>>>(d_bnd_all, rank, world, d_halo, d_st);
             LAUNCH_OK();
         }
-        CHECK(launch_argmax(X, 1));
+        if (fused_select) {
+            if (hot_stale) CHECK(rebuild_hot());
+            const uint64_t work = std::max<uint64_t>(T.hot_cap / 4, 2ull * X);
+            const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
+            NextArgs N{BeginArgs{X + 1, C, (uint32_t)lists_cap, d_log}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
+                       d_bnd_all, world};
+            zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, d_delta, X, N);
+            LAUNCH_OK();
+            if (C && X + 1 < run.vocab) {  // returns at once unless merge X+1 is a tie the select gathered
+                zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 1);
+                LAUNCH_OK();
+            }
+        } else {
+            CHECK(launch_argmax(X, 1));
+        }
         if (timed) HIP_OK(hipEventRecord(bev[4 * i + 3], stream));
     }
     if (world > 1) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
@@ -813,6 +832,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     const double wall = now_s() - t0;
     batches++;
     const uint32_t m = h_st->halt ? h_st->halt_at - X0 : K;
+    begun = fused_select && !h_st->halt;  // the last select started merge X0 + K
     if (h_st->halt) {
         *halted = true;
         batch_halts++;

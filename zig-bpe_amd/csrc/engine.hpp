@@ -101,8 +101,11 @@ struct Engine {
     std::vector<float> trace;
     // device-resident merge loop
     uint32_t merge_batch = 32;      // merges enqueued per host sync (1: synchronous loop)
-    bool merge_timing = true;
-    bool replace_split = false;     // profiling: apply and count update as separate launches       // HIP events around every scan of a batch (roofline, stats)
+    uint32_t merge_timing = 8;     // HIP events around every merge_timing-th merge of a batch (0: none)
+    bool replace_split = false;     // profiling: apply and count update as separate launches
+    bool fused_select = true;       // zbpe_select_next: the select of merge X also starts merge X+1 (ties included)
+    bool begun = false;             // the next batch's first merge was started by the last batch's final select
+    uint32_t *d_cand = nullptr;     // zbpe_select_next: keys at each argmax block's max
     MergeLog *d_log = nullptr;
     std::vector<MergeLog> h_log;
     Halo *d_halo = nullptr;

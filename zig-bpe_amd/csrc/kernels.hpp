@@ -2077,32 +2077,39 @@ __device__ inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_
     return last;
 }
 constexpr int DECIDE_THREADS = 256;
+// two smallest of two (smallest, second smallest) pairs
+__device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uint64_t b2) {
+    const uint64_t a1 = m1, a2 = m2;
+    m1 = min(a1, b1);
+    m2 = min(max(a1, b1), min(a2, b2));
+}
 // Zig-order decision over the tied keys `list` (home << 32 | key; `len` of `total` collected: a
-// shortfall decides nothing). Needs DECIDE_THREADS threads. dyn: batch mode (halt / commit).
+// shortfall decides nothing). NT threads (>= 192: three waves compute carries). dyn: batch mode
+// (halt / commit).
+template <int NT = DECIDE_THREADS>
 __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
                                    MergeLog *log, int dyn) {
-    __shared__ uint64_t s1[DECIDE_THREADS], s2[DECIDE_THREADS];
-    __shared__ uint32_t sh[DECIDE_THREADS];
+    static_assert(NT >= 192 && NT % 64 == 0, "three carry waves");
+    __shared__ uint64_t s1[NT / 64], s2[NT / 64];
+    __shared__ uint32_t sh[NT / 64];
     __shared__ long long s_c1, s_c0, s_cw, s_last, s_free;
     uint64_t m1 = ~0ull, m2 = ~0ull;
     uint32_t hmax = 0;
-    for (uint32_t i = threadIdx.x; i < len; i += DECIDE_THREADS) {
+    for (uint32_t i = threadIdx.x; i < len; i += NT) {
         const uint64_t e = list[i];
         if (e < m1) { m2 = m1; m1 = e; } else if (e < m2) m2 = e;
         hmax = max(hmax, (uint32_t)(e >> 32));
     }
-    s1[threadIdx.x] = m1; s2[threadIdx.x] = m2; sh[threadIdx.x] = hmax;
-    __syncthreads();
-    for (int stp = 1; stp < DECIDE_THREADS; stp <<= 1) {
-        if ((threadIdx.x & (2 * stp - 1)) == 0) {
-            const uint64_t a1 = s1[threadIdx.x], a2 = s2[threadIdx.x], b1 = s1[threadIdx.x + stp], b2 = s2[threadIdx.x + stp];
-            s1[threadIdx.x] = min(a1, b1);
-            s2[threadIdx.x] = min(max(a1, b1), min(a2, b2));
-            sh[threadIdx.x] = max(sh[threadIdx.x], sh[threadIdx.x + stp]);
-        }
-        __syncthreads();
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t b1 = __shfl_xor(m1, off), b2 = __shfl_xor(m2, off);
+        min2_combine(m1, m2, b1, b2);
+        hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
     }
+    if ((threadIdx.x & 63) == 0) { s1[threadIdx.x >> 6] = m1; s2[threadIdx.x >> 6] = m2; sh[threadIdx.x >> 6] = hmax; }
+    __syncthreads();
     m1 = s1[0]; m2 = s2[0]; hmax = sh[0];
+    for (int k = 1; k < NT / 64; k++) { min2_combine(m1, m2, s1[k], s2[k]); hmax = max(hmax, sh[k]); }
     const uint32_t h1 = (uint32_t)(m1 >> 32);
     const uint32_t ws = V.C > 4096 ? V.C - 4096 : 0;
     // three carries in parallel, one per wave
@@ -2150,7 +2157,171 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
                                                                   uint32_t tie_cap, HomeView V, MergeLog *log, int dyn) {
     if (tie_skip(st, dyn)) return;
     const uint32_t total = st->tie_len;
-    decide_body(st, tie_list, min(total, tie_cap), total, V, log, dyn);
+    decide_body<DECIDE_THREADS>(st, tie_list, min(total, tie_cap), total, V, log, dyn);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused end of merge X + start of merge X+1 (batch mode): one launch instead of select, collect,
+// refresh and decide. Blocks [0, sel_blocks) run the hot-list argmax and keep the keys at their
+// block's max; blocks [sel_blocks, grid) refresh one dirty home super-block each (when a home
+// histogram is kept). The last block to take the ticket (release / acquire at agent scope,
+// cdna_hip_programming.md §6 G16 counter form) reduces the argmax, rolls the merge, evaluates the
+// start of merge X+1 and, on a tie, gathers the tied keys for zbpe_tie_decide (the next launch:
+// the decision's carry code needs 256 VGPRs, more than a 1024-thread block may hold).
+// ------------------------------------------------------------------------------------------
+constexpr int NEXT_THREADS = 1024;
+constexpr int NEXT_CAND = 64;          // keys kept per argmax block at the block's max
+constexpr int NEXT_MAX_SEL = 1024;     // argmax blocks (the reducer keeps one LDS entry per block)
+struct NextArgs {
+    BeginArgs B;          // merge X + 1 (B.X < x_end)
+    uint32_t x_end;       // vocab size: no merge starts at x_end
+    HomeView V;           // V.C == 0: no home histogram, no refresh blocks
+    uint64_t *tie_list;
+    uint32_t tie_cap;
+    uint32_t sel_blocks;
+    uint32_t *cand;       // [sel_blocks][NEXT_CAND]
+    const Boundary *bnd;  // multi-GPU: boundary records (the stream's last pair on ties)
+    int world;
+};
+// every thread of the block calls it after its last global store of the phase; true in the last block
+__device__ inline bool block_ticket_last(uint32_t *ticket, uint32_t nblocks, uint32_t *s_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = t == nblocks - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *s_flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+__device__ inline MaxRec block_max(MaxRec r, MaxRec *sm) {
+    r = wave_max(r);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = r;
+    __syncthreads();
+    MaxRec q = sm[0];
+    for (uint32_t w = 1; w < blockDim.x / 64; w++) q = max_combine(q, sm[w]);
+    __syncthreads();
+    return q;
+}
+__global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevState *st, MaxRec *__restrict__ partial,
+                                                                 const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
+                                                                 uint32_t X, NextArgs N) {
+    if (st->halt) return;
+    __shared__ MaxRec sm[NEXT_THREADS / WAVE];
+    __shared__ uint32_t s_flag, s_nc, s_h, s_tie, s_len, s_ntb, s_ovf;
+    __shared__ uint32_t s_key[NEXT_CAND];
+    __shared__ uint32_t s_pc[NEXT_MAX_SEL], s_pt[NEXT_MAX_SEL];
+    const uint32_t tid = threadIdx.x;
+    if (blockIdx.x < N.sel_blocks) {
+        const uint32_t G = N.sel_blocks * NEXT_THREADS;
+        for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += G) delta[t] = 0;
+        const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
+        MaxRec r{0, 0, NO_ID};
+        uint32_t id0 = NO_ID, nmine = 0;
+        for (uint32_t i = blockIdx.x * NEXT_THREADS + tid; i < nh; i += G) {
+            const uint32_t id = T.hot[i], c = T.id_cnt[id];
+            if (c >= theta && c) r = max_combine(r, MaxRec{c, 1u, id});
+            if (!nmine++) id0 = id;
+        }
+        if (tid == 0) s_nc = 0;
+        const MaxRec R = block_max(r, sm);
+        // the block's keys at its max (usually one hot entry per thread: no second pass)
+        if (R.cnt && r.cnt == R.cnt) {
+            if (nmine == 1) {
+                const uint32_t j = atomicAdd(&s_nc, 1u);
+                if (j < NEXT_CAND) s_key[j] = T.id_key[id0];
+            } else {
+                for (uint32_t i = blockIdx.x * NEXT_THREADS + tid; i < nh; i += G) {
+                    const uint32_t id = T.hot[i];
+                    if (T.id_cnt[id] == R.cnt) {
+                        const uint32_t j = atomicAdd(&s_nc, 1u);
+                        if (j < NEXT_CAND) s_key[j] = T.id_key[id];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < min(s_nc, (uint32_t)NEXT_CAND)) N.cand[blockIdx.x * NEXT_CAND + tid] = s_key[tid];
+        if (tid == 0) partial[blockIdx.x] = MaxRec{R.cnt, R.cnt ? s_nc : 0u, R.id};
+    } else if (N.V.C) {
+        refresh_super(T, blockIdx.x - N.sel_blocks, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), false);
+    }
+    if (!block_ticket_last(&st->ticket, gridDim.x, &s_flag)) return;
+    // ---- the last block: argmax, roll of merge X -------------------------------------------------
+    MaxRec q{0, 0, NO_ID};
+    for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
+        const MaxRec p = partial[b];
+        s_pc[b] = p.cnt;
+        s_pt[b] = p.ties;
+        q = max_combine(q, p);
+    }
+    const MaxRec Q = block_max(q, sm);  // (its barriers also publish s_pc / s_pt)
+    if (tid == 0) {
+        select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world);
+        s_h = HALT_DONE;
+        s_tie = 0;
+        if (N.B.X < N.x_end) {
+            bool tie;
+            const uint32_t h = merge_begin_eval(T, st, N.B, &tie);
+            merge_begin_commit(st, N.B, h, tie);
+            s_h = h;
+            s_tie = tie ? 1u : 0u;
+        }
+        s_len = 0;
+        s_ovf = 0;
+    }
+    __syncthreads();
+    if (s_h || !s_tie) return;
+    // ---- merge X+1 ties: gather the keys of the blocks whose max is the top count ----------------
+    const uint32_t top = Q.cnt, total = Q.ties;
+    for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
+        if (s_pc[b] == top) {
+            if (s_pt[b] > NEXT_CAND) atomicOr(&s_ovf, 1u);
+            atomicAdd(&s_len, s_pt[b]);
+        }
+    }
+    __syncthreads();
+    if (s_ovf || s_len != total || total > N.tie_cap) {  // a block kept too few keys: the host path decides
+        if (tid == 0) { st->halt = HALT_TIE; st->halt_at = N.B.X; }
+        return;
+    }
+    // tied blocks in block order and the exclusive offsets of their keys (wave 0, 64 blocks per step)
+    __shared__ uint32_t s_tb[NEXT_MAX_SEL], s_to[NEXT_MAX_SEL + 1];
+    if (tid < 64) {
+        uint32_t k = 0, o = 0;
+        for (uint32_t b0 = 0; b0 < N.sel_blocks; b0 += 64) {
+            const uint32_t b = b0 + tid;
+            const bool t = b < N.sel_blocks && s_pc[b] == top;
+            const uint32_t c = t ? s_pt[b] : 0u;
+            const uint64_t m = __ballot(t);
+            const uint32_t below = (uint32_t)__popcll(m & ((1ull << tid) - 1ull));
+            const uint32_t inc = wave_incl_scan(c);
+            if (t) { s_tb[k + below] = b; s_to[k + below] = o + inc - c; }
+            k += (uint32_t)__popcll(m);
+            o += (uint32_t)__shfl((int)inc, 63);
+        }
+        if (tid == 0) { s_ntb = k; s_to[k] = o; }
+    }
+    __syncthreads();
+    const uint32_t ntb = s_ntb;
+    const uint32_t cap_mask = N.V.C - 1;
+    for (uint32_t e = tid; e < total; e += NEXT_THREADS) {
+        uint32_t lo = 0, hi = ntb;  // the tied block holding key e: s_to[lo] <= e < s_to[lo + 1]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_to[mid] <= e) lo = mid; else hi = mid;
+        }
+        const uint32_t key = N.cand[s_tb[lo] * NEXT_CAND + (e - s_to[lo])];
+        N.tie_list[e] = ((uint64_t)(zig_pair_hash(key) & cap_mask) << 32) | key;
+    }
+    if (tid == 0) st->tie_len = total;  // zbpe_tie_decide (the next launch) decides from the list
 }
 
 // rebuild the home histogram for a new Zig capacity
