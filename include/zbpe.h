@@ -63,6 +63,7 @@ typedef struct zbpe_stats {
     uint64_t scan_timed_alg_bytes;
     uint64_t list_scans;      /* pair scans that walked a token occurrence list instead of the stream */
     uint64_t list_builds;     /* occurrence-list rebuilds (after compactions) */
+    uint64_t replications;    /* multi-GPU: 1 once the ranks gathered the whole stream for the late phase */
 } zbpe_stats;
 
 /* Create a single-GPU context on HIP device `device`. */
@@ -70,7 +71,9 @@ zbpe_status zbpe_create(int device, zbpe_ctx **out);
 
 /* Multi-GPU: one process per GPU. Rank 0 calls zbpe_comm_unique_id() and broadcasts the 128 bytes
  * (e.g. with torch.distributed); every rank then calls zbpe_create_dist. The token stream is split
- * into `world` contiguous shards; pair-count deltas are summed with an RCCL all-reduce each merge. */
+ * into `world` contiguous shards; pair-count deltas are summed with an RCCL all-reduce each merge
+ * while scans stream the shards. When the occurrence lists take over, the ranks all-gather the
+ * whole stream once and finish as replicas (no per-merge collective; option "replicate_late"). */
 zbpe_status zbpe_comm_unique_id(void *out128);
 zbpe_status zbpe_create_dist(int device, int rank, int world, const void *unique_id128, zbpe_ctx **out);
 

@@ -26,12 +26,18 @@ CASES = [
     dict(text=b"abababababababababababab", vocab=300),
     dict(text=b"hello world hello", vocab=300),
     dict(text=b"ab", vocab=300),
+    # occurrence lists from the first compaction: the ranks gather the stream and finish as replicas
+    dict(kind="words_utf8", seed=65, n=200000, vocab=900, options={"list_start": 0}, replicated=True),
+    dict(kind="runs", seed=66, n=60000, vocab=500, options={"list_start": 0}, replicated=True),
+    # the same without the late-phase replication (every merge sharded to the end)
+    dict(kind="words_utf8", seed=65, n=200000, vocab=900, options={"list_start": 0, "replicate_late": 0}),
 ]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("case", CASES, ids=lambda c: c.get("kind", "text") + str(c.get("n", len(c.get("text", b"")))))
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c.get("kind", "text") + str(c.get("n", len(c.get("text", b""))))
+                         + "".join(f"-{k}{v}" for k, v in c.get("options", {}).items()))
 def test_sharded_training_matches_oracle(world, case):
     text = case["text"] if "text" in case else zbpe.synth_corpus(case["kind"], case["seed"], case["n"])
     ref = O.train(text, case["vocab"])
@@ -41,6 +47,11 @@ def test_sharded_training_matches_oracle(world, case):
         assert m == ref.merges.tolist(), f"rank {r}"
         assert c == ref.counts.tolist(), f"rank {r}"
     assert out[0][3]["final_tokens"] == len(ref.tokens)
+    # sum over merges of the stream length (the oracle also counts a final early-stop pass, n <= 1)
+    assert 0 <= ref.stats.pair_tokens - out[0][3]["sum_tokens"] <= 1
+    if case.get("replicated"):
+        assert all(out[r][3]["replications"] == 1 for r in range(world))
+
 
 
 @pytest.mark.gpu

@@ -56,7 +56,7 @@ void Engine::release() {
     f(T.ht); f(T.id_key); f(T.id_cnt);
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_sizes);
     for (auto &e : bev) if (e) (void)hipEventDestroy(e);
     bev.clear();
     if (h_st) (void)hipHostFree(h_st);
@@ -69,7 +69,7 @@ void Engine::release() {
     if (h_bnd) (void)hipHostFree(h_bnd);
     h_bnd = nullptr;
     comm.reset();
-    d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr; d_cand = nullptr;
+    d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr; d_cand = nullptr; d_sizes = nullptr; sizes_cap = 0;
     d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
     d_summ = nullptr; d_count_hist = nullptr; h_count_hist = nullptr; hot_cap_alloc = home_words_cap = 0; home_slots = 0;
     dirty_bits_cap = 0; d_sup = nullptr; sup_cap = 0; d_pres = nullptr; pres_cap = 0;
@@ -260,6 +260,7 @@ zbpe_status Engine::compact_train() {
     const bool want = list_mode && pres_vp <= PRES_MAX_VP && (uint64_t)n_slots < 0xF0000000ull &&
                       (lists_on || list_start == 0 || (uint64_t)h_st->top_count * list_start < (uint64_t)n_live);
     if (want) {
+        if (dist() && replicate_late) CHECK(replicate());
         CHECK(build_lists());
     } else {
         HIP_OK(hipMemsetAsync(&d_st->arena_top, 0, 4, stream));
@@ -271,6 +272,52 @@ zbpe_status Engine::compact_train() {
     HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
     run.ev_replace += ms * 1e-3;
     return sync_state();
+}
+
+// Multi-GPU, late phase: gather the compacted shards into the whole stream on every rank (one
+// all-gather of max-shard-sized pieces, padded with holes, then a compaction) and continue as
+// replicas. The pair table is already identical on every rank, so from here each rank computes
+// the same merges with no collective; the halo is empty and positions are global.
+zbpe_status Engine::replicate() {
+    CHECK(ensure(&d_sizes, sizes_cap, 2 * (size_t)world + 2, "shard sizes"));
+    const uint32_t mine = (uint32_t)n_live;
+    HIP_OK(hipMemcpyAsync(d_sizes, &mine, 4, hipMemcpyHostToDevice, stream));
+    if (!comm->allgather(d_sizes, d_sizes + world, 4, stream)) return fail(ZBPE_COMM_ERROR, "all-gather of shard sizes failed");
+    std::vector<uint32_t> sz(world);
+    HIP_OK(hipMemcpyAsync(sz.data(), d_sizes + world, 4 * (size_t)world, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    uint64_t total = 0, M = 0;
+    for (uint32_t v : sz) { total += v; M = std::max<uint64_t>(M, v); }
+    M = round_up(std::max<uint64_t>(M, 1), 64);  // whole 16-B vectors per piece
+    const size_t need = round_up((size_t)M * world + 1, 64) + 64;
+    if (need > 0xFFFFFFF0u) return fail(ZBPE_INVALID_ARGUMENT, "replicated stream of %zu slots exceeds 2^32", need);
+    // this rank's piece: its live tokens, then holes up to M (the shard buffer holds >= M + 64 slots)
+    if ((size_t)M > std::min(tok_cap0, tok_cap1)) return fail(ZBPE_INTERNAL, "shard buffer smaller than the gather piece");
+    zbpe_fill_u16<<<64, 256, 0, stream>>>(d_tok[cur], n_live, (int64_t)M, HOLE);
+    LAUNCH_OK();
+    uint16_t *full = nullptr;
+    if (hipMalloc(&full, need * 2) != hipSuccess) { (void)hipGetLastError(); return fail(ZBPE_OUT_OF_MEMORY, "replicated stream (%zu slots)", need); }
+    zbpe_fill_u16<<<256, 256, 0, stream>>>(full, 0, (int64_t)need, HOLE);
+    LAUNCH_OK();
+    if (!comm->allgather(d_tok[cur], full, (size_t)M * 2, stream)) { (void)hipFree(full); return fail(ZBPE_COMM_ERROR, "all-gather of the shards failed"); }
+    // the gathered stream becomes the current buffer; the compaction target grows to match
+    (void)hipFree(d_tok[cur]);
+    d_tok[cur] = full;
+    (cur == 0 ? tok_cap0 : tok_cap1) = need;
+    CHECK(ensure(&d_tok[cur ^ 1], cur == 0 ? tok_cap1 : tok_cap0, need, "token stream (compaction buffer)"));
+    replicated = true;
+    n_slots = (int64_t)M * world;
+    n_live = (int64_t)total;
+    const long long lt = (long long)total;
+    HIP_OK(hipMemcpyAsync(&d_st->live_tokens, &lt, sizeof(lt), hipMemcpyHostToDevice, stream));
+    halo = halo_empty();
+    shard_offset = 0;
+    CHECK(compact());  // squeeze the padding: the stream is the whole corpus's, in shard order
+    // the occurrence arena was sized for the shard: lists of the whole stream + later records
+    // (its contents are rebuilt by build_lists right after)
+    CHECK(ensure(&d_lists, lists_cap, std::min<size_t>(0xFFFFFFF0u, total + total / 2 + (16u << 20)), "occurrence arena"));
+    stats.replications++;
+    return ZBPE_OK;
 }
 
 // occurrence lists of the compacted stream (no holes): counting sort of positions by token
@@ -349,7 +396,7 @@ zbpe_status Engine::launch_argmax(uint32_t X, int roll) {
     if (hot_stale) CHECK(rebuild_hot());
     const int blocks = argmax_blocks(X);
     zbpe_select<<<blocks, ARGMAX_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], n_slots, d_delta, X, roll, d_bnd_all,
-                                                       world);
+                                                       dist() ? world : 1);
     LAUNCH_OK();
     return ZBPE_OK;
 }
@@ -468,7 +515,7 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     std::vector<LiveRec> recs(g);
     HIP_OK(hipMemcpyAsync(recs.data(), d_gather, (size_t)g * sizeof(LiveRec), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
-    if (world > 1) {
+    if (dist()) {
         // every rank holds the same live keys: in key order the local first positions line up, so one
         // all-reduce(min) gives the global first occurrence of each pair
         std::sort(recs.begin(), recs.end(), [](const LiveRec &x, const LiveRec &y) { return x.key < y.key; });
@@ -598,7 +645,7 @@ void Engine::halo_from_boundaries() {
 }
 
 zbpe_status Engine::comm_sum(uint32_t *d, size_t n) {
-    if (world > 1 && n && !comm->allreduce_u32(d, n, COMM_SUM_U32, stream))
+    if (dist() && n && !comm->allreduce_u32(d, n, COMM_SUM_U32, stream))
         return fail(ZBPE_COMM_ERROR, "all-reduce of %zu u32 failed", n);
     return ZBPE_OK;
 }
@@ -638,6 +685,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     }
     home_slots = 0;
     T.home_mask = 0;
+    replicated = false;
+    sum_tokens_rep = 0;
     if (T.home_cnt) { (void)hipFree(T.home_cnt); T.home_cnt = nullptr; home_words_cap = 0; }
     if (T.home_dirty) { (void)hipFree(T.home_dirty); T.home_dirty = nullptr; dirty_bits_cap = 0; }
     hot_stale = true;
@@ -714,7 +763,9 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     stats.replace_pair_s = ev_replace;
     stats.final_tokens = (uint64_t)n_live;
     if (world > 1) {  // stream lengths are per shard: sum them (scan bytes stay per rank, like scan time)
-        uint64_t v[2] = {stats.final_tokens, stats.sum_tokens};
+        // the replicated phase counted the whole stream on every rank: rank 0 contributes it once
+        uint64_t v[2] = {replicated ? (rank == 0 ? stats.final_tokens : 0) : stats.final_tokens,
+                         stats.sum_tokens - sum_tokens_rep + (rank == 0 ? sum_tokens_rep : 0)};
         uint32_t w[8] = {0};
         for (int i = 0; i < 2; i++) {  // exact u64 sums from 16-bit limbs (<= 2^16 ranks)
             w[4 * i] = (uint32_t)(v[i] & 0xFFFF);
@@ -724,7 +775,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         }
         uint32_t *d_w = d_delta + DELTA_WORDS - 16;
         HIP_OK(hipMemcpyAsync(d_w, w, 32, hipMemcpyHostToDevice, stream));
-        CHECK(comm_sum(d_w, 8));
+        if (!comm->allreduce_u32(d_w, 8, COMM_SUM_U32, stream)) return fail(ZBPE_COMM_ERROR, "all-reduce of the stream statistics failed");
         HIP_OK(hipMemcpyAsync(w, d_w, 32, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
         for (int i = 0; i < 2; i++)
@@ -758,7 +809,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         (uint64_t)h_st->arena_top + (uint64_t)K * top0 > lists_cap)
         CHECK(compact_train());
     CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
-    if (world > 1) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
+    if (dist()) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
     const uint64_t C = home_slots;
     const uint32_t nb = (uint32_t)((C + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
     const HomeView V{T.home_cnt, d_summ, d_sup, (uint32_t)C, nb, nsb};
@@ -785,7 +836,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         }
         if (timed) HIP_OK(hipEventRecord(bev[4 * i + 1], stream));
         ScanArgs A{d_tok[cur], slots, 0, 0, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
-                   pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 1, world > 1 ? d_halo : nullptr,
+                   pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 1, dist() ? d_halo : nullptr,
                    lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log};
         // a batch that follows one of list scans only launches a smaller grid (fewer idle workgroups
         // to dispatch); a stream scan still completes on it, only slower
@@ -793,7 +844,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         if (timed) HIP_OK(hipEventRecord(bev[4 * i + 2], stream));
         CHECK(comm_sum(d_delta, 2ull * X + 2));
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
-                      1, world > 1 ? d_halo : nullptr, 1};
+                      1, dist() ? d_halo : nullptr, 1};
         if (!replace_split) {
             zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
         } else {  // profiling: apply and count update as two launches
@@ -802,7 +853,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             zbpe_replace<<<update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
         }
         LAUNCH_OK();
-        if (world > 1) {
+        if (dist()) {
             zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], slots, 0, d_bnd_mine, d_st);
             LAUNCH_OK();
             if (!comm->allgather(d_bnd_mine, d_bnd_all, sizeof(Boundary), stream))
@@ -815,7 +866,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             const uint64_t work = std::max<uint64_t>(T.hot_cap / 4, 2ull * X);
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)lists_cap, d_log}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
-                       d_bnd_all, world};
+                       d_bnd_all, dist() ? world : 1};
             zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, d_delta, X, N);
             LAUNCH_OK();
             if (C && X + 1 < run.vocab) {  // returns at once unless merge X+1 is a tie the select gathered
@@ -827,7 +878,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         }
         if (timed) HIP_OK(hipEventRecord(bev[4 * i + 3], stream));
     }
-    if (world > 1) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
+    if (dist()) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
     CHECK(sync_state());
     const double wall = now_s() - t0;
     batches++;
@@ -850,6 +901,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         if (run.out_counts) run.out_counts[run.merges] = L.count;
         run.merges++;
         stats.sum_tokens += L.live;
+        if (replicated) sum_tokens_rep += L.live;
         stats.scan_alg_bytes += 2ull * L.live;
         stats.scan_launches++;
         stats.sort_pairs_calls++;
@@ -882,7 +934,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     for (uint32_t i = 0; i < m; i++) nlist += h_log[X0 - 256 + i].mode;
     list_streak = m > 0 && nlist == m;
     n_live = h_st->live_tokens;
-    if (world > 1) halo_from_boundaries();
+    if (dist()) halo_from_boundaries();
     *done = m;
     return ZBPE_OK;
 }
@@ -908,6 +960,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     if (run.out_counts) run.out_counts[run.merges] = top;
     run.merges++;
     stats.sum_tokens += (uint64_t)n_live;
+    if (replicated) sum_tokens_rep += (uint64_t)n_live;
 
     CHECK(maybe_grow_tables(X, 1));
     const bool self = a == b;
@@ -931,14 +984,14 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         CHECK(ensure(&d_carry, carry_cap, ntiles, "self carry"));
         zbpe_self_tiles<<<ntiles, SELF_THREADS, 0, stream>>>(d_tok[cur], n_slots, a, d_tile_fn);
         LAUNCH_OK();
-        if (world > 1) {  // parity of the run of a's entering this shard from the ranks to the left
+        if (dist()) {  // parity of the run of a's entering this shard from the ranks to the left
             zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, nullptr, d_shard_fn);
             LAUNCH_OK();
             if (!comm->allgather(d_shard_fn, d_fns_all, 4, stream)) return fail(ZBPE_COMM_ERROR, "all-gather of run carries failed");
             zbpe_self_x0<<<1, 1, 0, stream>>>(d_fns_all, rank, d_x0);
             LAUNCH_OK();
         }
-        zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, world > 1 ? d_x0 : nullptr, nullptr);
+        zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, dist() ? d_x0 : nullptr, nullptr);
         LAUNCH_OK();
         zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
         LAUNCH_OK();
@@ -950,11 +1003,11 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     {
         const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top / 256 + 1);
         ReplaceArgs R{d_tok[cur], n_slots, d_lists, (uint32_t)lists_cap, left, right, tail, a, b, X, key, ab, halo,
-                      (self && world > 1) ? d_x0 : nullptr, 0, nullptr, 1};
+                      (self && dist()) ? d_x0 : nullptr, 0, nullptr, 1};
         zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
         LAUNCH_OK();
     }
-    if (world > 1) {  // boundary tokens of every shard for the next merge's halos
+    if (dist()) {  // boundary tokens of every shard for the next merge's halos
         zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, n_live, d_bnd_mine, nullptr);
         LAUNCH_OK();
         if (!comm->allgather(d_bnd_mine, d_bnd_all, sizeof(Boundary), stream))
@@ -963,7 +1016,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     HIP_OK(hipEventRecord(ev[2], stream));
     // ---- select for the next merge (also clears the deltas, rolls the counters) ----------------------
     CHECK(launch_argmax(X, 1));
-    if (world > 1) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
+    if (dist()) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipEventRecord(ev[3], stream));
     CHECK(sync_state());
     CHECK(select_ready());
@@ -992,7 +1045,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         stats.count_pairs_calls++;
         stats.replace_pair_calls++;
     }
-    if (world > 1) halo_from_boundaries();
+    if (dist()) halo_from_boundaries();
     if (debug_checks) {
         uint64_t bad = 0;
         uint32_t info[3] = {0, 0, 0};
@@ -1029,7 +1082,7 @@ zbpe_status Engine::recount_check(uint64_t *mismatches, uint32_t *first_bad_key)
     ScanArgs A{d_tok[cur], n_slots, 0, 0, nullptr, nullptr, d_st, nullptr, 0, 0, nullptr, nullptr, halo};
     zbpe_recount<<<2048, 256, 0, stream>>>(A, T, d_recount, d_st);
     LAUNCH_OK();
-    if (world == 1) {
+    if (!dist()) {
         zbpe_recount_compare<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_recount, d_st);
         LAUNCH_OK();
         CHECK(sync_state());

@@ -46,6 +46,14 @@ struct Engine {
     int rank = 0, world = 1;
     std::unique_ptr<Comm> comm;
     bool sharded = false;
+    // multi-GPU, late phase: once the occurrence lists take over (scans stop streaming the shards),
+    // every rank gathers the whole stream and runs the remaining merges as a replica, with no
+    // per-merge collective (option "replicate_late")
+    bool replicate_late = true, replicated = false;
+    uint64_t sum_tokens_rep = 0;     // stats.sum_tokens accumulated while replicated (counted once)
+    uint32_t *d_sizes = nullptr;     // [2 * world + 2] live-token counts of the shards
+    size_t sizes_cap = 0;
+    bool dist() const { return world > 1 && !replicated; }
     uint32_t shard_offset = 0;  // global position of the shard's first byte
     int next_byte = -1;         // first byte of the next shard (-1: none)
     Halo halo0{}, halo{};
@@ -160,6 +168,7 @@ struct Engine {
     zbpe_status compact();
     zbpe_status compact_train();
     zbpe_status build_lists();
+    zbpe_status replicate();
     zbpe_status launch_argmax(uint32_t X, int roll);
     int argmax_blocks(uint32_t X) const;
     int scan_grid(int64_t slots) const;

@@ -615,6 +615,8 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
 // listed; entries overwritten since (merged or turned into holes) fail the token check.
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
                                                                      uint32_t len) {
+    // blocks past the list leave before touching LDS (the grid is sized for a stream scan)
+    if (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len) return;
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
     __shared__ uint32_t s_any;
     for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }

@@ -131,6 +131,7 @@ class Stats(ctypes.Structure):
         ("scan_timed_alg_bytes", ctypes.c_uint64),
         ("list_scans", ctypes.c_uint64),
         ("list_builds", ctypes.c_uint64),
+        ("replications", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
