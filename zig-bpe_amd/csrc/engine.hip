@@ -100,7 +100,7 @@ zbpe_status Engine::init(int dev) {
     bev.resize(4 * MAX_BATCH);
     for (auto &e : bev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no L2 writeback
     HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
-    HIP_OK(hipMalloc(&d_cand, (size_t)NEXT_MAX_SEL * NEXT_CAND * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_cand, ((size_t)NEXT_MAX_SEL * (NEXT_CAND + 1) + 64) * sizeof(uint32_t)));  // keys | pkey | lastpair
     HIP_OK(hipMalloc(&d_count_hist, COUNT_BINS * sizeof(uint32_t)));
     HIP_OK(hipHostMalloc((void **)&h_count_hist, COUNT_BINS * sizeof(uint32_t), hipHostMallocDefault));
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
@@ -142,6 +142,7 @@ zbpe_status Engine::upload(const uint8_t *text, size_t n, bool shard) {
     if (e > s) HIP_OK(hipMemcpyAsync(d_text, text + s, e - s, hipMemcpyHostToDevice, stream));
     HIP_OK(hipStreamSynchronize(stream));
     n_text = e - s;
+    n_total = n;
     shard_offset = (uint32_t)s;
     next_byte = e < n && shard ? (int)text[e] : -1;
     Halo H = halo_empty();
@@ -259,8 +260,7 @@ zbpe_status Engine::compact_train() {
     CHECK(compact());
     const bool want = list_mode && pres_vp <= PRES_MAX_VP && (uint64_t)n_slots < 0xF0000000ull &&
                       (lists_on || list_start == 0 || (uint64_t)h_st->top_count * list_start < (uint64_t)n_live);
-    if (want) {
-        if (dist() && replicate_late) CHECK(replicate());
+    if (want && !(dist() && replicate_late)) {  // sharded: lists come with the replication (run_batch)
         CHECK(build_lists());
     } else {
         HIP_OK(hipMemsetAsync(&d_st->arena_top, 0, 4, stream));
@@ -687,6 +687,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     T.home_mask = 0;
     replicated = false;
     sum_tokens_rep = 0;
+    global_live = sharded ? n_total : n;
     if (T.home_cnt) { (void)hipFree(T.home_cnt); T.home_cnt = nullptr; home_words_cap = 0; }
     if (T.home_dirty) { (void)hipFree(T.home_dirty); T.home_dirty = nullptr; dirty_bits_cap = 0; }
     hot_stale = true;
@@ -801,6 +802,22 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     const uint32_t K = std::min<uint32_t>(merge_batch, run.vocab - X0);
     *done = 0;
     *halted = false;
+    // multi-GPU: once pair counts are small against the stream (the single-GPU criterion for
+    // occurrence lists, on replicated quantities so every rank decides alike), gather the stream
+    // and continue as replicas
+    if (dist() && replicate_late && list_mode && pres_vp <= PRES_MAX_VP &&
+        (uint64_t)h_st->top_count * list_start * (uint64_t)world < global_live) {
+        HIP_OK(hipEventRecord(ev[3], stream));
+        CHECK(compact());  // this shard's live tokens, contiguous
+        CHECK(replicate());
+        CHECK(build_lists());
+        HIP_OK(hipEventRecord(ev[4], stream));
+        HIP_OK(hipEventSynchronize(ev[4]));
+        float ms;
+        HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
+        run.ev_replace += ms * 1e-3;
+        CHECK(sync_state());
+    }
     // headroom for K merges: ids, occurrence records (counts never grow), tie list; compaction
     CHECK(maybe_grow_tables(X0, K));
     if (hot_stale) CHECK(rebuild_hot());  // a table rebuild renumbered the ids the tie kernels read
@@ -863,10 +880,14 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         }
         if (fused_select) {
             if (hot_stale) CHECK(rebuild_hot());
-            const uint64_t work = std::max<uint64_t>(T.hot_cap / 4, 2ull * X);
+            // about four hot entries per thread (the list grows by the new ids of the batch), and
+            // the delta words to clear
+            const uint64_t hot_est = std::min<uint64_t>(T.hot_cap, (uint64_t)h_st->hot_len + (uint64_t)K * 1024 + 4096);
+            const uint64_t work = std::max<uint64_t>(hot_est / 4, 2ull * X / 4);
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)lists_cap, d_log}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
-                       d_bnd_all, dist() ? world : 1};
+                       d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
+                       dist() ? world : 1};
             zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, d_delta, X, N);
             LAUNCH_OK();
             if (C && X + 1 < run.vocab) {  // returns at once unless merge X+1 is a tie the select gathered
@@ -900,6 +921,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         run.out_triples[3 * run.merges + 2] = (uint16_t)X;
         if (run.out_counts) run.out_counts[run.merges] = L.count;
         run.merges++;
+        global_live -= L.count;  // batch merges are never self pairs: one token per occurrence
         stats.sum_tokens += L.live;
         if (replicated) sum_tokens_rep += L.live;
         stats.scan_alg_bytes += 2ull * L.live;
@@ -1055,6 +1077,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
                         X, a, b, (unsigned long long)bad, info[0] & 0xFFFF, info[0] >> 16, info[1], info[2]);
     }
     const uint32_t gocc = h_st->last_gocc;
+    global_live -= gocc;
     if (!self && gocc != top)
         return fail(ZBPE_INTERNAL, "merge %u: scan found %u occurrences of (%u,%u), count was %u", X, gocc, a, b, top);
     const uint64_t gone = h_st->last_holes;  // slots of this shard that became holes

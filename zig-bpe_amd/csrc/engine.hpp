@@ -51,6 +51,8 @@ struct Engine {
     // per-merge collective (option "replicate_late")
     bool replicate_late = true, replicated = false;
     uint64_t sum_tokens_rep = 0;     // stats.sum_tokens accumulated while replicated (counted once)
+    uint64_t n_total = 0;            // corpus bytes over all ranks
+    uint64_t global_live = 0;        // live tokens over all ranks (host-tracked from the merged counts)
     uint32_t *d_sizes = nullptr;     // [2 * world + 2] live-token counts of the shards
     size_t sizes_cap = 0;
     bool dist() const { return world > 1 && !replicated; }

@@ -596,7 +596,8 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
     const ScanArgs A = scan_args_resolve(A0);
     // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
     if (A.lists && A.a != A.b && A.st->lists_valid) {
-        const uint32_t la = A.lst_len[A.a], lb = A.lst_len[A.b];
+        // lengths and offsets in one round trip
+        const uint32_t la = A.lst_len[A.a], lb = A.lst_len[A.b], oa = A.lst_off[A.a], ob = A.lst_off[A.b];
         const bool by_b = lb < la;
         const uint32_t len = by_b ? lb : la;
         if (len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n) {
@@ -604,7 +605,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
                 A.st->scan_mode = 1;
                 if (A.log) A.log[A.X - 256].mode = 1;
             }
-            scan_list_body(A, by_b, A.lists + A.lst_off[by_b ? A.b : A.a], len);
+            scan_list_body(A, by_b, A.lists + (by_b ? ob : oa), len);
             return;
         }
     }
@@ -645,9 +646,37 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
         bool hit = false;
         uint32_t pr = 0;
         if (i < len) {
-            // the entry still holds the key token: resolve it from a cached window around it
+            // the entry's window (its 16-B vector and the neighbouring words) in one round trip; the
+            // entry counts only if it still holds the key token
             const int64_t p = L[i];
-            if (tok[p] == key) hit = resolve_candidate(A, H, p, by_b, nvec, xx, pr);
+            const int64_t vi = p >> 3;
+            const int k = (int)(p & 7);
+            const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
+            const uint32_t pw = vi > 0 ? tv[vi - 1].w : 0xffffffffu;
+            const uint4 cv = tv[vi];
+            uint32_t nx = 0xffffffffu, ny = 0xffffffffu;
+            if (vi + 1 < nvec) {
+                const uint4 nv = tv[vi + 1];
+                nx = nv.x;
+                ny = nv.y;
+            }
+            if (tok_at(cv, k) == key) {
+                if (!by_b) {
+                    pr = (uint32_t)p;
+                    hit = occ_window(A, H, vi, 1u << k, xx, pw, cv, nx, ny) != 0;
+                } else {
+                    int j = k - 1;  // the live token before p inside the vector
+                    while (j >= 0 && tok_at(cv, j) == HOLE) j--;
+                    if (j >= 0) {
+                        if (tok_at(cv, j) == A.a && occ_window(A, H, vi, 1u << j, xx, pw, cv, nx, ny)) {
+                            pr = (uint32_t)(vi * 8 + j);
+                            hit = true;
+                        }
+                    } else {
+                        hit = resolve_candidate(A, H, p, by_b, nvec, xx, pr);
+                    }
+                }
+            }
         }
         const uint64_t m = __ballot(hit);
         if (!m) continue;
@@ -1585,7 +1614,8 @@ __global__ void __launch_bounds__(256) zbpe_hot_build(Tables T, DevState *st) {
 // stream's last-pair count, and the end-of-merge resets (neighbour histograms, counters) when
 // roll != 0. One launch per merge instead of three.
 __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, const uint16_t *tok, int64_t n,
-                                     uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world);
+                                     uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world,
+                                     uint32_t key_hint = NO_ID, uint32_t lastpair_hint = NO_ID);
 __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState *st, MaxRec *__restrict__ partial,
                                                               const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
                                                               uint32_t X, int roll, const Boundary *__restrict__ bnd, int world) {
@@ -1631,13 +1661,16 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
 // the selection's state update (one thread): top pair, tie count, the stream's last pair (ties),
 // and at roll the end-of-merge bookkeeping (occurrence list of X, counters, deltas' tail)
 __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, const uint16_t *tok, int64_t n,
-                                     uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world) {
+                                     uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world,
+                                     uint32_t key_hint, uint32_t lastpair_hint) {
     {
         st->top_count = q.cnt;
         st->tie_count = q.cnt ? q.ties : 0;
         st->top_id = q.id;
-        st->top_key = q.id != NO_ID ? T.id_key[q.id] : EMPTY_KEY;
-        if (q.ties > 1) {
+        st->top_key = q.id == NO_ID ? EMPTY_KEY : key_hint != NO_ID ? key_hint : T.id_key[q.id];
+        if (q.ties > 1 && lastpair_hint != NO_ID) {
+            st->lastpair_count = lastpair_hint;
+        } else if (q.ties > 1) {
             uint32_t lt[2];  // last live token of the whole stream, then the one before
             int got = 0;
             if (world > 1) {
@@ -1980,7 +2013,20 @@ __device__ inline int64_t wave_carry_into(const HomeView &V, uint32_t s) {
     const Summ bs = bi < V.nb ? V.summ[bi] : Summ{0, 0};
     const uint32_t nsup = V.nsb - 1, per = (nsup + 63) / 64, i0 = min(nsup, lane * per), i1 = min(nsup, i0 + per);
     Summ x3{0, 0};
-    for (uint32_t i = i0; i < i1; i++) x3 = summ_cat(x3, V.sup[(sb + 1 + i) % V.nsb]);
+    if (per <= 8) {  // up to 512 super-blocks (C <= 2^27): every load issued at once
+        Summ sv[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t i = i0 + k;
+            uint32_t j = sb + 1 + i;
+            j = j >= V.nsb ? j - V.nsb : j;
+            sv[k] = i < i1 ? V.sup[j] : Summ{0, 0};
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) x3 = summ_cat(x3, sv[k]);
+    } else {
+        for (uint32_t i = i0; i < i1; i++) x3 = summ_cat(x3, V.sup[(sb + 1 + i) % V.nsb]);
+    }
     Summ x1{0, 0}, x5{0, 0};
 #pragma unroll
     for (int k = 0; k < 64; k++) {
@@ -2182,6 +2228,8 @@ struct NextArgs {
     uint32_t tie_cap;
     uint32_t sel_blocks;
     uint32_t *cand;       // [sel_blocks][NEXT_CAND]
+    uint32_t *pkey;       // [sel_blocks] key of the block's max when it is unique
+    uint32_t *lastpair;   // [1] count of the stream's last pair (one GPU)
     const Boundary *bnd;  // multi-GPU: boundary records (the stream's last pair on ties)
     int world;
 };
@@ -2225,20 +2273,49 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
         const uint32_t G = N.sel_blocks * NEXT_THREADS;
         for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += G) delta[t] = 0;
         const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
+        if (blockIdx.x == 0 && tid >= 64 && tid < 128 && N.world == 1) {
+            // wave 1 of block 0: the count of the stream's last pair (a tie needs it: Zig map capacity)
+            const uint32_t lane = tid - 64;
+            uint32_t lt[2] = {HOLE, HOLE};
+            int got = 0;
+            for (int64_t e = n; e > 0 && got < 2; e -= 64) {
+                const int64_t p = e - 1 - lane;
+                const uint32_t t = p >= 0 ? tok[p] : HOLE;
+                uint64_t live = __ballot(t != HOLE);
+                while (live && got < 2) {  // lowest lane = highest position
+                    const int l = __builtin_ctzll(live);
+                    live &= live - 1;
+                    lt[got++] = (uint32_t)__shfl((int)t, l);
+                }
+            }
+            if (lane == 0) N.lastpair[0] = got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0u;
+        }
+        // four hot entries per thread per step, every load of a step issued together
         MaxRec r{0, 0, NO_ID};
-        uint32_t id0 = NO_ID, nmine = 0;
-        for (uint32_t i = blockIdx.x * NEXT_THREADS + tid; i < nh; i += G) {
-            const uint32_t id = T.hot[i], c = T.id_cnt[id];
-            if (c >= theta && c) r = max_combine(r, MaxRec{c, 1u, id});
-            if (!nmine++) id0 = id;
+        uint32_t ids[4] = {NO_ID, NO_ID, NO_ID, NO_ID}, cs[4] = {0, 0, 0, 0};
+        bool one_step = true;
+        for (uint32_t i0 = blockIdx.x * NEXT_THREADS + tid; i0 < nh; i0 += 4 * G) {
+            one_step = i0 == blockIdx.x * NEXT_THREADS + tid;
+#pragma unroll
+            for (int u = 0; u < 4; u++) ids[u] = i0 + u * G < nh ? T.hot[i0 + u * G] : NO_ID;
+#pragma unroll
+            for (int u = 0; u < 4; u++) cs[u] = ids[u] != NO_ID ? T.id_cnt[ids[u]] : 0u;
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (cs[u] >= theta && cs[u]) r = max_combine(r, MaxRec{cs[u], 1u, ids[u]});
         }
         if (tid == 0) s_nc = 0;
         const MaxRec R = block_max(r, sm);
-        // the block's keys at its max (usually one hot entry per thread: no second pass)
+        // the block's keys at its max (from the registers when the thread's entries fit one step)
         if (R.cnt && r.cnt == R.cnt) {
-            if (nmine == 1) {
-                const uint32_t j = atomicAdd(&s_nc, 1u);
-                if (j < NEXT_CAND) s_key[j] = T.id_key[id0];
+            if (one_step && 4 * G >= nh) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (ids[u] != NO_ID && cs[u] == R.cnt) {
+                        const uint32_t j = atomicAdd(&s_nc, 1u);
+                        if (j < NEXT_CAND) s_key[j] = T.id_key[ids[u]];
+                    }
+                }
             } else {
                 for (uint32_t i = blockIdx.x * NEXT_THREADS + tid; i < nh; i += G) {
                     const uint32_t id = T.hot[i];
@@ -2251,7 +2328,10 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
         }
         __syncthreads();
         if (tid < min(s_nc, (uint32_t)NEXT_CAND)) N.cand[blockIdx.x * NEXT_CAND + tid] = s_key[tid];
-        if (tid == 0) partial[blockIdx.x] = MaxRec{R.cnt, R.cnt ? s_nc : 0u, R.id};
+        if (tid == 0) {
+            partial[blockIdx.x] = MaxRec{R.cnt, R.cnt ? s_nc : 0u, R.id};
+            N.pkey[blockIdx.x] = s_nc == 1 ? s_key[0] : NO_ID;  // the key of a block's unique max
+        }
     } else if (N.V.C) {
         refresh_super(T, blockIdx.x - N.sel_blocks, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), false);
     }
@@ -2265,8 +2345,14 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
         q = max_combine(q, p);
     }
     const MaxRec Q = block_max(q, sm);  // (its barriers also publish s_pc / s_pt)
+    if (Q.ties == 1 && Q.cnt) {  // the unique max: its block kept its key
+        for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS)
+            if (s_pc[b] == Q.cnt) s_key[0] = N.pkey[b];
+    }
+    __syncthreads();
     if (tid == 0) {
-        select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world);
+        select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, Q.ties == 1 && Q.cnt ? s_key[0] : NO_ID,
+                      N.world == 1 ? N.lastpair[0] : NO_ID);
         s_h = HALT_DONE;
         s_tie = 0;
         if (N.B.X < N.x_end) {
@@ -2290,8 +2376,33 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
         }
     }
     __syncthreads();
-    if (s_ovf || s_len != total || total > N.tie_cap) {  // a block kept too few keys: the host path decides
+    if (total > N.tie_cap) {  // the host path decides (replicated state: every rank takes it)
         if (tid == 0) { st->halt = HALT_TIE; st->halt_at = N.B.X; }
+        return;
+    }
+    const uint32_t cap_mask = N.V.C - 1;
+    if (s_ovf || s_len != total) {
+        // a block held more tied keys than it kept (how the hot list spreads them depends on the
+        // rank's id numbering): collect them from the whole hot list here, so every rank agrees
+        const uint32_t nh = min(st->hot_len, T.hot_cap);
+        if (tid == 0) s_len = 0;
+        __syncthreads();
+        for (uint32_t i0 = tid & ~63u; i0 < nh; i0 += NEXT_THREADS) {  // wave-uniform trip count
+            const uint32_t i = i0 + (tid & 63);
+            uint32_t id = NO_ID;
+            if (i < nh) id = T.hot[i];
+            const bool tied = id != NO_ID && T.id_cnt[id] == top;
+            const uint32_t j = wave_append(&s_len, tied);
+            if (tied && j < total) {
+                const uint32_t key = T.id_key[id];
+                N.tie_list[j] = ((uint64_t)(zig_pair_hash(key) & cap_mask) << 32) | key;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            if (s_len != total) atomicOr(&st->error, 128u);
+            st->tie_len = total;
+        }
         return;
     }
     // tied blocks in block order and the exclusive offsets of their keys (wave 0, 64 blocks per step)
@@ -2313,7 +2424,6 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
     }
     __syncthreads();
     const uint32_t ntb = s_ntb;
-    const uint32_t cap_mask = N.V.C - 1;
     for (uint32_t e = tid; e < total; e += NEXT_THREADS) {
         uint32_t lo = 0, hi = ntb;  // the tied block holding key e: s_to[lo] <= e < s_to[lo + 1]
         while (hi - lo > 1) {
