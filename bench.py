@@ -20,6 +20,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "zig-bpe_amd"))
 
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_c4_pmc_traffic.json")  # tools/pmc_traffic.py output
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
 C4_SEED = 0x5EED0004
 
@@ -37,6 +38,8 @@ def parse():
     p.add_argument("--cpu-sample-merges", type=int, default=2)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--stats-out", default="")
+    p.add_argument("--scan-log-out", default="",
+                   help="write the per-launch scan log + per-merge live tokens of the last step (for tools/pmc_traffic.py)")
     p.add_argument("--share-gpu", action="store_true",
                    help="all ranks on cuda:0 with host (gloo) collectives -- rehearses N>1 on one GPU")
     return p.parse_args()
@@ -106,6 +109,8 @@ def main():
     text = zbpe.synth_corpus(args.kind, args.seed, args.n_bytes, threads=16)
     gen_s = time.time() - t0
     eng.upload(text)  # HBM-resident before timing (this rank's shard)
+    if args.scan_log_out:
+        eng.set_option("trace", 1)
 
     def barrier():
         if dist is not None:
@@ -139,6 +144,12 @@ def main():
     merges = len(m)
     value = merges * args.steps / total
     achieved = alg_bytes / scan_s / 1e9 if scan_s > 0 else 0.0
+    traffic, traffic_note = None, "no PMC pass for this configuration"
+    if os.path.exists(PMC_TRAFFIC) and args.n_bytes == 1 << 30 and args.vocab == 32000 and world == 1:
+        t = json.load(open(PMC_TRAFFIC))["traffic"]["stream_timed"]
+        traffic = t["hbm_bytes_per_launch"]
+        traffic_note = ("HBM bytes per timed stream-scan launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 PMC passes of this "
+                        "command, %s): %.3g x the algorithmic bytes" % (os.path.relpath(PMC_TRAFFIC, ROOT), t["hbm_over_alg"]))
     if rank == 0:
         res = {
             "metric": "merges/sec (BasicTokenizer.train, 1 GiB corpus, vocab 32000) + pair-count HBM GB/s",
@@ -165,7 +176,8 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_note": traffic_note,
                 "note": "per GPU (rank 0): achieved = sum over the timed scan launches (every 8th merge, HIP events on the engine "
                         "stream) of 2 B x live tokens / sum of their durations; bytes actually streamed (block skipping, "
                         "holes) / algorithmic bytes over all launches: %.3g" % (read_bytes / max(all_alg_bytes, 1)),
@@ -179,6 +191,11 @@ def main():
                                                int(st.sum_tokens), merges)
         else:
             res["cpu_baseline"] = None
+        if args.scan_log_out:
+            tr = eng.trace()
+            with open(args.scan_log_out, "w") as f:
+                json.dump({"scan_log": eng.scan_log().tolist(),
+                           "live": tr[:, zbpe.TRACE_COLUMNS.index("live")].astype(np.int64).tolist()}, f)
         if args.stats_out:
             with open(args.stats_out, "w") as f:
                 json.dump({"merges": m.tolist(), "counts": c.tolist()}, f)

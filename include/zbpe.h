@@ -139,6 +139,12 @@ zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, dou
 #define ZBPE_TRACE_COLS 11
 zbpe_status zbpe_trace(zbpe_ctx *ctx, float *rows, size_t cap_rows, size_t *n_rows);
 
+/* Profiling diagnostic: one entry per pair-scan kernel launch (zbpe_scan_pairs_t) of the last
+ * train, in launch order: 2 * (merge index) + form (0 stream scan, 1 list scan), or -1 for a launch
+ * that returned at once (its batch had halted before it). Lets a rocprofv3 per-dispatch trace (PMC
+ * counters) be matched to merges. Copies up to `cap` entries; *n = entries recorded. */
+zbpe_status zbpe_scan_log(zbpe_ctx *ctx, int32_t *out, size_t cap, size_t *n);
+
 /* Host-only diagnostic (no device work): the Zig 0.13 pair-map iteration order emulation used by
  * the exact tie fallback. Given every live pair's first-occurrence position, key (first |
  * second << 16) and count, returns the first pair in slot order whose count == top. */

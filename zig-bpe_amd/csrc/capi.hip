@@ -149,6 +149,15 @@ zbpe_status zbpe_trace(zbpe_ctx *ctx, float *rows, size_t cap_rows, size_t *n_ro
     return ZBPE_OK;
 }
 
+zbpe_status zbpe_scan_log(zbpe_ctx *ctx, int32_t *out, size_t cap, size_t *n) {
+    if (!ctx || !n || (!out && cap)) return ZBPE_INVALID_ARGUMENT;
+    const auto &l = ctx->eng.scan_log;
+    *n = l.size();
+    const size_t k = std::min(cap, *n);
+    if (k) memcpy(out, l.data(), k * sizeof(int32_t));
+    return ZBPE_OK;
+}
+
 zbpe_status zbpe_zig_order_winner(const uint32_t *first_pos, const uint32_t *keys, const uint32_t *counts, size_t n,
                                   uint32_t top, int call_after_last_insert, uint32_t *winner) {
     if ((!first_pos || !keys || !counts) && n) return ZBPE_INVALID_ARGUMENT;

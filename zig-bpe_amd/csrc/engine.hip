@@ -731,6 +731,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     run.verbose = verbose;
     run.vocab = vocab_size;
     trace.clear();
+    scan_log.clear();
     uint32_t X = 256;
     while (X < vocab_size) {
         if (h_st->live <= 0) {  // sortedCodePointPairs.len == 0 (basic_tokenizer.zig:188-191)
@@ -952,6 +953,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             trace.insert(trace.end(), row, row + ZBPE_TRACE_COLS);
         }
     }
+    for (uint32_t i = 0; i < K; i++)  // every merge of the batch launched one scan; those past a halt returned at once
+        scan_log.push_back(i < m ? (int32_t)(2 * (X0 + i - 256) + (h_log[X0 - 256 + i].mode ? 1 : 0)) : -1);
     uint32_t nlist = 0;
     for (uint32_t i = 0; i < m; i++) nlist += h_log[X0 - 256 + i].mode;
     list_streak = m > 0 && nlist == m;
@@ -1047,6 +1050,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         float ms_r, ms_s;
         HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1])); run.ev_count += ms * 1e-3;
         if (!self) {
+            scan_log.push_back((int32_t)(2 * (X - 256) + (h_st->scan_mode ? 1 : 0)));
             stats.scan_alg_bytes += 2ull * (uint64_t)n_live;
             if (h_st->scan_mode) {
                 stats.list_scans++;

@@ -109,6 +109,7 @@ struct Engine {
     // per-merge trace (option "trace"), ZBPE_TRACE_COLS floats per merge
     bool trace_on = false;
     std::vector<float> trace;
+    std::vector<int32_t> scan_log;  // per pair-scan launch of the last train (zbpe_scan_log)
     // device-resident merge loop
     uint32_t merge_batch = 32;      // merges enqueued per host sync (1: synchronous loop)
     uint32_t merge_timing = 8;     // HIP events around every merge_timing-th merge of a batch (0: none)

@@ -586,13 +586,20 @@ __device__ inline bool resolve_candidate(const ScanArgs &A, NeighbourHist &H, in
     }
     return false;
 }
+// LDS neighbour histograms of one scan workgroup, shared by the stream and list forms (one allocation)
+struct ScanLds {
+    uint32_t left[LDS_BINS], right[LDS_BINS];
+    uint32_t any;
+    unsigned long long scanned;
+};
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
-__device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A);
+__device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S);
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
-                                                                     uint32_t len);
+                                                                     uint32_t len, ScanLds &S);
 template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false>
 __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
     if (A0.dyn && A0.st->halt) return;
+    __shared__ ScanLds S;
     const ScanArgs A = scan_args_resolve(A0);
     // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
     if (A.lists && A.a != A.b && A.st->lists_valid) {
@@ -605,21 +612,21 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
                 A.st->scan_mode = 1;
                 if (A.log) A.log[A.X - 256].mode = 1;
             }
-            scan_list_body(A, by_b, A.lists + (by_b ? ob : oa), len);
+            scan_list_body(A, by_b, A.lists + (by_b ? ob : oa), len, S);
             return;
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
-    scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT>(A);
+    scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT>(A, S);
 }
 // List scan: every entry of the key token's list is a position that held the key when it was
 // listed; entries overwritten since (merged or turned into holes) fail the token check.
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
-                                                                     uint32_t len) {
+                                                                     uint32_t len, ScanLds &S) {
     // blocks past the list leave before touching LDS (the grid is sized for a stream scan)
     if (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len) return;
-    __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
-    __shared__ uint32_t s_any;
+    uint32_t *s_left = S.left, *s_right = S.right;
+    uint32_t &s_any = S.any;
     for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
     if (threadIdx.x == 0) s_any = 0;
     __syncthreads();
@@ -706,17 +713,17 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     }
 }
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
-__device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A) {
+__device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S) {
     constexpr int STAGE = 4;                      // vectors per lane per record-staging step
     constexpr uint32_t WREC = 64 * STAGE * 8 / 2;  // at most one occurrence per 2 tokens
     static_assert(UNROLL % STAGE == 0 || UNROLL < STAGE, "UNROLL must be a multiple of 4 (or < 4)");
     static_assert(PRES_BLK % (64 * UNROLL * 8) == 0, "presence blocks hold whole wave-tiles");
-    __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
+    uint32_t *s_left = S.left, *s_right = S.right;
     __shared__ uint32_t s_rec[SCAN_THREADS / 64][WREC];
     constexpr uint32_t CAND_CAP = COMPACT ? 512 : 1;  // dense form: candidates resolved per round per wave
     __shared__ uint32_t s_cand[SCAN_THREADS / 64][CAND_CAP];
-    __shared__ uint32_t s_any;
-    __shared__ unsigned long long s_scanned;
+    uint32_t &s_any = S.any;
+    unsigned long long &s_scanned = S.scanned;
     for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
     if (threadIdx.x == 0) { s_any = 0; s_scanned = 0; }
     __syncthreads();
@@ -816,6 +823,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             }
             cand &= f;
         }
+        const bool tile_cand = __ballot(cand != 0) != 0;
         // the tile's vectors are dead: start streaming the next present tile (its loads overlap
         // this tile's phase 2)
         const bool more = todo != 0;
@@ -825,7 +833,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             todo &= todo - 1;
             if (PIPE) load_tile(wt_next * WT_VEC);
         }
-        if (__ballot(cand != 0) != 0) {
+        if (tile_cand) {
         if constexpr (COMPACT) {
             // phase 2, dense form: the tile's candidates are compacted into a per-wave LDS list and
             // resolved one per lane (a lane-per-vector loop would iterate as often as the busiest lane)
@@ -935,7 +943,8 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
     // flush LDS neighbour histograms, the xx count and the streamed-slot count
     xx = wave_sum(xx);
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
-    if (lane == 0 && any) s_any = 1;
+    const bool wave_any = __ballot(any != 0) != 0;  // (a directly recorded occurrence sets it in one lane)
+    if (lane == 0 && wave_any) s_any = 1;
     if (lane == 0 && tiles) atomicAdd(&s_scanned, (unsigned long long)tiles * WT_VEC * 8);
     __syncthreads();
     if (threadIdx.x == 0 && s_scanned) atomicAdd(&A.st->scanned_slots, s_scanned);

@@ -141,7 +141,7 @@ class Stats(ctypes.Structure):
 EXPORTS = (
     "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_create_dist_host", "zbpe_destroy", "zbpe_last_error",
     "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts",
-    "zbpe_set_option", "zbpe_bench_scan", "zbpe_trace", "zbpe_zig_order_winner", "zbpe_version",
+    "zbpe_set_option", "zbpe_bench_scan", "zbpe_trace", "zbpe_scan_log", "zbpe_zig_order_winner", "zbpe_version",
 )
 TRACE_COLUMNS = ("merge", "count", "live", "slots", "streamed", "scan_ms", "replace_ms", "select_ms", "wall_ms",
                  "self_pair", "ties")
@@ -205,6 +205,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_bench_scan.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double)]
     L.zbpe_trace.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    L.zbpe_scan_log.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.zbpe_zig_order_winner.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
     L.zbpe_version.restype = ctypes.c_char_p
     for name in EXPORTS:
@@ -311,6 +312,15 @@ class Engine:
         out = np.zeros((n.value, len(TRACE_COLUMNS)), dtype=np.float32)
         if n.value:
             self._check(self._L.zbpe_trace(self._ctx, _ptr(out), n.value, ctypes.byref(n)), "zbpe_trace")
+        return out
+
+    def scan_log(self) -> np.ndarray:
+        """Per pair-scan launch of the last train: 2 * merge index + form (0 stream, 1 list), -1 = no-op launch."""
+        n = ctypes.c_size_t(0)
+        self._check(self._L.zbpe_scan_log(self._ctx, None, 0, ctypes.byref(n)), "zbpe_scan_log")
+        out = np.zeros(n.value, dtype=np.int32)
+        if n.value:
+            self._check(self._L.zbpe_scan_log(self._ctx, _ptr(out), n.value, ctypes.byref(n)), "zbpe_scan_log")
         return out
 
     def verify_counts(self) -> int:
