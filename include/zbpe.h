@@ -114,9 +114,8 @@ zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches);
 
 /* Tuning / test options: "debug_checks" (0/1), "exact_ties" (resolve every tie by the exact
  * first-occurrence emulation and cross-check the GPU cluster test), "compact_den" (compact when
- * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..6: unroll, load kind, compacted
- * phase 2; see engine.hip kScanVariants), "scan_auto" (0/1: per merge, the compacted phase 2 when
- * matches are dense), "hot_target" (ids kept by the argmax hot list),
+ * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..6: unroll, load kind, phase-2 form;
+ * see engine.hip kScanVariants), "hot_target" (ids kept by the argmax hot list),
  * "block_skip" (0/1: stream only the 8192-slot blocks that hold the pair's rarer token),
  * "trace" (0/1: record per-merge timings, see zbpe_trace), "merge_batch" (merges enqueued per host
  * sync, 1 = synchronous loop), "merge_timing" (time every N-th merge of a batch with HIP events;

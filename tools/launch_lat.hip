@@ -1,0 +1,156 @@
+// Latency microbenchmarks that decide the late-phase design (per-merge kernels vs a persistent loop):
+//  - back-to-back launches of an empty kernel at several grid sizes (dispatch + drain per launch)
+//  - a dependent pointer chase (one lane) through an array that lives in L2 / Infinity Cache / HBM
+//  - a grid barrier (atomic arrive + spin) inside one persistent launch, per barrier
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/launch_lat tools/launch_lat.hip
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+__global__ void empty_k(int *p) { if (p && threadIdx.x == 1023) p[0] = 1; }
+
+__global__ void chase_k(const uint32_t *next, int steps, uint32_t *out) {
+    uint32_t i = 0;
+    for (int s = 0; s < steps; s++) i = __builtin_nontemporal_load(&next[i]);
+    out[0] = i;
+}
+
+// sense-reversing grid barrier; gives up after ~50 ms of spinning (sets *err) so every wave ends
+__device__ bool grid_sync(unsigned *count, unsigned *gen, unsigned nblocks, unsigned *err) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        if (atomicAdd(count, 1u) == nblocks - 1) {
+            __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const long long t0 = wall_clock64();
+            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > 5000000) { atomicOr(err, 1u); break; }  // 100 MHz clock: 50 ms
+            }
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    }
+    __syncthreads();
+    return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+}
+
+// select_next's end pattern: every block writes `words` u32 per thread, then release fence (agent) +
+// ticket; the last block acquires and reads one word per block
+template <bool FENCE>
+__global__ void ticket_k(uint32_t *data, int words, unsigned *ticket, uint32_t *out) {
+    __shared__ unsigned s_last;
+    for (int k = 0; k < words; k++) data[((size_t)blockIdx.x * words + k) * blockDim.x + threadIdx.x] = k + threadIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = t == gridDim.x - 1;
+        if (last && FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    uint32_t acc = 0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) acc += data[(size_t)b * words * blockDim.x];
+    if (acc == 12345) out[0] = acc;
+    if (threadIdx.x == 0) *ticket = 0;
+}
+
+__global__ void barrier_k(unsigned *count, unsigned *gen, int iters, unsigned *err) {
+    for (int i = 0; i < iters; i++)
+        if (!grid_sync(count, gen, gridDim.x, err)) return;
+}
+
+int main() {
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float ms;
+    const int R = 2000;
+    for (int grid : {1, 64, 256, 1024, 2048, 8192}) {
+        for (int w = 0; w < 2; w++) {
+            CK(hipEventRecord(e0, s));
+            for (int r = 0; r < R; r++) empty_k<<<grid, 256, 0, s>>>(nullptr);
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+        }
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"test\": \"empty_launch\", \"grid\": %d, \"us_per_launch\": %.3f}\n", grid, ms * 1e3 / R);
+    }
+    // pointer chase: random cycle over n words
+    for (size_t bytes : {(size_t)1 << 20, (size_t)64 << 20, (size_t)512 << 20}) {
+        const size_t n = bytes / 4;
+        std::vector<uint32_t> h(n);
+        std::vector<uint32_t> perm(n);
+        for (size_t i = 0; i < n; i++) perm[i] = (uint32_t)i;
+        srand(1);
+        for (size_t i = n - 1; i > 0; i--) { size_t j = ((size_t)rand() * 65536u + rand()) % (i + 1); std::swap(perm[i], perm[j]); }
+        for (size_t i = 0; i < n; i++) h[perm[i]] = perm[(i + 1) % n];
+        uint32_t *d, *o;
+        CK(hipMalloc(&d, bytes));
+        CK(hipMalloc(&o, 4));
+        CK(hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice));
+        const int steps = 20000;
+        chase_k<<<1, 1, 0, s>>>(d, steps, o);
+        CK(hipEventRecord(e0, s));
+        chase_k<<<1, 1, 0, s>>>(d, steps, o);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"test\": \"chase\", \"bytes\": %zu, \"ns_per_load\": %.1f}\n", bytes, ms * 1e6 / steps);
+        CK(hipFree(d));
+        CK(hipFree(o));
+    }
+    {
+        uint32_t *data, *out;
+        unsigned *tk;
+        CK(hipMalloc(&data, (size_t)256 << 20));
+        CK(hipMalloc(&out, 4));
+        CK(hipMalloc(&tk, 4));
+        CK(hipMemset(tk, 0, 4));
+        for (int fence = 0; fence < 2; fence++)
+            for (int grid : {16, 64, 256})
+                for (int words : {1, 16, 64}) {
+                    const int iters = 500;
+                    for (int w = 0; w < 2; w++) {
+                        CK(hipEventRecord(e0, s));
+                        for (int i = 0; i < iters; i++) {
+                            if (fence) ticket_k<true><<<grid, 1024, 0, s>>>(data, words, tk, out);
+                            else ticket_k<false><<<grid, 1024, 0, s>>>(data, words, tk, out);
+                        }
+                        CK(hipEventRecord(e1, s));
+                        CK(hipEventSynchronize(e1));
+                    }
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    printf("{\"test\": \"ticket\", \"fence\": %d, \"grid\": %d, \"dirty_KB_per_block\": %d, \"us_per_launch\": %.3f}\n",
+                           fence, grid, words * 4, ms * 1e3 / iters);
+                }
+        CK(hipFree(data));
+    }
+    // grid barrier: all blocks resident (grid <= CUs)
+    unsigned *cnt, *gen, *err;
+    CK(hipMalloc(&cnt, 4)); CK(hipMalloc(&gen, 4)); CK(hipMalloc(&err, 4));
+    for (int grid : {8, 64, 256}) {
+        CK(hipMemset(cnt, 0, 4)); CK(hipMemset(gen, 0, 4)); CK(hipMemset(err, 0, 4));
+        const int iters = 2000;
+        barrier_k<<<grid, 256, 0, s>>>(cnt, gen, 10, err);
+        CK(hipEventRecord(e0, s));
+        barrier_k<<<grid, 256, 0, s>>>(cnt, gen, iters, err);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        unsigned herr = 0;
+        CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+        printf("{\"test\": \"grid_barrier\", \"grid\": %d, \"us_per_barrier\": %.3f, \"err\": %u}\n", grid, ms * 1e3 / iters, herr);
+    }
+    return 0;
+}

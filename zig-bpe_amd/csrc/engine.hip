@@ -538,13 +538,14 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
 }
 
 using ScanFn = void (*)(ScanArgs);
-// 0 is the default (unroll 4, non-temporal loads, next-token filter); the others for A/B runs
-// 2 (dense matches, chosen by scan_auto): candidates compacted per wave before phase 2
-// (`tools/scan_variants.py`: +22 % at 1/75 density, -14 % at 1/400, so only above 1/128)
-static const ScanFn kScanVariants[] = {zbpe_scan_pairs_t<4, true, true>,  zbpe_scan_pairs_t<8, true, true>,
-                                       zbpe_scan_pairs_t<4, true, true, true, true>, zbpe_scan_pairs_t<4, true, false>,
-                                       zbpe_scan_pairs_t<2, true, true>,  zbpe_scan_pairs_t<4, true, true, false>,
-                                       zbpe_scan_pairs_t<4, false, true>};
+// 0 is the default: unroll 4, non-temporal loads, two-token-window candidate test, candidates
+// compacted per wave and resolved one per lane on the LDS-staged tile. The others for A/B runs
+// (tools/scan_density.py): 2 resolves per vector in its lane (slower at every density measured:
+// 4.8 vs 5.2 TB/s for a rare pair with a frequent first token, 1.7 vs 2.9 TB/s for (e, ' ')).
+static const ScanFn kScanVariants[] = {zbpe_scan_pairs_t<4, true, true, true, true>, zbpe_scan_pairs_t<8, true, true, true, true>,
+                                       zbpe_scan_pairs_t<4, true, true>, zbpe_scan_pairs_t<4, true, false>,
+                                       zbpe_scan_pairs_t<2, true, true, true, true>, zbpe_scan_pairs_t<4, true, true, false, true>,
+                                       zbpe_scan_pairs_t<4, false, true, true, true>};
 static const int kScanUnroll[] = {4, 8, 4, 4, 2, 4, 4};
 
 zbpe_status Engine::set_scan_variant(int v) {
@@ -557,10 +558,9 @@ zbpe_status Engine::set_scan_variant(int v) {
     return ZBPE_OK;
 }
 
-zbpe_status Engine::launch_scan(const ScanArgs &A, uint64_t expected_occ, int grid) {
+zbpe_status Engine::launch_scan(const ScanArgs &A, int grid) {
     // default variant 0; when matches are dense (> 1/128 of the stream) the compacted phase 2
-    int v = scan_variant;
-    if (v == 0 && scan_auto && expected_occ * 128 > (uint64_t)A.n) v = 2;
+    const int v = scan_variant;
     hipLaunchKernelGGL(kScanVariants[v], dim3(grid > 0 ? grid : scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, A);
     LAUNCH_OK();
     return ZBPE_OK;
@@ -581,7 +581,7 @@ zbpe_status Engine::bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms,
     for (int r = 0; r < reps; r++) {
         HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
         HIP_OK(hipEventRecord(ev[0], stream));
-        CHECK(launch_scan(A, 0));
+        CHECK(launch_scan(A));
         HIP_OK(hipEventRecord(ev[1], stream));
         zbpe_reset_merge<<<256, 256, 0, stream>>>(d_st, d_delta, d_delta + 65536, 65536);
         LAUNCH_OK();
@@ -858,7 +858,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                    lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log};
         // a batch that follows one of list scans only launches a smaller grid (fewer idle workgroups
         // to dispatch); a stream scan still completes on it, only slower
-        CHECK(launch_scan(A, top0, list_streak ? list_grid : 0));
+        CHECK(launch_scan(A, list_streak ? list_grid : 0));
         if (timed) HIP_OK(hipEventRecord(bev[4 * i + 2], stream));
         CHECK(comm_sum(d_delta, 2ull * X + 2));
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
@@ -891,10 +891,6 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                        dist() ? world : 1};
             zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, d_delta, X, N);
             LAUNCH_OK();
-            if (C && X + 1 < run.vocab) {  // returns at once unless merge X+1 is a tie the select gathered
-                zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 1);
-                LAUNCH_OK();
-            }
         } else {
             CHECK(launch_argmax(X, 1));
         }
@@ -1000,7 +996,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
                T.lst_len, list_ratio, 1, nullptr};
     HIP_OK(hipEventRecord(ev[0], stream));
     if (!self) {
-        CHECK(launch_scan(A, top));
+        CHECK(launch_scan(A));
         stats.scan_launches++;
     } else {
         stats.self_pair_merges++;
@@ -1195,7 +1191,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
                    nullptr, vp, X, nullptr, 0, nullptr, use_lists ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio,
                    use_lists ? 1 : 0, nullptr};
         if (a != b) {
-            CHECK(launch_scan(A, 0));
+            CHECK(launch_scan(A));
         } else {  // holes are transparent to the self-pair path
             const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);
             CHECK(ensure(&d_tile_fn, tile_fn_cap, ntiles, "self tiles"));

@@ -430,6 +430,34 @@ __device__ inline uint32_t match8(uint4 v, uint32_t a) {
     return m;
 }
 
+// Phase-1 candidate test of one 16-B vector (8 tokens) by two-token windows: each window is one
+// 32-bit compare against (a, b) and against (a, HOLE) (by a) or (HOLE, b) (by b), so a vector
+// costs ~20 VALU ops into lane masks, and per-lane bits only when some lane of the wave matched.
+// By a, bit k = the window starting at token k matched; by b, the window ending at token k. `edge`
+// is the neighbouring vector's word in stream order (by a: the next vector's first, by b: the
+// previous vector's last), so the test is exact at every lane.
+template <bool BY_B>
+__device__ __attribute__((always_inline)) inline uint32_t pair_windows8(uint4 v, uint32_t edge, uint32_t P1, uint32_t P2) {
+    const uint32_t ww[5] = {BY_B ? edge : v.x, BY_B ? v.x : v.y, BY_B ? v.y : v.z, BY_B ? v.z : v.w, BY_B ? v.w : edge};
+    auto win = [&](int k) -> uint32_t {  // the two-token window of bit k
+        const int t = k + (BY_B ? 1 : 0);
+        return (t & 1) ? __builtin_amdgcn_alignbit(ww[t / 2 + 1], ww[t / 2], 16) : ww[t / 2];
+    };
+    auto hit = [&](int k) -> bool {
+        const uint32_t x = win(k);
+        return (x == P1) | (x == P2);
+    };
+    // the common case (no lane matches) only ORs lane masks; the bits are recomputed on a match
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 8; k++) any |= hit(k);
+    if (!__ballot(any)) return 0;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) bits |= hit(k) ? (1u << k) : 0u;
+    return bits;
+}
+
 // ------------------------------------------------------------------------------------------
 // THE HOT KERNEL (one launch per merge): stream the token stream once, find every occurrence
 // of the top pair (a, b), a != b (every occurrence is merged: non-overlapping by construction),
@@ -550,6 +578,47 @@ __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64
         if (hit) hits |= 1u << k;
     }
     return hits;
+}
+
+// One candidate start p = 8 vi + k of the window tok[8 vi - 2 .. 8 vi + 11] (see occ_window): 1 if
+// (p, next live) == (a, b) (deltas counted), 0 if not, -1 if the window cannot decide (occ_slow).
+__device__ __attribute__((always_inline)) inline int occ_fast1(const ScanArgs &A, NeighbourHist &H, int64_t vi, int k, uint32_t &xx,
+                                                               uint32_t pw, uint4 cv, uint32_t nx, uint32_t ny) {
+    const uint64_t W0 = (uint64_t)pw | ((uint64_t)cv.x << 32);
+    const uint64_t W1 = (uint64_t)cv.y | ((uint64_t)cv.z << 32);
+    const uint64_t W2 = (uint64_t)cv.w | ((uint64_t)nx << 32);
+    const uint64_t W3 = (uint64_t)ny;
+    auto win = [&](int i) -> uint32_t {
+        const uint64_t q = i < 4 ? W0 : i < 8 ? W1 : i < 12 ? W2 : W3;
+        return (uint32_t)(q >> ((i & 3) * 16)) & 0xffffu;
+    };
+    uint32_t live = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) live |= (win(i) != HOLE ? 1u : 0u) << i;
+    const int i = k + 2;
+    const int64_t p = vi * 8 + k;
+    const uint32_t after = live >> (i + 1), before = live & ((1u << i) - 1u);
+    if (!after || !before || p < 2 || p + 3 >= A.n) return -1;
+    const int q = i + 1 + __builtin_ctz(after);
+    const int l = 31 - __builtin_clz(before);
+    const uint32_t aq = live >> (q + 1);
+    if (!aq) return -1;
+    const int r = q + 1 + __builtin_ctz(aq);
+    const uint32_t bl = live & ((1u << l) - 1u), ar = live >> (r + 1);
+    const int ll = bl ? 31 - __builtin_clz(bl) : -1;
+    const int rn = ar ? r + 1 + __builtin_ctz(ar) : 14;
+    // every token the delta rules may look at must be inside the window
+    if ((win(r) == A.a && rn >= 14) || (win(l) == A.b && ll < 0)) return -1;
+    if (win(q) != A.b) return 0;
+    if (A.count_deltas) {
+        const uint32_t tl = win(l), tr = win(r);
+        const bool merged_end = (tl == A.b) && (win(ll < 0 ? 0 : ll) == A.a);
+        if (!merged_end) H.left((uint16_t)tl);
+        const bool r_occ = (tr == A.a) && (win(rn > 13 ? 13 : rn) == A.b);
+        if (r_occ) xx++;
+        else H.right((uint16_t)tr);
+    }
+    return 1;
 }
 
 __device__ inline void pres_set(const ScanArgs &A, int64_t pos) {
@@ -714,13 +783,15 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
 }
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S) {
-    constexpr int STAGE = 4;                      // vectors per lane per record-staging step
+    constexpr int STAGE = 2;                      // vectors per lane per record-staging step
     constexpr uint32_t WREC = 64 * STAGE * 8 / 2;  // at most one occurrence per 2 tokens
-    static_assert(UNROLL % STAGE == 0 || UNROLL < STAGE, "UNROLL must be a multiple of 4 (or < 4)");
+    static_assert(UNROLL % STAGE == 0 || UNROLL < STAGE, "UNROLL must be a multiple of STAGE (or < STAGE)");
     static_assert(PRES_BLK % (64 * UNROLL * 8) == 0, "presence blocks hold whole wave-tiles");
     uint32_t *s_left = S.left, *s_right = S.right;
     __shared__ uint32_t s_rec[SCAN_THREADS / 64][WREC];
-    constexpr uint32_t CAND_CAP = COMPACT ? 512 : 1;  // dense form: candidates resolved per round per wave
+    // a wave's current tile, staged in LDS when it holds candidates: phase 2 reads its windows here
+    __shared__ uint4 s_tile[SCAN_THREADS / 64][64 * UNROLL];
+    constexpr uint32_t CAND_CAP = COMPACT ? 256 : 1;  // compacted form: candidates resolved per round per wave
     __shared__ uint32_t s_cand[SCAN_THREADS / 64][CAND_CAP];
     uint32_t &s_any = S.any;
     unsigned long long &s_scanned = S.scanned;
@@ -768,22 +839,36 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
       if (!todo) continue;
       // phase 1: stream UNROLL x 16 B per lane, keep only the positions holding the key token
       uint4 v[UNROLL];
+      // the stream words just outside the tile (wave-uniform): the last one before it and the first
+      // two after it (holes outside the stream)
+      uint32_t ld_prev = 0xffffffffu, ld_nx = 0xffffffffu, ld_ny = 0xffffffffu;
+      // Branch-free: addresses are clamped into the stream and out-of-range values replaced after
+      // the load (a load under a branch makes the compiler wait for it at the join).
       auto load_tile = [&](int64_t vb) {
+          {
+              const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tok);
+              const int64_t last = nvec * 4 - 1;  // last word of the stream
+              const int64_t ip = vb > 0 ? vb * 4 - 1 : 0, in = min((vb + WT_VEC) * 4, last - 1);
+              const uint32_t wp = t32[ip];
+              const uint2 wn = *reinterpret_cast<const uint2 *>(t32 + (in & ~(int64_t)1));
+              const bool has_next = vb + WT_VEC < nvec;
+              ld_prev = vb > 0 ? wp : 0xffffffffu;
+              ld_nx = has_next ? wn.x : 0xffffffffu;
+              ld_ny = has_next ? wn.y : 0xffffffffu;
+          }
 #pragma unroll
           for (int u = 0; u < UNROLL; u++) {
               const int64_t vi = vb + u * 64 + lane;
-              if (vi < nvec) {
-                  const uint4 *src = reinterpret_cast<const uint4 *>(tok) + vi;
-                  if constexpr (NT) {
-                      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
-                      v[u] = make_uint4(x.x, x.y, x.z, x.w);
-                  } else {
-                      v[u] = *src;
-                  }
+              const uint4 *src = reinterpret_cast<const uint4 *>(tok) + min(vi, nvec - 1);
+              uint4 x;
+              if constexpr (NT) {
+                  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                  const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
+                  x = make_uint4(y.x, y.y, y.z, y.w);
               } else {
-                  v[u] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+                  x = *src;
               }
+              v[u] = vi < nvec ? x : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
           }
       };
       int64_t wt = wt0 + (int64_t)__builtin_ctzll(todo) * wstride;
@@ -791,39 +876,40 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
       load_tile(wt * WT_VEC);
       for (;;) {
         const int64_t vbase = wt * WT_VEC;
+        const uint32_t e_prev = ld_prev, e_nx = ld_nx, e_ny = ld_ny;  // this tile's (ld_* may be the next's soon)
         tiles++;
         uint64_t cand = 0;  // bit 8u+k: token k of vector u is the key token
+        if constexpr (FILTER) {
+            // candidates: key-token positions whose partner slot holds the other token or a hole
+            const uint32_t P1 = pair_key(A.a, A.b);
+            // the neighbouring vector of lane 63 (by a) / lane 0 (by b) is in the next / previous
+            // row of the tile, or outside it (edge_w, loaded with the tile)
+            if (!by_b) {
+                const uint32_t P2 = pair_key(A.a, HOLE);
 #pragma unroll
-        for (int u = 0; u < UNROLL; u++) cand |= (uint64_t)match8(v[u], key_tok) << (8 * u);
-        if (FILTER && __ballot(cand != 0) != 0) {
-            // by a: keep a where the next slot holds b or a hole; by b: keep b where the previous slot
-            // holds a or a hole (across lanes by a shuffle; lanes 63 / 0 keep their edge candidate)
-            uint64_t f = 0;
-#pragma unroll
-            for (int u = 0; u < UNROLL; u++) {
-                uint32_t nb = 0;
-                if (!by_b) {
-                    const uint32_t nx = (uint32_t)__shfl_down((int)v[u].x, 1) & 0xffffu;
-#pragma unroll
-                    for (int k = 0; k < 7; k++) {
-                        const uint32_t t = tok_at(v[u], k + 1);
-                        nb |= (t == A.b || t == HOLE ? 1u : 0u) << k;
-                    }
-                    nb |= (lane == 63 || nx == A.b || nx == HOLE ? 1u : 0u) << 7;
-                } else {
-                    const uint32_t pv = (uint32_t)__shfl_up((int)v[u].w, 1) >> 16;
-                    nb |= (lane == 0 || pv == A.a || pv == HOLE ? 1u : 0u);
-#pragma unroll
-                    for (int k = 1; k < 8; k++) {
-                        const uint32_t t = tok_at(v[u], k - 1);
-                        nb |= (t == A.a || t == HOLE ? 1u : 0u) << k;
-                    }
+                for (int u = 0; u < UNROLL; u++) {
+                    const uint32_t nrow = u + 1 < UNROLL ? (uint32_t)__shfl((int)v[u + 1 < UNROLL ? u + 1 : u].x, 0) : e_nx;
+                    const uint32_t dn = (uint32_t)__shfl_down((int)v[u].x, 1);
+                    cand |= (uint64_t)pair_windows8<false>(v[u], lane == 63 ? nrow : dn, P1, P2) << (8 * u);
                 }
-                f |= (uint64_t)nb << (8 * u);
+            } else {
+                const uint32_t P2 = pair_key(HOLE, A.b);
+#pragma unroll
+                for (int u = 0; u < UNROLL; u++) {
+                    const uint32_t prow = u > 0 ? (uint32_t)__shfl((int)v[u > 0 ? u - 1 : 0].w, 63) : e_prev;
+                    const uint32_t up = (uint32_t)__shfl_up((int)v[u].w, 1);
+                    cand |= (uint64_t)pair_windows8<true>(v[u], lane == 0 ? prow : up, P1, P2) << (8 * u);
+                }
             }
-            cand &= f;
+        } else {
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++) cand |= (uint64_t)match8(v[u], key_tok) << (8 * u);
         }
         const bool tile_cand = __ballot(cand != 0) != 0;
+        if (tile_cand) {
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++) s_tile[wib][u * 64 + lane] = v[u];
+        }
         // the tile's vectors are dead: start streaming the next present tile (its loads overlap
         // this tile's phase 2)
         const bool more = todo != 0;
@@ -833,7 +919,62 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             todo &= todo - 1;
             if (PIPE) load_tile(wt_next * WT_VEC);
         }
+        // window of vector vi of this tile: tok[8 vi - 2 .. 8 vi + 11] from the LDS tile and the edge words
+        auto tile_window = [&](int64_t vi, uint32_t &pw, uint4 &cv, uint32_t &nx, uint32_t &ny) {
+            const int j = (int)(vi - vbase);
+            const uint4 *T = s_tile[wib];
+            cv = T[j];
+            pw = j > 0 ? T[j - 1].w : e_prev;
+            nx = e_nx;
+            ny = e_ny;
+            if (j + 1 < WT_VEC) {
+                const uint2 q = *reinterpret_cast<const uint2 *>(&T[j + 1]);
+                nx = q.x;
+                ny = q.y;
+            }
+        };
+        // candidate p (holding the key token) of this tile: is it part of an occurrence? *pr = its start.
+        // One window test and one slow-path call site (register pressure of the inlined code)
+        auto resolve = [&](int64_t p, uint32_t &pr) -> bool {
+            int64_t vi = p >> 3;
+            const int k = (int)(p & 7);
+            uint32_t pw, nx, ny;
+            uint4 cv;
+            tile_window(vi, pw, cv, nx, ny);
+            int64_t start = p;
+            bool in_win = true;
+            if (by_b) {  // the occurrence starts at the live slot before p (window slot k + 2)
+                uint32_t tl = HOLE;
+                int l = -1;
+#pragma unroll
+                for (int i = 0; i < 10; i++) {
+                    const uint32_t t = i < 2 ? (i ? pw >> 16 : pw & 0xffffu) : tok_at(cv, i - 2);
+                    if (i < k + 2 && t != HOLE) { l = i; tl = t; }
+                }
+                if (l >= 0) {
+                    if (tl != A.a) return false;
+                    start = vi * 8 + l - 2;
+                    if (l < 2) {
+                        if (vi > vbase) {  // the start is in the previous vector of the tile
+                            vi -= 1;
+                            tile_window(vi, pw, cv, nx, ny);
+                        } else {
+                            in_win = false;
+                        }
+                    }
+                } else {  // a run of holes reaches past the window (q < 0: the left shard owns it)
+                    start = prev_live_h(A, p);
+                    if (start < 0 || tok[start] != A.a) return false;
+                    in_win = false;
+                }
+            }
+            pr = (uint32_t)start;
+            int r = in_win ? occ_fast1(A, H, vi, (int)(start - vi * 8), xx, pw, cv, nx, ny) : -1;
+            if (r < 0) r = occ_slow(A, H, start, xx);
+            return r != 0;
+        };
         if (tile_cand) {
+        wave_lds_sync();  // the staged tile is visible to every lane of the wave
         if constexpr (COMPACT) {
             // phase 2, dense form: the tile's candidates are compacted into a per-wave LDS list and
             // resolved one per lane (a lane-per-vector loop would iterate as often as the busiest lane)
@@ -858,7 +999,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
                 for (uint32_t j = lane; j - lane < nr; j += 64) {
                     bool hit = false;
                     uint32_t pr = 0;
-                    if (j < nr) hit = resolve_candidate(A, H, wc[j], by_b, nvec, xx, pr);
+                    if (j < nr) hit = resolve(wc[j], pr);
                     const uint64_t hm = __ballot(hit);
                     if (!hm) continue;
                     any = 1;
@@ -880,30 +1021,35 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             }
             if (A.pres && tile_hit && lane == 0) pres_set(A, vbase * 8);
         } else {
-        // phase 2 (lanes with candidates): resolve occurrences, stage them per STAGE vectors
-#pragma unroll
+        // phase 2 (lanes with candidates): resolve occurrences on the LDS tile, stage their starts per
+        // STAGE vectors; occ holds 16 bits per vector, bit s = start 8 vi - 2 + s
+        const uint64_t tile_blk = (uint64_t)vbase * 8 / PRES_BLK;
+#pragma unroll 1
         for (int ug = 0; ug < UNROLL; ug += STAGE) {
-            uint32_t occ = 0;  // bit 8(u-ug)+k (by b: the occurrence's b sits there)
-            uint64_t c = (cand >> (8 * ug)) & ((STAGE * 8 >= 64) ? ~0ull : ((1ull << (STAGE * 8)) - 1));
+            constexpr int SG = STAGE < UNROLL ? STAGE : UNROLL;
+            uint64_t occ = 0;
+            uint64_t c = (cand >> (8 * ug)) & ((SG * 8 >= 64) ? ~0ull : ((1ull << (SG * 8)) - 1));
 #pragma unroll 1
             while (c) {
-                const int u = (__ffsll((unsigned long long)c) - 1) >> 3;
-                uint32_t m = (uint32_t)(c >> (8 * u)) & 0xffu;
-                c &= ~(0xffull << (8 * u));
+                const int k8 = __ffsll((unsigned long long)c) - 1;
+                c &= c - 1;
+                const int u = k8 >> 3;
                 const int64_t vi = vbase + (ug + u) * 64 + lane;
-                if (!by_b) {
-                    occ |= occ_vector(A, H, vi, nvec, m, xx) << (8 * u);
-                } else {
-                    while (m) {
-                        const int k = __ffs(m) - 1;
-                        m &= m - 1;
-                        const int64_t q = vi * 8 + k, p = prev_live_h(A, q);
-                        // p < 0: the a is the left shard's, which owns the occurrence
-                        if (p >= 0 && tok[p] == A.a && occ_slow(A, H, p, xx)) occ |= 1u << (8 * u + k);
-                    }
+                uint32_t pr;
+                if (!resolve(vi * 8 + (k8 & 7), pr)) continue;
+                const int64_t sft = (int64_t)pr - (vi * 8 - 2);
+                if (sft >= 0 && sft < 16) {
+                    occ |= 1ull << (16 * u + sft);
+                } else {  // a start beyond the window (hole run): record it directly
+                    const uint32_t j = atomicAdd(&A.st->rec_count, 1u);
+                    atomicAdd(A.occ_out, 1u);
+                    if (j < A.rec_cap) A.rec[j] = pr;
+                    else atomicOr(&A.st->error, 8u);
+                    if (A.pres) pres_set(A, pr);
+                    any = 1;
                 }
             }
-            const uint32_t cnt = __popc(occ);
+            const uint32_t cnt = (uint32_t)__popcll(occ);
             const uint32_t incl = wave_incl_scan(cnt);
             const uint32_t total = (uint32_t)__shfl((int)incl, 63);
             if (total == 0) continue;
@@ -915,15 +1061,11 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
                 wave_lds_sync();
             }
             uint32_t o = nbuf + incl - cnt;
-            const uint64_t tile_blk = (uint64_t)vbase * 8 / PRES_BLK;
             while (occ) {
-                const int bit = __ffs(occ) - 1;
+                const int bit = __ffsll((unsigned long long)occ) - 1;
                 occ &= occ - 1;
-                int64_t p = (vbase + (ug + (bit >> 3)) * 64 + lane) * 8 + (bit & 7);
-                if (by_b) {
-                    p = prev_live(tok, p);
-                    if (A.pres && (uint64_t)p / PRES_BLK != tile_blk) pres_set(A, p);
-                }
+                const int64_t p = (vbase + (ug + (bit >> 4)) * 64 + lane) * 8 + (bit & 15) - 2;
+                if (A.pres && (uint64_t)p / PRES_BLK != tile_blk) pres_set(A, p);
                 wrec[o++] = (uint32_t)p;
             }
             nbuf += total;
@@ -1724,7 +1866,7 @@ __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, co
 // ------------------------------------------------------------------------------------------
 __device__ inline Summ summ_cat(Summ a, Summ b) { return Summ{a.q + b.q, max(b.m, a.m + b.q)}; }
 __device__ inline Summ summ_slot(uint32_t k) {
-    const int64_t q = (int64_t)k - 1;
+    const int32_t q = (int32_t)k - 1;
     return Summ{q, q > 0 ? q : 0};
 }
 __device__ inline uint32_t home_at(const uint32_t *hc, uint32_t s) { return (hc[s >> 2] >> (8 * (s & 3))) & 0xffu; }
@@ -2002,7 +2144,7 @@ __device__ inline Summ wave_reduce_summ(Summ x) {
 // slots after s in its block, the blocks after it in its super-block, the other super-blocks, the
 // blocks before it in its super-block, the slots before s. Every load is issued before the first
 // reduction (one memory latency, not five).
-__device__ inline int64_t wave_carry_into(const HomeView &V, uint32_t s) {
+__device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const HomeView &V, uint32_t s) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t b = s / SUMM_SLOTS, sb = b / SUPER_BLOCKS, bbase = b * SUMM_SLOTS;
     const uint32_t s0 = bbase + 64 * lane, bend = min(V.C, bbase + SUMM_SLOTS);
@@ -2055,7 +2197,7 @@ __device__ inline int64_t wave_carry_into(const HomeView &V, uint32_t s) {
 }
 // first free slot at or after h given the carry into h, by one wave, 64 slots per step; -1 when
 // the run reaches slot C-1 (wraps) or is absurdly long
-__device__ inline int64_t wave_first_free(const HomeView &V, uint32_t h, int64_t carry_in) {
+__device__ __attribute__((always_inline)) inline int64_t wave_first_free(const HomeView &V, uint32_t h, int64_t carry_in) {
     const uint32_t lane = threadIdx.x & 63;
     int64_t c = carry_in;
     for (uint32_t base = h; base < V.C && base - h <= (1u << 20); base += 64) {
@@ -2075,7 +2217,7 @@ __device__ inline int64_t wave_first_free(const HomeView &V, uint32_t h, int64_t
         ex.q = __shfl_up(inc.q, 1);
         ex.m = __shfl_up(inc.m, 1);
         if (lane == 0) ex = Summ{0, 0};
-        const int64_t cin = max(ex.m, c + ex.q);
+        const int64_t cin = max((int64_t)ex.m, c + ex.q);
         const uint64_t fr = __ballot(valid && cin + k == 0);
         if (fr) return (int64_t)base + __builtin_ctzll(fr);
         if (base + 64 >= V.C) return -1;
@@ -2087,7 +2229,7 @@ __device__ inline int64_t wave_first_free(const HomeView &V, uint32_t h, int64_t
 // last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none)
 // last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none); lo is a multiple
 // of 64 and hi - lo <= 4096: lane L owns slots lo + 64L .. +63, read once as four 16-B vectors
-__device__ inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int64_t carry_in) {
+__device__ __attribute__((always_inline)) inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int64_t carry_in) {
     const uint32_t lane = threadIdx.x & 63, s0 = lo + 64 * lane;
     uint32_t w[16];
     const bool mine = s0 < hi;
@@ -2119,7 +2261,7 @@ __device__ inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_
     ex.q = __shfl_up(inc.q, 1);
     ex.m = __shfl_up(inc.m, 1);
     if (lane == 0) ex = Summ{0, 0};
-    int64_t c = max(ex.m, carry_in + ex.q);
+    int64_t c = max((int64_t)ex.m, carry_in + ex.q);
     long long last = -1;
 #pragma unroll
     for (int k = 0; k < 64; k++) {
@@ -2226,7 +2368,7 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
 // start of merge X+1 and, on a tie, gathers the tied keys for zbpe_tie_decide (the next launch:
 // the decision's carry code needs 256 VGPRs, more than a 1024-thread block may hold).
 // ------------------------------------------------------------------------------------------
-constexpr int NEXT_THREADS = 1024;
+constexpr int NEXT_THREADS = 512;  // (the fused tie decision needs > 128 VGPRs per lane)
 constexpr int NEXT_CAND = 64;          // keys kept per argmax block at the block's max
 constexpr int NEXT_MAX_SEL = 1024;     // argmax blocks (the reducer keeps one LDS entry per block)
 struct NextArgs {
@@ -2412,8 +2554,7 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
             if (s_len != total) atomicOr(&st->error, 128u);
             st->tie_len = total;
         }
-        return;
-    }
+    } else {
     // tied blocks in block order and the exclusive offsets of their keys (wave 0, 64 blocks per step)
     __shared__ uint32_t s_tb[NEXT_MAX_SEL], s_to[NEXT_MAX_SEL + 1];
     if (tid < 64) {
@@ -2442,7 +2583,12 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
         const uint32_t key = N.cand[s_tb[lo] * NEXT_CAND + (e - s_to[lo])];
         N.tie_list[e] = ((uint64_t)(zig_pair_hash(key) & cap_mask) << 32) | key;
     }
-    if (tid == 0) st->tie_len = total;  // zbpe_tie_decide (the next launch) decides from the list
+    if (tid == 0) st->tie_len = total;
+    }
+    // ---- merge X+1 ties: the Zig-order decision, by this block (the list and the refreshed home
+    // summaries are this block's writes or were published before its ticket) -------------------------
+    __syncthreads();
+    decide_body<NEXT_THREADS>(st, N.tie_list, total, total, N.V, N.B.log, 1);
 }
 
 // rebuild the home histogram for a new Zig capacity

@@ -98,7 +98,9 @@ struct Tables {
 constexpr int COUNT_BINS = 64 + 26 * 32;  // count histogram for choosing theta: exact < 64, then 32 per octave
 constexpr int SUMM_SLOTS = 4096;          // home-histogram slots per max-plus block summary
 constexpr int SUPER_BLOCKS = 64;          // block summaries per super-block summary
-struct Summ { int64_t q, m; };            // carry function c -> max(m, c + q) of a run of slots
+// carry function c -> max(m, c + q) of a run of slots; |q|, m <= Zig capacity < 2^31, so 32-bit
+// arithmetic (half the VALU chain and shuffles of the tie decision)
+struct Summ { int32_t q, m; };
 
 // Live tokens just outside this rank's shard (multi-GPU): left token 0 is the last live token before
 // the shard, left 1 the one before it; right 0..2 the first live tokens after it. Packed 16 bits per
