@@ -170,6 +170,50 @@ def test_encode_list_and_stream_scans_vs_oracle(list_mode, ratio):
     e.close()
 
 
+@pytest.mark.parametrize("batch", [1, 2, 32])
+def test_encode_batched_vs_oracle(batch):
+    """Batched encode (disjoint consecutive merges applied together) equals the reference's merge-by-merge
+    replay, with self pairs and merges sharing tokens breaking the batches."""
+    e = zbpe.Engine(0)
+    e.set_option("encode_batch", batch)
+    for kind, seed, n, vocab in (("words_utf8", 47, 400000, 1200), ("runs", 48, 60000, 400), ("uniform", 49, 30000, 700)):
+        text = zbpe.synth_corpus(kind, seed, n)
+        m, _, _ = e.train(text, vocab)
+        other = zbpe.synth_corpus(kind, seed + 100, n)
+        for t in (text, other, text[:1], b""):
+            assert np.array_equal(e.encode(m, t), O.encode(m, t)), (kind, batch)
+        # a merge table whose order is shuffled within windows still encodes like the reference
+        if kind == "words_utf8":
+            rng = np.random.default_rng(seed)
+            mm = m.copy()
+            for s0 in range(0, len(mm) - 8, 8):
+                mm[s0:s0 + 8] = mm[s0 + rng.permutation(8)]
+            assert np.array_equal(e.encode(mm, other), O.encode(mm, other)), (kind, batch, "shuffled")
+    e.close()
+
+
+@pytest.mark.parametrize("kind,seed,n,vocab", [("runs", 51, 60000, 500), ("words_utf8", 52, 300000, 900), ("uniform", 53, 8000, 700)])
+def test_self_pairs_from_lists_vs_oracle(kind, seed, n, vocab):
+    """Self pairs (a, a) walked from a's occurrence list (lists built at the first compaction, used for
+    every self pair) give the reference's merges and counts, in training and in encode."""
+    text = zbpe.synth_corpus(kind, seed, n)
+    r = O.train(text, vocab)
+    e = zbpe.Engine(0)
+    e.set_option("list_start", 0)
+    e.set_option("compact_den", 2)
+    e.set_option("compact_den_lists", 2)
+    e.set_option("self_list_ratio", 1)
+    m, c, st = e.train(text, vocab)
+    assert m.tolist() == r.merges.tolist()
+    assert c.tolist() == r.counts.tolist()
+    assert e.verify_counts() == 0
+    e.set_option("list_ratio", 1)
+    other = zbpe.synth_corpus(kind, seed + 100, n)
+    for t in (text, other):
+        assert np.array_equal(e.encode(m, t), O.encode(m, t))
+    e.close()
+
+
 def test_encode_runs_vs_oracle(engine):
     text = zbpe.synth_corpus("runs", 43, 100000)
     m, _, _ = _train(engine, text, 600)

@@ -42,6 +42,23 @@ __device__ bool grid_sync(unsigned *count, unsigned *gen, unsigned nblocks, unsi
 
 // select_next's end pattern: every block writes `words` u32 per thread, then release fence (agent) +
 // ticket; the last block acquires and reads one word per block
+// dependent chain of returning device-scope atomics (one lane): each add's address depends on the last result
+__global__ void atomic_chain_k(uint32_t *a, int steps, uint32_t *out) {
+    uint32_t i = 0;
+    for (int s = 0; s < steps; s++) i = (atomicAdd(&a[(i & 1023) * 16], 1u) + s) & 1023;
+    out[0] = i;
+}
+// the same with LDS atomics
+__global__ void lds_chain_k(int steps, uint32_t *out) {
+    __shared__ uint32_t l[1024];
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) l[k] = 0;
+    __syncthreads();
+    uint32_t i = 0;
+    if (threadIdx.x == 0)
+        for (int s = 0; s < steps; s++) i = (atomicAdd(&l[i & 1023], 1u) + s) & 1023;
+    if (threadIdx.x == 0) out[0] = i;
+}
+
 template <bool FENCE>
 __global__ void ticket_k(uint32_t *data, int words, unsigned *ticket, uint32_t *out) {
     __shared__ unsigned s_last;
@@ -135,6 +152,27 @@ int main() {
                            fence, grid, words * 4, ms * 1e3 / iters);
                 }
         CK(hipFree(data));
+    }
+    {
+        uint32_t *a, *o;
+        CK(hipMalloc(&a, 1024 * 16 * 4));
+        CK(hipMalloc(&o, 4));
+        CK(hipMemset(a, 0, 1024 * 16 * 4));
+        const int steps = 20000;
+        atomic_chain_k<<<1, 1, 0, s>>>(a, 100, o);
+        CK(hipEventRecord(e0, s));
+        atomic_chain_k<<<1, 1, 0, s>>>(a, steps, o);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"test\": \"atomic_chain\", \"ns_per_atomic\": %.1f}\n", ms * 1e6 / steps);
+        CK(hipEventRecord(e0, s));
+        lds_chain_k<<<1, 64, 0, s>>>(steps, o);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"test\": \"lds_atomic_chain\", \"ns_per_atomic\": %.1f}\n", ms * 1e6 / steps);
+        CK(hipFree(a));
     }
     // grid barrier: all blocks resident (grid <= CUs)
     unsigned *cnt, *gen, *err;

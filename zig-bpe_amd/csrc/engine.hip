@@ -57,6 +57,8 @@ void Engine::release() {
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_sizes);
+    f(d_enc_cnt); f(d_enc_ctr);
+    d_enc_cnt = nullptr; d_enc_ctr = nullptr; enc_cnt_cap = enc_ctr_cap = 0;
     for (auto &e : bev) if (e) (void)hipEventDestroy(e);
     bev.clear();
     if (h_st) (void)hipHostFree(h_st);
@@ -595,6 +597,18 @@ zbpe_status Engine::bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms,
     return ZBPE_OK;
 }
 
+// a self pair (a, a) walks a's occurrence list when the lists describe the stream, no shard edge
+// is involved and the list is short against the stream (self_list_ratio; the stream form costs
+// three passes over it)
+bool Engine::self_list_ok(uint32_t a, bool training) {
+    if (!lists_on || dist() || self_list_ratio == 0 || (training && !h_st->lists_valid)) return false;
+    uint32_t len = NO_LIST;
+    if (hipMemcpyAsync(&len, T.lst_len + a, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        return false;
+    return len != NO_LIST && (uint64_t)len * self_list_ratio < (uint64_t)n_slots;
+}
+
 // persistent grid: as many blocks as are resident at once, fewer for short streams
 int Engine::scan_grid(int64_t slots) const {
     const int unroll = kScanUnroll[scan_variant];
@@ -1000,6 +1014,11 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         stats.scan_launches++;
     } else {
         stats.self_pair_merges++;
+        if (self_list_ok(a, true)) {
+            zbpe_scan_self_list<<<scan_grid(n_slots), SCAN_THREADS, 0, stream>>>(A);
+            LAUNCH_OK();
+            stats.list_scans++;
+        } else {
         const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);
         CHECK(ensure(&d_tile_fn, tile_fn_cap, ntiles, "self tiles"));
         CHECK(ensure(&d_carry, carry_cap, ntiles, "self carry"));
@@ -1016,6 +1035,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         LAUNCH_OK();
         zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
         LAUNCH_OK();
+        }
     }
     HIP_OK(hipEventRecord(ev[1], stream));
     // ---- exchange: sum the count deltas of all shards (one RCCL all-reduce per merge) ---------------
@@ -1185,13 +1205,59 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
     const uint32_t reccap = (uint32_t)(use_lists ? lists_cap : rec_cap);
     uint32_t *tail = d_delta + DELTA_WORDS - 32;  // scratch: encode keeps no counts
     uint64_t holes = 0;
-    for (size_t k = 0; k < n_merges; k++) {
+    // batched path (with lists): live token counts (exact after the list build of the fresh stream),
+    // one record counter per merge of a batch, a scratch region of n records
+    const bool batched = use_lists && enc_batch > 1;
+    if (batched) {
+        CHECK(ensure(&d_rec, rec_cap, (size_t)n + 1, "encode scratch"));
+        CHECK(ensure(&d_enc_cnt, enc_cnt_cap, 65536, "token counts"));
+        CHECK(ensure(&d_enc_ctr, enc_ctr_cap, ENC_MAX_BATCH, "batch counters"));
+        HIP_OK(hipMemsetAsync(d_enc_cnt, 0, 65536 * sizeof(int32_t), stream));
+        HIP_OK(hipMemcpyAsync(d_enc_cnt, d_list_total, vp * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream));
+        HIP_OK(hipMemsetAsync(d_enc_ctr, 0, ENC_MAX_BATCH * sizeof(uint32_t), stream));
+    }
+    const uint32_t maxb = std::min<uint32_t>(enc_batch, ENC_MAX_BATCH);
+    enc_batches = 0;
+    for (size_t k = 0; k < n_merges;) {
+        if (batched && triples[3 * k] != triples[3 * k + 1]) {
+            // greedy batch: the next merges while none uses a token an earlier one of the batch uses or makes
+            EncBatch E{};
+            uint32_t used[3 * ENC_MAX_BATCH];
+            uint32_t nused = 0;
+            auto is_used = [&](uint32_t t) { return std::find(used, used + nused, t) != used + nused; };
+            while (k < n_merges && E.nb < maxb) {
+                const uint32_t a = triples[3 * k], b = triples[3 * k + 1], X = triples[3 * k + 2];
+                if (a == b || is_used(a) || is_used(b)) break;
+                E.a[E.nb] = a;
+                E.b[E.nb] = b;
+                E.X[E.nb] = X;
+                E.nb++;
+                used[nused++] = a;
+                used[nused++] = b;
+                used[nused++] = X;
+                k++;
+            }
+            ScanArgs A{d_tok[cur], n_slots, 0, 0, d_delta, d_delta + 65536, d_st, d_rec, 0, 0, tail, tail + 1, Halo{},
+                       nullptr, vp, 0, nullptr, 0, nullptr, d_lists, T.lst_off, T.lst_len, list_ratio, 0, nullptr};
+            hipLaunchKernelGGL(zbpe_encode_scan_batch, dim3(scan_grid(n_slots), E.nb), dim3(SCAN_THREADS), 0, stream, A, E,
+                               (const int32_t *)d_enc_cnt, d_enc_ctr, d_rec);
+            LAUNCH_OK();
+            zbpe_encode_apply_batch<<<dim3(std::max<uint32_t>(8, 512 / E.nb), E.nb), 256, 0, stream>>>(
+                d_tok[cur], n_slots, E, d_rec, d_enc_cnt, d_enc_ctr, d_lists, d_st, T);
+            LAUNCH_OK();
+            enc_batches++;
+            continue;
+        }
         const uint32_t a = triples[3 * k], b = triples[3 * k + 1], X = triples[3 * k + 2];
+        k++;
         ScanArgs A{d_tok[cur], n_slots, a, b, d_delta, d_delta + 65536, d_st, recbuf, reccap, 0, tail, tail + 1, Halo{},
                    nullptr, vp, X, nullptr, 0, nullptr, use_lists ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio,
                    use_lists ? 1 : 0, nullptr};
         if (a != b) {
             CHECK(launch_scan(A));
+        } else if (use_lists && self_list_ok(a, false)) {
+            zbpe_scan_self_list<<<scan_grid(n_slots), SCAN_THREADS, 0, stream>>>(A);
+            LAUNCH_OK();
         } else {  // holes are transparent to the self-pair path
             const int64_t ntiles = std::max<int64_t>(1, (n_slots + SELF_TILE - 1) / SELF_TILE);
             CHECK(ensure(&d_tile_fn, tile_fn_cap, ntiles, "self tiles"));
@@ -1203,9 +1269,11 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
             zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
             LAUNCH_OK();
         }
-        zbpe_encode_apply<<<512, 256, 0, stream>>>(d_tok[cur], n_slots, recbuf, reccap, use_lists ? 1 : 0, X, d_st, T, tail);
+        zbpe_encode_apply<<<512, 256, 0, stream>>>(d_tok[cur], n_slots, recbuf, reccap, use_lists ? 1 : 0, X, d_st, T, tail,
+                                                   batched ? d_enc_cnt : nullptr, a, b);
         LAUNCH_OK();
-        if (!use_lists && (k & 255) == 255) {  // without lists: squeeze the holes now and then
+        enc_batches++;
+        if (!use_lists && (k & 255) == 0) {  // without lists: squeeze the holes now and then
             CHECK(sync_state());
             holes += h_st->total_occ;
             n_live -= h_st->total_occ;

@@ -104,11 +104,19 @@ struct Engine {
     int list_grid = 0;          // scan grid after such a batch (option "list_grid"; 0 = the full grid)
     int list_mode = 1;          // 0: never build lists, 1: once pair counts are small against the stream
     uint32_t list_ratio = 256;  // list scan when list length * ratio < stream slots
+    uint32_t self_list_ratio = 8;  // self pair from a's list when length * ratio < stream slots (0: never)
     uint64_t list_start = 64;   // build lists at a compaction once top count * list_start < live tokens (0: always)
     // per-merge trace (option "trace"), ZBPE_TRACE_COLS floats per merge
     bool trace_on = false;
     std::vector<float> trace;
     std::vector<int32_t> scan_log;  // per pair-scan launch of the last train (zbpe_scan_log)
+    // encode: merges applied per launch pair (option "encode_batch"; 1 = one merge at a time)
+    uint32_t enc_batch = 32;
+    uint64_t enc_batches = 0;       // launch pairs of the last encode
+    int32_t *d_enc_cnt = nullptr;   // live count per token
+    size_t enc_cnt_cap = 0;
+    uint32_t *d_enc_ctr = nullptr;  // records per merge of the batch
+    size_t enc_ctr_cap = 0;
     // device-resident merge loop
     uint32_t merge_batch = 32;      // merges enqueued per host sync (1: synchronous loop)
     uint32_t merge_timing = 8;     // HIP events around every merge_timing-th merge of a batch (0: none)
@@ -175,6 +183,7 @@ struct Engine {
     int argmax_blocks(uint32_t X) const;
     int scan_grid(int64_t slots) const;
     zbpe_status launch_scan(const ScanArgs &A, int grid = 0);
+    bool self_list_ok(uint32_t a, bool training);
     zbpe_status rebuild_hot();
     zbpe_status rebuild_home(uint64_t cap);
     zbpe_status select_ready();

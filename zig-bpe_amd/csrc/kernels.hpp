@@ -332,6 +332,7 @@ struct ScanArgs {
     uint32_t list_ratio;    // list scan when list length * list_ratio < stream slots
     int rec_arena;          // records at rec + st->arena_top (they become the new token's list)
     MergeLog *log;          // batch mode: the scan records its mode in log[X - 256]
+    uint32_t *rec_ctr;      // record counter (nullptr: st->rec_count); batched encode: one per merge
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // the device-held parts of the arguments: pair (batch mode), halo (batch mode, multi-GPU), record
@@ -354,7 +355,7 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
     }
     return ScanArgs{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
                     A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
-                    A0.log};
+                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count};
 }
 
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
@@ -490,7 +491,7 @@ __device__ inline void wave_flush_records(const ScanArgs &A, const uint32_t *rec
     const int lane = threadIdx.x & 63;
     uint32_t base = 0;
     if (lane == 0) {
-        base = atomicAdd(&A.st->rec_count, n);
+        base = atomicAdd(A.rec_ctr, n);
         atomicAdd(A.occ_out, n);
     }
     base = (uint32_t)__shfl((int)base, 0);
@@ -665,11 +666,10 @@ template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S);
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
                                                                      uint32_t len, ScanLds &S);
-template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false>
-__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
-    if (A0.dyn && A0.st->halt) return;
-    __shared__ ScanLds S;
-    const ScanArgs A = scan_args_resolve(A0);
+// one pair scan with resolved arguments: the list form when the shorter token list is short
+// enough, else the stream form
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
+__device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S) {
     // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
     if (A.lists && A.a != A.b && A.st->lists_valid) {
         // lengths and offsets in one round trip
@@ -688,6 +688,95 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
     scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT>(A, S);
 }
+template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false>
+__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
+    if (A0.dyn && A0.st->halt) return;
+    __shared__ ScanLds S;
+    const ScanArgs A = scan_args_resolve(A0);
+    scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT>(A, S);
+}
+
+// ------------------------------------------------------------------------------------------
+// Batched encode (Engine::encode, basic_tokenizer.zig:71-88). A batch holds consecutive merges of
+// which none uses a token that an earlier one of the batch uses or makes: their occurrences do not
+// interact, so applying them together equals applying them in rank order. One launch scans every
+// merge of the batch (grid row y = merge y), one applies them. Records go to a scratch region per
+// merge sized by min(live count of a, live count of b) (a sound bound; the batch's tokens are
+// distinct, so the regions sum to at most the live tokens), then the apply copies them to the arena,
+// where they become the new tokens' occurrence lists.
+// ------------------------------------------------------------------------------------------
+constexpr int ENC_MAX_BATCH = 32;
+struct EncBatch {
+    uint32_t a[ENC_MAX_BATCH], b[ENC_MAX_BATCH], X[ENC_MAX_BATCH];
+    uint32_t nb;
+};
+__device__ inline uint32_t enc_bound(const EncBatch &E, const int32_t *cnt, uint32_t k) {
+    return (uint32_t)max(0, min(cnt[E.a[k]], cnt[E.b[k]]));
+}
+// scratch offset and bound of merge j (every thread computes it; nb <= 32 cached loads)
+__device__ inline uint32_t enc_scratch_off(const EncBatch &E, const int32_t *cnt, uint32_t j, uint32_t *bound) {
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < j; k++) off += enc_bound(E, cnt, k);
+    *bound = enc_bound(E, cnt, j);
+    return off;
+}
+__global__ void __launch_bounds__(SCAN_THREADS) zbpe_encode_scan_batch(ScanArgs A0, EncBatch E, const int32_t *__restrict__ cnt,
+                                                                       uint32_t *ctr, uint32_t *scratch) {
+    __shared__ ScanLds S;
+    const uint32_t j = blockIdx.y;
+    uint32_t bound;
+    const uint32_t off = enc_scratch_off(E, cnt, j, &bound);
+    ScanArgs A = A0;
+    A.a = E.a[j];
+    A.b = E.b[j];
+    A.X = E.X[j];
+    A.rec = scratch + off;
+    A.rec_cap = bound;
+    A.rec_ctr = &ctr[j];
+    A.rec_arena = 0;
+    A.dyn = 0;
+    scan_dispatch<4, true, true, true, true>(A, S);
+}
+__global__ void __launch_bounds__(256) zbpe_encode_apply_batch(uint16_t *tok, int64_t n, EncBatch E, const uint32_t *__restrict__ scratch,
+                                                               int32_t *cnt, uint32_t *ctr, uint32_t *arena, DevState *st, Tables T) {
+    const uint32_t j = blockIdx.y;
+    uint32_t bound, pre = 0;
+    const uint32_t off = enc_scratch_off(E, cnt, j, &bound);
+    for (uint32_t k = 0; k < j; k++) pre += min(ctr[k], enc_bound(E, cnt, k));
+    const uint32_t m = min(ctr[j], bound), base = st->arena_top + pre, X = E.X[j];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < m; i += gridDim.x * 256) {
+        const int64_t p = scratch[off + i];
+        tok[p] = (uint16_t)X;
+        const int64_t q = next_live(tok, n, p);
+        if (q >= 0) tok[q] = HOLE;
+        arena[base + i] = (uint32_t)p;
+    }
+    __shared__ uint32_t s_last;
+    __syncthreads();  // every thread of the block has read the counts and arena_top
+    if (threadIdx.x == 0) s_last = atomicAdd(&st->ticket, 1u) == gridDim.x * gridDim.y - 1;
+    __syncthreads();
+    if (!s_last || threadIdx.x) return;
+    uint32_t top = st->arena_top, total = 0;
+    for (uint32_t k = 0; k < E.nb; k++) {
+        const uint32_t mk = min(ctr[k], enc_bound(E, cnt, k));
+        if (ctr[k] > mk) atomicOr(&st->error, 8u);
+        T.lst_off[E.X[k]] = top;
+        T.lst_len[E.X[k]] = mk;
+        top += mk;
+        total += mk;
+        ctr[k] = 0;
+    }
+    for (uint32_t k = 0; k < E.nb; k++) {  // after every bound above was read
+        const int32_t mk = (int32_t)T.lst_len[E.X[k]];
+        cnt[E.X[k]] = mk;
+        cnt[E.a[k]] -= mk;
+        cnt[E.b[k]] -= mk;
+    }
+    st->arena_top = top;
+    st->total_occ += total;
+    st->ticket = 0;
+}
+
 // List scan: every entry of the key token's list is a position that held the key when it was
 // listed; entries overwritten since (merged or turned into holes) fail the token check.
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
@@ -708,7 +797,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
         // the occurrence leaving the shard: its b is the next shard's, in no list here
         const int64_t p = prev_live(tok, A.n);
         if (p >= 0 && tok[p] == A.a && occ_slow(A, H, p, xx)) {
-            const uint32_t j = atomicAdd(&A.st->rec_count, 1u);
+            const uint32_t j = atomicAdd(A.rec_ctr, 1u);
             atomicAdd(A.occ_out, 1u);
             if (j < A.rec_cap) A.rec[j] = (uint32_t)p;
             else atomicOr(&A.st->error, 8u);
@@ -759,7 +848,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
         any = 1;
         uint32_t base = 0;
         if (lane == 0) {
-            base = atomicAdd(&A.st->rec_count, (uint32_t)__popcll(m));
+            base = atomicAdd(A.rec_ctr, (uint32_t)__popcll(m));
             atomicAdd(A.occ_out, (uint32_t)__popcll(m));
         }
         base = (uint32_t)__shfl((int)base, 0);
@@ -815,7 +904,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
         // the occurrence leaving the shard: its b is the next shard's, so no tile here holds it
         const int64_t p = prev_live(tok, A.n);
         if (p >= 0 && tok[p] == A.a && occ_slow(A, H, p, xx)) {
-            const uint32_t j = atomicAdd(&A.st->rec_count, 1u);
+            const uint32_t j = atomicAdd(A.rec_ctr, 1u);
             atomicAdd(A.occ_out, 1u);
             if (j < A.rec_cap) A.rec[j] = (uint32_t)p;
             else atomicOr(&A.st->error, 8u);
@@ -1041,7 +1130,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
                 if (sft >= 0 && sft < 16) {
                     occ |= 1ull << (16 * u + sft);
                 } else {  // a start beyond the window (hole run): record it directly
-                    const uint32_t j = atomicAdd(&A.st->rec_count, 1u);
+                    const uint32_t j = atomicAdd(A.rec_ctr, 1u);
                     atomicAdd(A.occ_out, 1u);
                     if (j < A.rec_cap) A.rec[j] = pr;
                     else atomicOr(&A.st->error, 8u);
@@ -1435,7 +1524,8 @@ __global__ void zbpe_halo_build(const Boundary *__restrict__ bnd, int rank, int 
 // encode: apply one merge at the recorded occurrences, then (last block to finish) roll the
 // counters; with occurrence lists the records, kept in the arena, become X's list
 __global__ void __launch_bounds__(256) zbpe_encode_apply(uint16_t *tok, int64_t n, uint32_t *rec, uint32_t rec_cap, int rec_arena,
-                                                         uint32_t X, DevState *st, Tables T, uint32_t *scratch) {
+                                                         uint32_t X, DevState *st, Tables T, uint32_t *scratch,
+                                                         int32_t *tcnt = nullptr, uint32_t a = 0, uint32_t b = 0) {
     const uint32_t top = rec_arena ? st->arena_top : 0;
     const uint32_t cap = rec_cap > top ? rec_cap - top : 0;
     const uint32_t cnt = min(st->rec_count, cap);
@@ -1456,6 +1546,11 @@ __global__ void __launch_bounds__(256) zbpe_encode_apply(uint16_t *tok, int64_t 
         T.lst_off[X] = top;
         T.lst_len[X] = cnt;
         st->arena_top = top + cnt;
+    }
+    if (tcnt) {  // live token counts of the batched path (a self pair consumes 2 a's per occurrence)
+        tcnt[X] = (int32_t)cnt;
+        tcnt[a] -= (int32_t)cnt;
+        tcnt[b] -= (int32_t)cnt;
     }
     st->rec_count = 0;
     st->ticket = 0;
@@ -1622,7 +1717,7 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
     const uint32_t nrec = s_nrec;
     if (nrec) {
         if (threadIdx.x == 0) {
-            s_base = atomicAdd(&A.st->rec_count, nrec);
+            s_base = atomicAdd(A.rec_ctr, nrec);
             atomicAdd(A.occ_out, nrec);
             if (A.pres) pres_set(A, beg);  // SELF_TILE == PRES_BLK: the tile is one presence block
         }
@@ -1639,6 +1734,76 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
             uint32_t l = s_left[i], r = s_right[i];
             if (l) atomicAdd(&A.left[i], l);
             if (r) atomicAdd(&A.right[i], r);
+        }
+    }
+}
+
+// Self pair (a, a) from the occurrence list of a (one GPU, or the replicas of the late phase: no
+// shard edges). A thread takes an entry that still holds a and starts a live run of a's, walks the
+// run and takes every other pair of it from the start (left-greedy, basic_tokenizer.zig:217-226),
+// with the count deltas of zbpe_scan_self: the token before the run is the first occurrence's left
+// neighbour, adjacent occurrences give (X, X), and the last one's right neighbour is the lone
+// trailing a of an odd run or the token after the run. Two walks: count, then (after one atomic per
+// wave for the records) emit. O(list length) instead of three passes over the stream.
+__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_self_list(ScanArgs A0) {
+    const ScanArgs A = scan_args_resolve(A0);
+    const uint32_t a = A.a, len = A.lst_len[a];
+    if (len == NO_LIST || (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len)) return;
+    const uint32_t *L = A.lists + A.lst_off[a];
+    __shared__ ScanLds S;
+    for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { S.left[i] = 0; S.right[i] = 0; }
+    if (threadIdx.x == 0) S.any = 0;
+    __syncthreads();
+    NeighbourHist H{S.left, S.right, A.left, A.right};
+    const uint16_t *tok = A.tok;
+    const int lane = threadIdx.x & 63;
+    uint32_t xx = 0, any = 0;
+    const uint32_t stride = gridDim.x * SCAN_THREADS, len64 = (len + 63) & ~63u;
+    for (uint32_t i = blockIdx.x * SCAN_THREADS + threadIdx.x; i - lane < len64; i += stride) {
+        int64_t p = -1, l = -1;
+        uint32_t run = 0;
+        if (i < len) {
+            p = L[i];
+            if (tok[p] == a) {
+                l = prev_live(tok, p);
+                if (l < 0 || tok[l] != a)  // the run starts here: walk it
+                    for (int64_t q = p; q >= 0 && tok[q] == a; q = next_live(tok, A.n, q)) run++;
+            }
+        }
+        const uint32_t cnt = run / 2;
+        const uint32_t incl = wave_incl_scan(cnt), total = (uint32_t)__shfl((int)incl, 63);
+        if (!total) continue;
+        any = 1;
+        uint32_t base = 0;
+        if (lane == 0) {
+            base = atomicAdd(A.rec_ctr, total);
+            atomicAdd(A.occ_out, total);
+        }
+        base = (uint32_t)__shfl((int)base, 0) + incl - cnt;
+        if (!cnt) continue;
+        if (A.count_deltas && l >= 0) H.left((uint16_t)tok[l]);
+        int64_t q = p;
+        for (uint32_t k = 0; k < cnt; k++) {
+            if (base + k < A.rec_cap) A.rec[base + k] = (uint32_t)q;
+            else atomicOr(&A.st->error, 8u);
+            q = next_live(tok, A.n, q);       // the second a of occurrence k
+            q = q >= 0 ? next_live(tok, A.n, q) : -1;  // the next live token after it
+        }
+        if (A.count_deltas) {
+            xx += cnt - 1;
+            if (run & 1) H.right((uint16_t)a);  // the lone trailing a
+            else if (q >= 0) H.right((uint16_t)tok[q]);
+        }
+    }
+    xx = wave_sum(xx);
+    if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
+    if (lane == 0 && any) S.any = 1;
+    __syncthreads();
+    if (S.any) {
+        for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) {
+            const uint32_t lft = S.left[i], rgt = S.right[i];
+            if (lft) atomicAdd(&A.left[i], lft);
+            if (rgt) atomicAdd(&A.right[i], rgt);
         }
     }
 }
