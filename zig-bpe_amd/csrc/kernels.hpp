@@ -291,18 +291,44 @@ __device__ inline int64_t prev_live(const uint16_t *tok, int64_t i) {
     return -1;
 }
 
-// LDS-privatised neighbour histograms: tokens < LDS_BINS in LDS, the rest straight to HBM.
+// LDS-privatised neighbour histograms: tokens < LDS_BINS directly in LDS; larger tokens (the merged
+// ones, the common neighbours once merges are long) in a small LDS hash of (token << 16 | count)
+// with a few linear probes, and only the rest straight to HBM. Contended global atomics on a few hot
+// neighbour tokens cost more than the whole list walk of a late merge.
+constexpr int HASH_LOG = 9;
+constexpr int HASH_BINS = 1 << HASH_LOG;
 struct NeighbourHist {
     uint32_t *lds_left, *lds_right;
     uint32_t *g_left, *g_right;
-    __device__ inline void left(uint16_t t) {
-        if (t < LDS_BINS) atomicAdd(&lds_left[t], 1u);
-        else atomicAdd(&g_left[t], 1u);
+    uint32_t *h_left = nullptr, *h_right = nullptr;  // nullptr: no hash (large tokens go to HBM)
+    __device__ static inline void add(uint32_t *lds, uint32_t *h, uint32_t *g, uint16_t t) {
+        if (t < LDS_BINS) {
+            atomicAdd(&lds[t], 1u);
+            return;
+        }
+        if (h) {
+            uint32_t s = ((uint32_t)t * 2654435761u) >> (32 - HASH_LOG);
+            for (int k = 0; k < 4; k++, s = (s + 1) & (HASH_BINS - 1)) {
+                uint32_t e = h[s];
+                if (e == 0) {
+                    e = atomicCAS(&h[s], 0u, ((uint32_t)t << 16) | 1u);
+                    if (e == 0) return;
+                }
+                if ((e >> 16) == t) {
+                    // 16-bit count: every 2^15 increments one thread moves 2^15 to HBM
+                    const uint32_t old = atomicAdd(&h[s], 1u);
+                    if ((old & 0xffffu) == 0x7fffu) {
+                        atomicSub(&h[s], 0x8000u);
+                        atomicAdd(&g[t], 0x8000u);
+                    }
+                    return;
+                }
+            }
+        }
+        atomicAdd(&g[t], 1u);
     }
-    __device__ inline void right(uint16_t t) {
-        if (t < LDS_BINS) atomicAdd(&lds_right[t], 1u);
-        else atomicAdd(&g_right[t], 1u);
-    }
+    __device__ inline void left(uint16_t t) { add(lds_left, h_left, g_left, t); }
+    __device__ inline void right(uint16_t t) { add(lds_right, h_right, g_right, t); }
 };
 
 struct ScanArgs {
@@ -659,9 +685,28 @@ __device__ inline bool resolve_candidate(const ScanArgs &A, NeighbourHist &H, in
 // LDS neighbour histograms of one scan workgroup, shared by the stream and list forms (one allocation)
 struct ScanLds {
     uint32_t left[LDS_BINS], right[LDS_BINS];
+    uint32_t hleft[HASH_BINS], hright[HASH_BINS];
     uint32_t any;
     unsigned long long scanned;
 };
+// zero the workgroup's neighbour histograms (every thread calls it, then a barrier)
+__device__ inline void scan_lds_clear(ScanLds &S) {
+    for (int i = threadIdx.x; i < LDS_BINS; i += blockDim.x) { S.left[i] = 0; S.right[i] = 0; }
+    for (int i = threadIdx.x; i < HASH_BINS; i += blockDim.x) { S.hleft[i] = 0; S.hright[i] = 0; }
+}
+// add the workgroup's neighbour histograms to the global deltas (every thread calls it)
+__device__ inline void scan_lds_flush(ScanLds &S, uint32_t *g_left, uint32_t *g_right) {
+    for (int i = threadIdx.x; i < LDS_BINS; i += blockDim.x) {
+        const uint32_t l = S.left[i], r = S.right[i];
+        if (l) atomicAdd(&g_left[i], l);
+        if (r) atomicAdd(&g_right[i], r);
+    }
+    for (int i = threadIdx.x; i < HASH_BINS; i += blockDim.x) {
+        const uint32_t l = S.hleft[i], r = S.hright[i];
+        if (l) atomicAdd(&g_left[l >> 16], l & 0xffffu);
+        if (r) atomicAdd(&g_right[r >> 16], r & 0xffffu);
+    }
+}
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S);
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
@@ -785,10 +830,10 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     if (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len) return;
     uint32_t *s_left = S.left, *s_right = S.right;
     uint32_t &s_any = S.any;
-    for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
+    scan_lds_clear(S);
     if (threadIdx.x == 0) s_any = 0;
     __syncthreads();
-    NeighbourHist H{s_left, s_right, A.left, A.right};
+    NeighbourHist H{s_left, s_right, A.left, A.right, S.hleft, S.hright};
     const uint16_t *tok = A.tok;
     const uint32_t key = by_b ? A.b : A.a;
     uint32_t xx = 0, any = 0;
@@ -807,68 +852,93 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     const uint32_t stride = gridDim.x * SCAN_THREADS;
     const int64_t nvec = (A.n + 7) / 8;
     const uint32_t len64 = (len + 63) & ~63u;  // wave-uniform trip count (wave_append)
-    for (uint32_t i = blockIdx.x * SCAN_THREADS + threadIdx.x; i - lane < len64; i += stride) {
-        bool hit = false;
-        uint32_t pr = 0;
-        if (i < len) {
-            // the entry's window (its 16-B vector and the neighbouring words) in one round trip; the
-            // entry counts only if it still holds the key token
-            const int64_t p = L[i];
-            const int64_t vi = p >> 3;
-            const int k = (int)(p & 7);
-            const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
-            const uint32_t pw = vi > 0 ? tv[vi - 1].w : 0xffffffffu;
-            const uint4 cv = tv[vi];
-            uint32_t nx = 0xffffffffu, ny = 0xffffffffu;
-            if (vi + 1 < nvec) {
-                const uint4 nv = tv[vi + 1];
-                nx = nv.x;
-                ny = nv.y;
+    // LU entries per thread in flight: their list words, then their 16-B vectors (one request each,
+    // clamped addresses, no branches); an entry that still holds the key and whose partner slot inside
+    // the vector is the other token or a hole (or lies outside the vector) loads the neighbouring
+    // words too and is resolved. Most entries end after the one vector load.
+    constexpr int LU = 3;
+    const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
+    for (uint32_t i0 = blockIdx.x * SCAN_THREADS + threadIdx.x; i0 - lane < len64; i0 += LU * stride) {
+        int64_t ps[LU];
+#pragma unroll
+        for (int u = 0; u < LU; u++) {
+            const uint32_t i = i0 + u * stride;
+            const uint32_t e = L[i < len ? i : len - 1];
+            ps[u] = i < len ? (int64_t)e : -1;
+        }
+        uint4 cvs[LU];
+#pragma unroll
+        for (int u = 0; u < LU; u++) cvs[u] = tv[(ps[u] < 0 ? 0 : ps[u]) >> 3];
+#pragma unroll 1
+        for (int u = 0; u < LU; u++) {
+            // this entry's values (selects, not an indexed private array)
+            int64_t p = ps[0];
+            uint4 cv = cvs[0];
+#pragma unroll
+            for (int k2 = 1; k2 < LU; k2++)
+                if (u == k2) { p = ps[k2]; cv = cvs[k2]; }
+            bool cand = false;
+            if (p >= 0) {
+                const int k = (int)(p & 7);
+                if (tok_at(cv, k) == key) {
+                    const uint32_t t = !by_b ? (k < 7 ? tok_at(cv, k + 1) : A.b) : (k > 0 ? tok_at(cv, k - 1) : A.a);
+                    cand = t == HOLE || t == (by_b ? A.a : A.b);
+                }
             }
-            if (tok_at(cv, k) == key) {
-                if (!by_b) {
-                    pr = (uint32_t)p;
-                    hit = occ_window(A, H, vi, 1u << k, xx, pw, cv, nx, ny) != 0;
-                } else {
-                    int j = k - 1;  // the live token before p inside the vector
-                    while (j >= 0 && tok_at(cv, j) == HOLE) j--;
-                    if (j >= 0) {
-                        if (tok_at(cv, j) == A.a && occ_window(A, H, vi, 1u << j, xx, pw, cv, nx, ny)) {
-                            pr = (uint32_t)(vi * 8 + j);
-                            hit = true;
-                        }
+            uint32_t pw = 0xffffffffu, nx = 0xffffffffu, ny = 0xffffffffu;
+            if (cand) {
+                const int64_t vi = p >> 3;
+                if (vi > 0) pw = tv[vi - 1].w;
+                if (vi + 1 < nvec) {
+                    const uint2 nv = *reinterpret_cast<const uint2 *>(&tv[vi + 1]);
+                    nx = nv.x;
+                    ny = nv.y;
+                }
+            }
+            bool hit = false;
+            uint32_t pr = 0;
+            if (cand) {
+                const int64_t vi = p >> 3;
+                const int k = (int)(p & 7);
+                {
+                    if (!by_b) {
+                        pr = (uint32_t)p;
+                        hit = occ_window(A, H, vi, 1u << k, xx, pw, cv, nx, ny) != 0;
                     } else {
-                        hit = resolve_candidate(A, H, p, by_b, nvec, xx, pr);
+                        int j = k - 1;  // the live token before p inside the vector
+                        while (j >= 0 && tok_at(cv, j) == HOLE) j--;
+                        if (j >= 0) {
+                            if (tok_at(cv, j) == A.a && occ_window(A, H, vi, 1u << j, xx, pw, cv, nx, ny)) {
+                                pr = (uint32_t)(vi * 8 + j);
+                                hit = true;
+                            }
+                        } else {
+                            hit = resolve_candidate(A, H, p, by_b, nvec, xx, pr);
+                        }
                     }
                 }
             }
-        }
-        const uint64_t m = __ballot(hit);
-        if (!m) continue;
-        any = 1;
-        uint32_t base = 0;
-        if (lane == 0) {
-            base = atomicAdd(A.rec_ctr, (uint32_t)__popcll(m));
-            atomicAdd(A.occ_out, (uint32_t)__popcll(m));
-        }
-        base = (uint32_t)__shfl((int)base, 0);
-        if (hit) {
-            const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (j < A.rec_cap) A.rec[j] = pr;
-            else atomicOr(&A.st->error, 8u);
+            const uint64_t m = __ballot(hit);
+            if (!m) continue;
+            any = 1;
+            uint32_t base = 0;
+            if (lane == 0) {
+                base = atomicAdd(A.rec_ctr, (uint32_t)__popcll(m));
+                atomicAdd(A.occ_out, (uint32_t)__popcll(m));
+            }
+            base = (uint32_t)__shfl((int)base, 0);
+            if (hit) {
+                const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (j < A.rec_cap) A.rec[j] = pr;
+                else atomicOr(&A.st->error, 8u);
+            }
         }
     }
     xx = wave_sum(xx);
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     if (lane == 0 && any) s_any = 1;
     __syncthreads();
-    if (s_any) {
-        for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) {
-            uint32_t l = s_left[i], r = s_right[i];
-            if (l) atomicAdd(&A.left[i], l);
-            if (r) atomicAdd(&A.right[i], r);
-        }
-    }
+    if (s_any) scan_lds_flush(S, A.left, A.right);
 }
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S) {
@@ -880,14 +950,14 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
     __shared__ uint32_t s_rec[SCAN_THREADS / 64][WREC];
     // a wave's current tile, staged in LDS when it holds candidates: phase 2 reads its windows here
     __shared__ uint4 s_tile[SCAN_THREADS / 64][64 * UNROLL];
-    constexpr uint32_t CAND_CAP = COMPACT ? 256 : 1;  // compacted form: candidates resolved per round per wave
+    constexpr uint32_t CAND_CAP = COMPACT ? 128 : 1;  // compacted form: candidates resolved per round per wave
     __shared__ uint32_t s_cand[SCAN_THREADS / 64][CAND_CAP];
     uint32_t &s_any = S.any;
     unsigned long long &s_scanned = S.scanned;
-    for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { s_left[i] = 0; s_right[i] = 0; }
+    scan_lds_clear(S);
     if (threadIdx.x == 0) { s_any = 0; s_scanned = 0; }
     __syncthreads();
-    NeighbourHist H{s_left, s_right, A.left, A.right};
+    NeighbourHist H{s_left, s_right, A.left, A.right, S.hleft, S.hright};
     const uint16_t *tok = A.tok;
     const int64_t nvec = (A.n + 7) / 8;
     constexpr int WT_VEC = 64 * UNROLL;  // vectors per wave-tile
@@ -1179,13 +1249,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
     if (lane == 0 && tiles) atomicAdd(&s_scanned, (unsigned long long)tiles * WT_VEC * 8);
     __syncthreads();
     if (threadIdx.x == 0 && s_scanned) atomicAdd(&A.st->scanned_slots, s_scanned);
-    if (s_any) {
-        for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) {
-            uint32_t l = s_left[i], r = s_right[i];
-            if (l) atomicAdd(&A.left[i], l);
-            if (r) atomicAdd(&A.right[i], r);
-        }
-    }
+    if (s_any) scan_lds_flush(S, A.left, A.right);
 }
 
 // Presence bitmap from the stream: one workgroup per PRES_GROUP blocks, a bitset per block in LDS
@@ -1751,10 +1815,10 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_self_list(ScanArgs A0)
     if (len == NO_LIST || (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len)) return;
     const uint32_t *L = A.lists + A.lst_off[a];
     __shared__ ScanLds S;
-    for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) { S.left[i] = 0; S.right[i] = 0; }
+    scan_lds_clear(S);
     if (threadIdx.x == 0) S.any = 0;
     __syncthreads();
-    NeighbourHist H{S.left, S.right, A.left, A.right};
+    NeighbourHist H{S.left, S.right, A.left, A.right, S.hleft, S.hright};
     const uint16_t *tok = A.tok;
     const int lane = threadIdx.x & 63;
     uint32_t xx = 0, any = 0;
@@ -1799,13 +1863,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_self_list(ScanArgs A0)
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     if (lane == 0 && any) S.any = 1;
     __syncthreads();
-    if (S.any) {
-        for (int i = threadIdx.x; i < LDS_BINS; i += SCAN_THREADS) {
-            const uint32_t lft = S.left[i], rgt = S.right[i];
-            if (lft) atomicAdd(&A.left[i], lft);
-            if (rgt) atomicAdd(&A.right[i], rgt);
-        }
-    }
+    if (S.any) scan_lds_flush(S, A.left, A.right);
 }
 
 // ------------------------------------------------------------------------------------------
