@@ -121,6 +121,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "trace") e.trace_on = value != 0;
     else if (k == "merge_batch" && value >= 1) e.merge_batch = (uint32_t)std::min<int64_t>(value, zbpe::MAX_BATCH);
     else if (k == "merge_timing" && value >= 0) e.merge_timing = (uint32_t)value;
+    else if (k == "sel_prof" && value >= 0) e.sel_prof = (uint32_t)value;
     else if (k == "replace_split") e.replace_split = value != 0;
     else if (k == "fused_select") e.fused_select = value != 0;
     else if (k == "replicate_late") e.replicate_late = value != 0;

@@ -800,6 +800,15 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         stats.sum_tokens = v[1];
         HIP_OK(hipMemsetAsync(d_w, 0, 32, stream));
     }
+    if (sel_prof) {  // wall_clock64 runs at 100 MHz
+        HIP_OK(hipMemcpy(h_st, d_st, sizeof(DevState), hipMemcpyDeviceToHost));
+        const unsigned long long *P = h_st->sel_prof;
+        const double calls = std::max(1.0, (double)P[7]), us = 0.01;
+        fprintf(stderr, "sel_prof: %llu last-block calls; avg us: argmax+ticket %.2f, reduce %.2f, finish+begin %.2f, "
+                        "tie gather %.2f, decide %.2f; argmax blocks done %.2f, refresh blocks done %.2f\n",
+                P[7], P[0] * us / calls, P[1] * us / calls, P[2] * us / calls, P[3] * us / calls, P[4] * us / calls,
+                P[5] * us / calls, P[6] * us / calls);
+    }
     stats.total_s = now_s() - t_start;
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
     stats.distinct_pairs = (uint64_t)std::max(h_st->live, 0);
@@ -902,7 +911,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)lists_cap, d_log}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
-                       dist() ? world : 1};
+                       dist() ? world : 1, (int)sel_prof};
             zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, d_delta, X, N);
             LAUNCH_OK();
         } else {

@@ -119,6 +119,7 @@ struct Engine {
     size_t enc_ctr_cap = 0;
     // device-resident merge loop
     uint32_t merge_batch = 32;      // merges enqueued per host sync (1: synchronous loop)
+    uint32_t sel_prof = 0;          // phase timestamps inside zbpe_select_next (printed to stderr after train)
     uint32_t merge_timing = 8;     // HIP events around every merge_timing-th merge of a batch (0: none)
     bool replace_split = false;     // profiling: apply and count update as separate launches
     bool fused_select = true;       // zbpe_select_next: the select of merge X also starts merge X+1 (ties included)

@@ -2197,13 +2197,19 @@ __global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st,
 constexpr int REFRESH_THREADS = 1024;
 // one super-block (all threads of the block call it). wt: write-through (sc1) stores, for a reader
 // in another workgroup of the same launch
-__device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslots, uint32_t nb, Summ *__restrict__ summ,
-                                     Summ *__restrict__ sup, bool wt) {
+__device__ inline uint64_t home_dirty_bits(const Tables &T, uint32_t sb) {
     static_assert(SUPER_BLOCKS == 64, "two dirty-bitmap words per super-block");
-    const uint64_t bits = (uint64_t)T.home_dirty[2 * sb] | ((uint64_t)T.home_dirty[2 * sb + 1] << 32);
+    const uint2 w = *reinterpret_cast<const uint2 *>(T.home_dirty + 2 * sb);
+    return (uint64_t)w.x | ((uint64_t)w.y << 32);
+}
+__device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslots, uint32_t nb, Summ *__restrict__ summ,
+                                     Summ *__restrict__ sup, bool wt, uint64_t bits) {
     if (!bits) return;
     __shared__ Summ s_new[SUPER_BLOCKS];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
+    // wave 0: the clean blocks' summaries, loaded while the dirty ones are composed
+    Summ old{0, 0};
+    if (wave == 0 && sb * SUPER_BLOCKS + lane < nb && !((bits >> lane) & 1)) old = summ[sb * SUPER_BLOCKS + lane];
     const int ndirty = __popcll(bits);
     for (int k = wave; k < ndirty; k += nwaves) {
         uint64_t m = bits;  // k-th set bit
@@ -2243,7 +2249,7 @@ __device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslo
     if (wave == 0) {
         const uint32_t bi = lane, blk = sb * SUPER_BLOCKS + bi;
         Summ x{0, 0};
-        if (blk < nb) x = ((bits >> bi) & 1) ? s_new[bi] : summ[blk];
+        if (blk < nb) x = ((bits >> bi) & 1) ? s_new[bi] : old;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             Summ y;
@@ -2271,7 +2277,7 @@ __global__ void __launch_bounds__(REFRESH_THREADS) zbpe_home_refresh(Tables T, D
                                                                      Summ *__restrict__ summ, Summ *__restrict__ sup,
                                                                      int dyn) {
     if (tie_skip(st, dyn)) return;
-    refresh_super(T, blockIdx.x, nslots, nb, summ, sup, false);
+    refresh_super(T, blockIdx.x, nslots, nb, summ, sup, false, home_dirty_bits(T, blockIdx.x));
 }
 // super-block summaries: one wave composes SUPER_BLOCKS block summaries
 __global__ void __launch_bounds__(256) zbpe_super_summary(const Summ *__restrict__ summ, uint32_t nb, Summ *__restrict__ sup,
@@ -2606,14 +2612,23 @@ struct NextArgs {
     uint32_t *lastpair;   // [1] count of the stream's last pair (one GPU)
     const Boundary *bnd;  // multi-GPU: boundary records (the stream's last pair on ties)
     int world;
+    int prof;             // option sel_prof: accumulate phase times into st->sel_prof
 };
-// every thread of the block calls it after its last global store of the phase; true in the last block
+// sel_prof: add the ticks since *t to st->sel_prof[k] (one thread; fire-and-forget atomic)
+__device__ inline void sel_tick(DevState *st, int k, unsigned long long *t) {
+    const unsigned long long now = wall_clock64();
+    atomicAdd(&st->sel_prof[k], now - *t);
+    *t = now;
+}
+// every thread of the block calls it after its last global store of the phase; true in the last block.
+// Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
+// relaxed atomic stores) and is drained here, so no release fence (an L2 writeback, 1.7-6.5 us on
+// the critical path) is needed; the last block's acquire drops its CU's stale L1 lines
+// (cdna_hip_programming.md section 6 G16; MI355X_MICROARCH.md fence table)
 __device__ inline bool block_ticket_last(uint32_t *ticket, uint32_t nblocks, uint32_t *s_flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool last = t == nblocks - 1;
         if (last) {
@@ -2637,17 +2652,23 @@ __device__ inline MaxRec block_max(MaxRec r, MaxRec *sm) {
 __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevState *st, MaxRec *__restrict__ partial,
                                                                  const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
                                                                  uint32_t X, NextArgs N) {
+    // blocks [0, nref) refresh the home super-blocks (the longest role: dispatched first, one
+    // workgroup per CU at this kernel's VGPR count), blocks [nref, nref + sel_blocks) run the argmax
+    const uint32_t nref = N.V.C ? N.V.nsb : 0u;
+    const uint64_t rbits = blockIdx.x < nref ? home_dirty_bits(T, blockIdx.x) : 0ull;  // in flight with the halt load
     if (st->halt) return;
     __shared__ MaxRec sm[NEXT_THREADS / WAVE];
     __shared__ uint32_t s_flag, s_nc, s_h, s_tie, s_len, s_ntb, s_ovf;
     __shared__ uint32_t s_key[NEXT_CAND];
     __shared__ uint32_t s_pc[NEXT_MAX_SEL], s_pt[NEXT_MAX_SEL];
     const uint32_t tid = threadIdx.x;
-    if (blockIdx.x < N.sel_blocks) {
+    if (N.prof && blockIdx.x == 0 && tid == 0) st->sel_t0 = wall_clock64();
+    const uint32_t bx = blockIdx.x - nref;  // argmax block index
+    if (blockIdx.x >= nref) {
         const uint32_t G = N.sel_blocks * NEXT_THREADS;
-        for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += G) delta[t] = 0;
+        for (uint32_t t = bx * NEXT_THREADS + tid; t < 2 * X; t += G) delta[t] = 0;
         const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
-        if (blockIdx.x == 0 && tid >= 64 && tid < 128 && N.world == 1) {
+        if (bx == 0 && tid >= 64 && tid < 128 && N.world == 1) {
             // wave 1 of block 0: the count of the stream's last pair (a tie needs it: Zig map capacity)
             const uint32_t lane = tid - 64;
             uint32_t lt[2] = {HOLE, HOLE};
@@ -2662,14 +2683,16 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
                     lt[got++] = (uint32_t)__shfl((int)t, l);
                 }
             }
-            if (lane == 0) N.lastpair[0] = got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0u;
+            if (lane == 0)
+                __hip_atomic_store(N.lastpair, got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
         // four hot entries per thread per step, every load of a step issued together
         MaxRec r{0, 0, NO_ID};
         uint32_t ids[4] = {NO_ID, NO_ID, NO_ID, NO_ID}, cs[4] = {0, 0, 0, 0};
         bool one_step = true;
-        for (uint32_t i0 = blockIdx.x * NEXT_THREADS + tid; i0 < nh; i0 += 4 * G) {
-            one_step = i0 == blockIdx.x * NEXT_THREADS + tid;
+        for (uint32_t i0 = bx * NEXT_THREADS + tid; i0 < nh; i0 += 4 * G) {
+            one_step = i0 == bx * NEXT_THREADS + tid;
 #pragma unroll
             for (int u = 0; u < 4; u++) ids[u] = i0 + u * G < nh ? T.hot[i0 + u * G] : NO_ID;
 #pragma unroll
@@ -2691,7 +2714,7 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
                     }
                 }
             } else {
-                for (uint32_t i = blockIdx.x * NEXT_THREADS + tid; i < nh; i += G) {
+                for (uint32_t i = bx * NEXT_THREADS + tid; i < nh; i += G) {
                     const uint32_t id = T.hot[i];
                     if (T.id_cnt[id] == R.cnt) {
                         const uint32_t j = atomicAdd(&s_nc, 1u);
@@ -2701,15 +2724,30 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
             }
         }
         __syncthreads();
-        if (tid < min(s_nc, (uint32_t)NEXT_CAND)) N.cand[blockIdx.x * NEXT_CAND + tid] = s_key[tid];
+        // write-through stores: the last block reads them (block_ticket_last)
+        if (tid < min(s_nc, (uint32_t)NEXT_CAND))
+            __hip_atomic_store(&N.cand[bx * NEXT_CAND + tid], s_key[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (tid == 0) {
-            partial[blockIdx.x] = MaxRec{R.cnt, R.cnt ? s_nc : 0u, R.id};
-            N.pkey[blockIdx.x] = s_nc == 1 ? s_key[0] : NO_ID;  // the key of a block's unique max
+            __hip_atomic_store(&partial[bx].cnt, R.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&partial[bx].ties, R.cnt ? s_nc : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&partial[bx].id, R.id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the key of a block's unique max
+            __hip_atomic_store(&N.pkey[bx], s_nc == 1 ? s_key[0] : NO_ID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     } else if (N.V.C) {
-        refresh_super(T, blockIdx.x - N.sel_blocks, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), false);
+        refresh_super(T, blockIdx.x, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), true, rbits);
     }
+    if (N.prof && tid == 0) atomicMax(blockIdx.x >= nref ? &st->sel_ta : &st->sel_tr, (unsigned long long)wall_clock64());
     if (!block_ticket_last(&st->ticket, gridDim.x, &s_flag)) return;
+    unsigned long long pt = 0;
+    if (N.prof && tid == 0) {
+        pt = st->sel_t0;
+        atomicAdd(&st->sel_prof[5], st->sel_ta - pt);
+        if (st->sel_tr) atomicAdd(&st->sel_prof[6], st->sel_tr - pt);
+        st->sel_ta = st->sel_tr = 0;
+        sel_tick(st, 0, &pt);
+        atomicAdd(&st->sel_prof[7], 1ull);
+    }
     // ---- the last block: argmax, roll of merge X -------------------------------------------------
     MaxRec q{0, 0, NO_ID};
     for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
@@ -2724,6 +2762,7 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
             if (s_pc[b] == Q.cnt) s_key[0] = N.pkey[b];
     }
     __syncthreads();
+    if (N.prof && tid == 0) sel_tick(st, 1, &pt);
     if (tid == 0) {
         select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, Q.ties == 1 && Q.cnt ? s_key[0] : NO_ID,
                       N.world == 1 ? N.lastpair[0] : NO_ID);
@@ -2740,6 +2779,7 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
         s_ovf = 0;
     }
     __syncthreads();
+    if (N.prof && tid == 0) sel_tick(st, 2, &pt);
     if (s_h || !s_tie) return;
     // ---- merge X+1 ties: gather the keys of the blocks whose max is the top count ----------------
     const uint32_t top = Q.cnt, total = Q.ties;
@@ -2811,7 +2851,9 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
     // ---- merge X+1 ties: the Zig-order decision, by this block (the list and the refreshed home
     // summaries are this block's writes or were published before its ticket) -------------------------
     __syncthreads();
+    if (N.prof && tid == 0) sel_tick(st, 3, &pt);
     decide_body<NEXT_THREADS>(st, N.tie_list, total, total, N.V, N.B.log, 1);
+    if (N.prof && tid == 0) sel_tick(st, 4, &pt);
 }
 
 // rebuild the home histogram for a new Zig capacity

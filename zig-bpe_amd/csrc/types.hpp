@@ -62,6 +62,10 @@ struct DevState {
     long long live_tokens;   // live tokens of this shard (rolled by zbpe_select)
     uint32_t arena_top;      // arena entries in use (lists, then this merge's records)
     uint32_t scan_mode;      // last pair scan: 0 streamed the token stream, 1 walked an occurrence list
+    uint32_t pad4;
+    // option sel_prof: zbpe_select_next phase times (wall_clock64 ticks, summed over merges)
+    unsigned long long sel_t0, sel_ta, sel_tr;  // start; latest argmax / refresh block finish
+    unsigned long long sel_prof[8];
 };
 // why a device-resident batch stopped (the host finishes that merge on the synchronous path)
 enum HaltReason : uint32_t {
