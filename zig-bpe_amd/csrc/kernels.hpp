@@ -2092,6 +2092,25 @@ __device__ inline Summ summ_slot(uint32_t k) {
     const int32_t q = (int32_t)k - 1;
     return Summ{q, q > 0 ? q : 0};
 }
+// summ_cat(x, summ_slot(k)) for x.m >= 0, which every summary has (summ_slot and summ_cat keep m >= 0):
+// max(max(k - 1, 0), x.m + k - 1) = max(0, x.m + k - 1)
+__device__ inline Summ slot_fold(Summ x, uint32_t k) {
+    const int32_t d = (int32_t)k - 1;
+    return Summ{x.q + d, max(0, x.m + d)};
+}
+// the summary of 64 consecutive slots (16 words of 4 one-byte home counts): q from byte sums
+// (v_sad_u8, one per word), m by the slot_fold recurrence
+__device__ inline Summ fold64(const uint32_t (&w)[16]) {
+    uint32_t ks = 0;
+    int32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        ks = __builtin_amdgcn_sad_u8(w[j], 0u, ks);
+#pragma unroll
+        for (int b = 0; b < 4; b++) m = max(0, m + (int32_t)((w[j] >> (8 * b)) & 0xffu) - 1);
+    }
+    return Summ{(int32_t)ks - 64, m};
+}
 __device__ inline uint32_t home_at(const uint32_t *hc, uint32_t s) { return (hc[s >> 2] >> (8 * (s & 3))) & 0xffu; }
 
 __device__ inline bool tie_skip(const DevState *st, int dyn) { return dyn && (st->halt || !st->tie_on); }
@@ -2178,7 +2197,7 @@ __global__ void __launch_bounds__(256) zbpe_home_summary(Tables T, DevState *st,
             const uint32_t end = min(nslots, beg + PER);
             for (uint32_t s = beg; s < end; s += 4) {
                 const uint32_t word = T.home_cnt[s >> 2];
-                for (int k = 0; k < 4 && s + k < end; k++) acc = summ_cat(acc, summ_slot((word >> (8 * k)) & 0xffu));
+                for (int k = 0; k < 4 && s + k < end; k++) acc = slot_fold(acc, ((word >> (8 * k)) & 0xffu));
             }
         }
         sm[threadIdx.x] = acc;
@@ -2217,7 +2236,16 @@ __device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslo
         const uint32_t bi = (uint32_t)__builtin_ctzll(m), blk = sb * SUPER_BLOCKS + bi;
         const uint32_t s0 = blk * SUMM_SLOTS + 64 * lane;
         Summ x{0, 0};
-        if (s0 < nslots) {
+        if (s0 + 64 <= nslots) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(T.home_cnt + s0 / 4);
+            uint32_t w[16];
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const uint4 q = p[v];
+                w[4 * v] = q.x; w[4 * v + 1] = q.y; w[4 * v + 2] = q.z; w[4 * v + 3] = q.w;
+            }
+            x = fold64(w);
+        } else if (s0 < nslots) {
             const uint4 *p = reinterpret_cast<const uint4 *>(T.home_cnt + s0 / 4);
 #pragma unroll
             for (int v = 0; v < 4; v++) {
@@ -2225,7 +2253,7 @@ __device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslo
                 const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                 for (int kk = 0; kk < 16; kk++)
-                    if (s0 + 16 * v + kk < nslots) x = summ_cat(x, summ_slot((w[kk >> 2] >> (8 * (kk & 3))) & 0xffu));
+                    if (s0 + 16 * v + kk < nslots) x = slot_fold(x, ((w[kk >> 2] >> (8 * (kk & 3))) & 0xffu));
             }
         }
 #pragma unroll
@@ -2338,7 +2366,7 @@ __device__ __attribute__((always_inline)) inline Summ wave_compose_slots(const u
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 const uint32_t s = s0 + 16 * v + k;
-                if (s >= lo && s < hi) x = summ_cat(x, summ_slot((w[k >> 2] >> (8 * (k & 3))) & 0xffu));
+                if (s >= lo && s < hi) x = slot_fold(x, ((w[k >> 2] >> (8 * (k & 3))) & 0xffu));
             }
         }
     }
@@ -2411,9 +2439,9 @@ __device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const H
 #pragma unroll
     for (int k = 0; k < 64; k++) {
         const uint32_t t = s0 + k;
-        const Summ e = summ_slot((w[k >> 2] >> (8 * (k & 3))) & 0xffu);
-        if (t > s && t < bend) x1 = summ_cat(x1, e);
-        if (t < s) x5 = summ_cat(x5, e);
+        const uint32_t e = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        if (t > s && t < bend) x1 = slot_fold(x1, e);
+        if (t < s) x5 = slot_fold(x5, e);
     }
     const Summ x2 = (bi > b && bi < V.nb) ? bs : Summ{0, 0};
     const Summ x4 = bi < b ? bs : Summ{0, 0};
@@ -2474,9 +2502,13 @@ __device__ __attribute__((always_inline)) inline int64_t wave_last_free(const Ho
         for (int k = 0; k < 16; k++) w[k] = 0;
     }
     Summ x{0, 0};
+    if (s0 + 64 <= hi) {
+        x = fold64(w);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 64; k++)
-        if (s0 + k < hi) x = summ_cat(x, summ_slot((w[k >> 2] >> (8 * (k & 3))) & 0xffu));
+        for (int k = 0; k < 64; k++)
+            if (s0 + k < hi) x = slot_fold(x, ((w[k >> 2] >> (8 * (k & 3))) & 0xffu));
+    }
     // exclusive ordered scan over lanes
     Summ inc = x;
 #pragma unroll
