@@ -2038,6 +2038,12 @@ __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, co
                                      uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world,
                                      uint32_t key_hint, uint32_t lastpair_hint) {
     {
+        // every state word the roll reads, loaded together before the first store (the stores
+        // below may alias them as far as the compiler knows, which would serialise each load)
+        uint32_t *tail = delta + 2 * X;
+        const uint32_t rec_count = st->rec_count, total_occ = st->total_occ, holes_made = st->holes_made;
+        const uint32_t arena_top = st->arena_top, gocc = roll ? tail[1] : 0u;
+        const long long live_tokens = st->live_tokens;
         st->top_count = q.cnt;
         st->tie_count = q.cnt ? q.ties : 0;
         st->top_id = q.id;
@@ -2057,17 +2063,16 @@ __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, co
             st->lastpair_count = got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0;
         }
         if (roll) {
-            uint32_t *tail = delta + 2 * X;
-            st->last_occ = st->rec_count;
-            st->total_occ += st->rec_count;
-            st->last_gocc = tail[1];
-            st->last_holes = st->holes_made;
-            st->live_tokens -= st->holes_made;
+            st->last_occ = rec_count;
+            st->total_occ = total_occ + rec_count;
+            st->last_gocc = gocc;
+            st->last_holes = holes_made;
+            st->live_tokens = live_tokens - holes_made;
             st->tie_len = 0;
             if (T.lst_off) {  // this merge's records (positions of X) are X's occurrence list
-                T.lst_off[X] = st->arena_top;
-                T.lst_len[X] = st->rec_count;
-                st->arena_top += st->rec_count;
+                T.lst_off[X] = arena_top;
+                T.lst_len[X] = rec_count;
+                st->arena_top = arena_top + rec_count;
             }
             st->holes_made = 0;
             st->rec_count = 0;
@@ -2132,27 +2137,30 @@ struct BeginArgs {
 };
 __device__ inline uint32_t merge_begin_eval(const Tables &T, const DevState *st, const BeginArgs &B, bool *tie) {
     *tie = false;
-    if (st->live <= 0) return HALT_DONE;
-    if (st->hot_len > T.hot_cap || st->top_count == 0) return HALT_SELECT;
-    if ((uint64_t)st->arena_top + st->top_count > B.rec_cap) return HALT_RECORDS;
-    if (st->tie_count > 1) {
-        if (dev_zig_final_capacity((uint64_t)st->live, st->lastpair_count >= 2) != B.home_cap) return HALT_HOME;
+    const int32_t live = st->live;  // the words read, loaded together
+    const uint32_t hot_len = st->hot_len, top_count = st->top_count, arena_top = st->arena_top, tie_count = st->tie_count;
+    const uint32_t lastpair = st->lastpair_count, key = st->top_key;
+    if (live <= 0) return HALT_DONE;
+    if (hot_len > T.hot_cap || top_count == 0) return HALT_SELECT;
+    if ((uint64_t)arena_top + top_count > B.rec_cap) return HALT_RECORDS;
+    if (tie_count > 1) {
+        if (dev_zig_final_capacity((uint64_t)live, lastpair >= 2) != B.home_cap) return HALT_HOME;
         *tie = true;
         return HALT_NONE;
     }
-    const uint32_t key = st->top_key;
     return (key & 0xFFFF) == (key >> 16) ? HALT_SELF : HALT_NONE;
 }
 __device__ inline void merge_begin_commit(DevState *st, const BeginArgs &B, uint32_t h, bool tie) {
+    const uint32_t key = st->top_key, top_count = st->top_count, tie_count = st->tie_count;  // loaded before the stores
+    const long long live_tokens = st->live_tokens;
     st->cur_x = B.X;
     st->tie_on = tie ? 1u : 0u;
     if (h) {
         st->halt = h;
         st->halt_at = B.X;
     } else if (!tie) {
-        const uint32_t key = st->top_key;
         st->cur_key = key;
-        B.log[B.X - 256] = MergeLog{key, st->top_count, (uint32_t)st->live_tokens, st->tie_count};
+        B.log[B.X - 256] = MergeLog{key, top_count, (uint32_t)live_tokens, tie_count};
     }
 }
 __global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, uint32_t top, uint32_t cap_mask,
