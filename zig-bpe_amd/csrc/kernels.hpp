@@ -1406,7 +1406,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                                     uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per) {
     __shared__ uint32_t s_t[UPD_THREADS * UPD_MAX_PER], s_c[UPD_THREADS * UPD_MAX_PER];
     __shared__ uint32_t s_hot[UPD_THREADS * UPD_MAX_PER];
-    __shared__ uint32_t s_n, s_nhot, s_base;
+    __shared__ uint32_t s_n, s_nhot, s_base, s_hbase;
     __shared__ int s_live;
     const uint32_t nch = update_chunks(X, per);
     const uint32_t tid = threadIdx.x;
@@ -1451,12 +1451,26 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
     const uint32_t n = s_n;
     if (n == 0) return;
     const bool create = g == 1 || g == 3;
-    if (create && tid == 0) {
-        s_base = atomicAdd(&st->num_ids, n);
-        atomicAdd(&st->live, (int)n);
+    if (create) {
+        // the new ids that reach theta join the hot list: their slots are reserved by the same
+        // thread and at the same time as the ids (two returning atomics in flight, not in series)
+        const uint32_t theta = st->theta;
+        for (uint32_t i = tid; i < n; i += UPD_THREADS)
+            if (s_c[i] >= theta) s_hot[atomicAdd(&s_nhot, 1u)] = i;
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t nh = s_nhot;
+            uint32_t hb = 0;
+            if (nh) hb = atomicAdd(&st->hot_len, nh);
+            s_base = atomicAdd(&st->num_ids, n);
+            atomicAdd(&st->live, (int)n);
+            s_hbase = hb;
+        }
+        __syncthreads();
+        const uint32_t base = s_base, hbase = s_hbase;
+        for (uint32_t j = tid; j < s_nhot; j += UPD_THREADS)
+            if (hbase + j < T.hot_cap && base + s_hot[j] < T.id_cap) T.hot[hbase + j] = base + s_hot[j];
     }
-    __syncthreads();
-    const uint32_t theta = st->theta;
     int live_delta = 0;
     for (uint32_t i = tid; i < n; i += UPD_THREADS) {
         const uint32_t t = s_t[i], c = s_c[i];
@@ -1478,19 +1492,13 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 T.id_cnt[id] = c;
                 home_add(T, st, key, true);
                 ht_insert_new(T, key, id);
-                if (c >= theta) s_hot[atomicAdd(&s_nhot, 1u)] = id;
             }
         }
     }
+    if (create) return;  // creating blocks kill no pair
     if (live_delta) atomicAdd(&s_live, live_delta);
     __syncthreads();
-    if (tid == 0) {
-        if (s_live) atomicAdd(&st->live, s_live);
-        s_base = s_nhot ? atomicAdd(&st->hot_len, s_nhot) : 0;
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < s_nhot; i += UPD_THREADS)
-        if (s_base + i < T.hot_cap) T.hot[s_base + i] = s_hot[i];
+    if (tid == 0 && s_live) atomicAdd(&st->live, s_live);
 }
 
 // replaceTopPairWithNewToken in one launch: blocks [0, apply_blocks) rewrite the stream at the
