@@ -1403,7 +1403,8 @@ __host__ __device__ inline uint32_t update_per(uint32_t X) {
 }
 __device__ inline void update_block(const Tables &T, DevState *st, const uint32_t *__restrict__ left,
                                     const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
-                                    uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per) {
+                                    uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per,
+                                    const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta) {
     __shared__ uint32_t s_t[UPD_THREADS * UPD_MAX_PER], s_c[UPD_THREADS * UPD_MAX_PER];
     __shared__ uint32_t s_hot[UPD_THREADS * UPD_MAX_PER];
     __shared__ uint32_t s_n, s_nhot, s_base, s_hbase;
@@ -1435,12 +1436,12 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
         return;
     }
     const uint32_t g = ublk / nch, beg = (ublk - g * nch) * UPD_THREADS * per;
-    const uint32_t *delta = (g < 2) ? left : right;
     if (tid == 0) { s_n = 0; s_nhot = 0; s_live = 0; }
     __syncthreads();
-    for (uint32_t k = 0; k < per; k++) {
+#pragma unroll
+    for (uint32_t k = 0; k < UPD_MAX_PER; k++) {
         const uint32_t t = beg + k * UPD_THREADS + tid;
-        const uint32_t c = t < X ? delta[t] : 0;
+        const uint32_t c = k < per ? dv[k] : 0u;  // (update_preload: delta[t], 0 past X)
         if (c) {
             const uint32_t j = atomicAdd(&s_n, 1u);
             s_t[j] = t;
@@ -1454,7 +1455,6 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
     if (create) {
         // the new ids that reach theta join the hot list: their slots are reserved by the same
         // thread and at the same time as the ids (two returning atomics in flight, not in series)
-        const uint32_t theta = st->theta;
         for (uint32_t i = tid; i < n; i += UPD_THREADS)
             if (s_c[i] >= theta) s_hot[atomicAdd(&s_nhot, 1u)] = i;
         __syncthreads();
@@ -1519,7 +1519,25 @@ struct ReplaceArgs {
     const Halo *dhalo;
     int rec_arena;      // records at rec + st->arena_top (ScanArgs::rec_arena)
 };
+// this thread's deltas of an update block, loaded before anything that waits on the state (they do
+// not depend on the merged pair: group and range follow from the block index)
+__device__ inline void update_preload(const uint32_t *left, const uint32_t *right, uint32_t X, uint32_t ublk, uint32_t per,
+                                      uint32_t (&dv)[UPD_MAX_PER]) {
+    const uint32_t nch = update_chunks(X, per);
+    const uint32_t g = ublk < 4 * nch ? ublk / nch : 0u, beg = (ublk - g * nch) * UPD_THREADS * per;
+    const uint32_t *delta = (g < 2) ? left : right;
+    const bool real = ublk < 4 * nch;
+#pragma unroll
+    for (uint32_t k = 0; k < UPD_MAX_PER; k++) {
+        const uint32_t t = beg + k * UPD_THREADS + threadIdx.x;
+        dv[k] = real && k < per && t < X ? delta[t] : 0u;
+    }
+}
 __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, DevState *st) {
+    uint32_t dv[UPD_MAX_PER];
+    const uint32_t per = update_per(R.X);
+    if (blockIdx.x >= R.apply_blocks) update_preload(R.left, R.right, R.X, blockIdx.x - R.apply_blocks, per, dv);
+    const uint32_t theta = st->theta;
     if (R.dyn) {
         if (st->halt) return;
         R.top_key = st->cur_key;
@@ -1567,7 +1585,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
     }
     const uint32_t ublk = blockIdx.x - R.apply_blocks;
     if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != st->top_count) atomicOr(&st->error, 64u);  // occurrences != count
-    update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, update_per(R.X));
+    update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta);
 }
 
 // this shard's boundary record: first 3 / last 2 live tokens (holes skipped) and its live count
