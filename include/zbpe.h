@@ -112,6 +112,13 @@ zbpe_status zbpe_encode(zbpe_ctx *ctx, const uint16_t *triples, size_t n_merges,
  * *mismatches = 0 when they agree. Valid after zbpe_train*. */
 zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches);
 
+/* Diagnostic used by the parity tests: the current token stream (the `currentTokens` of
+ * expandVocabulary after the last zbpe_train*, basic_tokenizer.zig:173-204, or the result of the
+ * last zbpe_encode), holes removed. *n_tokens receives its length; the tokens are copied to `out`
+ * when cap >= *n_tokens (pass out = NULL, cap = 0 to query the length). In a sharded context
+ * this is the rank's shard (the whole stream once the ranks replicated). No training state changes. */
+zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_tokens);
+
 /* Tuning / test options: "debug_checks" (0/1), "exact_ties" (resolve every tie by the exact
  * first-occurrence emulation and cross-check the GPU cluster test), "compact_den" (compact when
  * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..6: unroll, load kind, phase-2 form;

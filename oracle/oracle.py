@@ -12,6 +12,7 @@ import ctypes
 import os
 import subprocess
 from dataclasses import dataclass
+from typing import Optional
 
 import numpy as np
 
@@ -57,6 +58,7 @@ def lib() -> ctypes.CDLL:
         L.zref_map_order.restype = ctypes.c_uint32
         L.zref_encode.restype = ctypes.c_int
         L.zref_decode.restype = ctypes.c_int
+        L.zref_step.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -97,6 +99,32 @@ def train(text: bytes, vocab_size: int, verbose: bool = False, max_merges: int =
     m = nm.value
     return TrainResult(tri[: 3 * m].reshape(m, 3).copy(), cnt[:m].copy(), ties[:m].copy(), dist[:m].copy(),
                        toks[: nt.value].copy(), st)
+
+
+@dataclass
+class StepResult:
+    pair: tuple        # (first, second) of sortedCodePointPairs[0]
+    count: int         # its count
+    ties: int          # pairs sharing that count
+    distinct: int      # D_t: distinct pairs of the stream
+    stats: ZrefStats
+
+
+def step(tokens, literal: bool = False) -> Optional[StepResult]:
+    """One expandVocabulary iteration (basic_tokenizer.zig:183-204) on a u16 token stream: the pair
+    the reference would merge next. None when the stream has no pairs (:188-191)."""
+    L = lib()
+    t = np.ascontiguousarray(np.asarray(tokens, dtype=np.uint16))
+    tt = t if len(t) else np.zeros(1, dtype=np.uint16)
+    pair, cnt, ties, d = ctypes.c_uint32(0), ctypes.c_uint64(0), ctypes.c_uint32(0), ctypes.c_uint64(0)
+    st = ZrefStats()
+    rc = L.zref_step(_p(tt), ctypes.c_size_t(len(t)), ctypes.c_int(int(literal)), ctypes.byref(pair), ctypes.byref(cnt),
+                     ctypes.byref(ties), ctypes.byref(d), ctypes.byref(st))
+    if rc == 3:
+        return None
+    if rc != 0:
+        raise MemoryError("OutOfMemory")
+    return StepResult((pair.value & 0xFFFF, pair.value >> 16), int(cnt.value), int(ties.value), int(d.value), st)
 
 
 def map_order(tokens) -> tuple[np.ndarray, np.ndarray, np.ndarray, int]:

@@ -124,7 +124,14 @@ static uint32_t ceil_pow2(uint64_t x) {
 static uint32_t capacity_for_size(uint32_t size) { /* capacityForSize */
     return ceil_pow2(((uint64_t)size * 100) / 80 + 1);
 }
-static uint64_t key_hash(uint32_t k) { return zref_pair_hash((uint16_t)k, (uint16_t)(k >> 16)); }
+/* zref_pair_hash with the 4-byte path of zref_wyhash unfolded (len 4: quarter 0, so a = b =
+ * w << 32 | w; seed 0 gives a constant state); zref_selftest checks the two agree. */
+static inline uint64_t key_hash(uint32_t k) {
+    const uint64_t s = wy_mix(WY_S0, WY_S1); /* seed 0: 0 ^ mix(0 ^ s0, s1) */
+    uint64_t a = ((uint64_t)k << 32 | k) ^ WY_S1, b = ((uint64_t)k << 32 | k) ^ s;
+    wy_mum(&a, &b);
+    return wy_mix(a ^ WY_S0 ^ 4u, b ^ WY_S1);
+}
 
 static void zmap_free(zmap *m) {
     free(m->keys);
@@ -349,6 +356,79 @@ int zref_train(const uint8_t *text, size_t n, uint32_t vocab_size, int verbose, 
     return 0;
 }
 
+/* ONE iteration of expandVocabulary (basic_tokenizer.zig:183-204) on a given token stream:
+ * generateCodePointPairs (:234-255) -> countCodePointPairs (:257-278) -> sortCodePointPairs
+ * (:280-306) -> sortedCodePointPairs[0] (:193). Used by the parity tests to check the device's
+ * merge k+1 on the device's own stream after k merges (any merge of C3/C4, where a full oracle
+ * run is out of reach), and by bench.py's cpu_baseline to time a late merge.
+ *   literal = 1: materialise the pairs array and stable-sort the slot-ordered entries, exactly as
+ *                the reference does (the cost the CPU baseline prices);
+ *   literal = 0: the same map, but pairs are hashed as they are read and the winner is taken as
+ *                the first maximum in slot order -- what a stable sort by count descending puts
+ *                at [0] -- so no n-sized or D-sized array is allocated.
+ * Returns 0 ok, 2 OutOfMemory, 3 no pairs ("Stopping early", :188-191). */
+int zref_step(const uint16_t *tok, size_t len, int literal, uint32_t *out_pair, uint64_t *out_count,
+              uint32_t *out_ties, uint64_t *out_distinct, zref_stats *stats) {
+    zref_stats st;
+    memset(&st, 0, sizeof(st));
+    double t0 = now_s();
+    size_t np = len >= 1 ? len - 1 : 0;
+    uint32_t *pairs = NULL;
+    if (literal && np) {
+        pairs = (uint32_t *)malloc(sizeof(uint32_t) * np);
+        if (!pairs) return 2;
+        for (size_t i = 0; i < np; i++) pairs[i] = (uint32_t)tok[i] | ((uint32_t)tok[i + 1] << 16);
+    }
+    double t1 = now_s();
+    st.generate_pairs_s = t1 - t0;
+    zmap m;
+    memset(&m, 0, sizeof(m));
+    for (size_t i = 0; i < np; i++) {
+        int found;
+        uint32_t key = pairs ? pairs[i] : ((uint32_t)tok[i] | ((uint32_t)tok[i + 1] << 16));
+        uint64_t *v = zmap_get_or_put(&m, key, &found);
+        if (!found) *v = 1;
+        else *v += 1;
+    }
+    double t2 = now_s();
+    st.count_pairs_s = t2 - t1;
+    st.pair_tokens = len;
+    free(pairs);
+    size_t d = m.size;
+    uint32_t best_pair = 0, ties = 0;
+    uint64_t best = 0;
+    if (literal && d) {
+        pair_count *sorted = (pair_count *)malloc(sizeof(pair_count) * d);
+        pair_count *tmp = (pair_count *)malloc(sizeof(pair_count) * d);
+        if (!sorted || !tmp) { free(sorted); free(tmp); zmap_free(&m); return 2; }
+        size_t k = 0;
+        for (uint32_t s = 0; s < m.cap; s++)
+            if (m.used[s]) { sorted[k].pair = m.keys[s]; sorted[k].count = m.vals[s]; k++; }
+        merge_sort_desc(sorted, tmp, d);
+        best_pair = sorted[0].pair;
+        best = sorted[0].count;
+        while (ties < d && sorted[ties].count == best) ties++;
+        free(sorted);
+        free(tmp);
+    } else {
+        for (uint32_t s = 0; s < m.cap; s++) {
+            if (!m.used[s]) continue;
+            if (m.vals[s] > best) { best = m.vals[s]; best_pair = m.keys[s]; ties = 1; }
+            else if (m.vals[s] == best) ties++;
+        }
+    }
+    st.sort_pairs_s = now_s() - t2;
+    st.total_s = now_s() - t0;
+    zmap_free(&m);
+    if (stats) *stats = st;
+    if (out_distinct) *out_distinct = d;
+    if (d == 0) return 3;
+    *out_pair = best_pair;
+    *out_count = best;
+    if (out_ties) *out_ties = ties;
+    return 0;
+}
+
 /* Hash-map iteration order of the pair map built from `tokens` (countCodePointPairs +
  * iterator). Writes keys in slot order, their slots, counts; returns the final capacity. */
 uint32_t zref_map_order(const uint16_t *tok, size_t len, uint32_t *out_keys, uint32_t *out_slots,
@@ -480,5 +560,9 @@ int zref_selftest(void) {
     int fails = 0;
     for (size_t i = 0; i < sizeof(v) / sizeof(v[0]); i++)
         if (zref_wyhash(v[i].seed, (const uint8_t *)v[i].in, strlen(v[i].in)) != v[i].want) fails++;
+    /* the map's unfolded key hash == Wyhash.hash(0, key bytes) */
+    uint32_t k = 0x12345u;
+    for (int i = 0; i < 4096; i++, k = k * 2654435761u + 12345u)
+        if (key_hash(k) != zref_pair_hash((uint16_t)k, (uint16_t)(k >> 16))) { fails++; break; }
     return fails;
 }

@@ -220,30 +220,6 @@ def test_encode_runs_vs_oracle(engine):
     assert np.array_equal(engine.encode(m, text), O.encode(m, text))
 
 
-def test_large_properties(engine):
-    """64 MiB: too slow for the oracle per merge, so check size-independent properties."""
-    text = zbpe.synth_corpus("words_utf8", 0x5EED0003, 64 << 20)
-    vocab = 1500
-    m, c, st = _train(engine, text, vocab)
-    assert len(m) == vocab - 256
-    assert m[:, 2].tolist() == list(range(256, vocab))
-    assert all(int(a) < int(x) and int(b) < int(x) for a, b, x in m)
-    assert np.all(np.diff(c.astype(np.int64)) <= 0)  # the top count never increases
-    assert engine.verify_counts() == 0  # incremental counts == full recount of the final stream
-    # the first merge's count equals the oracle's full count of the byte stream's top pair
-    r0 = O.train(text[: 1 << 20], 257)
-    assert st.final_tokens > 0
-    # encode(train text) reproduces the training stream length; decode round-trips a prefix
-    enc = engine.encode(m, text)
-    assert len(enc) == st.final_tokens
-    t = zbpe.BasicTokenizer()
-    for a, b, x in m:
-        t.merges.put(zbpe.CharPair(int(a), int(b)), int(x))
-    pre = text[: 1 << 20]
-    assert t.decode(engine.encode(m, pre)) == pre
-    assert r0 is not None
-
-
 def test_oracle_prefix_first_merges_large(engine):
     """At 16 MiB the oracle can still run a few merges: the first merges must agree."""
     text = zbpe.synth_corpus("words", 77, 16 << 20)

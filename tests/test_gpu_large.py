@@ -1,0 +1,162 @@
+"""Parity at the BASELINE.json sizes (C3, C4, C5) on the MI355X.
+
+A full oracle run of C3/C4 is out of reach on the CPU (the reference recounts every pair of the
+stream per merge: hours to days), so each check is one reference loop iteration on the device's own
+state: train to 256 + k merges, download the device's token stream (zbpe_tokens) and ask the oracle
+what expandVocabulary would merge next on it (oracle.step = basic_tokenizer.zig:183-204 once:
+count in the Zig map, slot order, stable sort, [0]). That must be the full run's merge k + 1 with
+its count. Together with "the first k merges of a run to 256 + k equal the full run's" this checks
+merge k + 1 against the reference at the sampled k, on the real C4 stream, ties included.
+
+Size-independent properties at full size: the incremental counts equal a full recount of the final
+stream (zbpe_verify_counts), encode(corpus) reproduces the training stream, decode(encode(x)) == x.
+C5: encode with all 31,744 C4 merges against the oracle's encode on a 1 MiB slice of the C5 text.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle as O
+import zbpe
+
+pytestmark = pytest.mark.gpu
+
+C3_SEED, C4_SEED, C5_SEED = 0x5EED0003, 0x5EED0004, 0x5EED0005
+
+
+class Run:
+    def __init__(self, n_bytes, seed, vocab):
+        self.text = zbpe.synth_corpus("words_utf8", seed, n_bytes, threads=16)
+        self.vocab = vocab
+        self.e = zbpe.Engine(0)
+        self.e.upload(self.text)
+        self.merges, self.counts, self.stats = self.e.train_resident(vocab)
+        self.mismatches = self.e.verify_counts()
+        fin = self.e.tokens()
+        self.final_len = len(fin)
+        self.final_sha = hashlib.sha256(fin.tobytes()).hexdigest()
+        del fin
+
+    def check_step(self, k):
+        """train to 256 + k; the oracle's next merge on the device stream == the full run's merge k + 1"""
+        m, c, st = self.e.train_resident(256 + k)
+        assert len(m) == k
+        assert np.array_equal(m, self.merges[:k]) and np.array_equal(c, self.counts[:k])
+        tok = self.e.tokens()
+        assert len(tok) == st.final_tokens
+        r = O.step(tok)
+        assert r is not None
+        a, b, x = (int(v) for v in self.merges[k])
+        assert (r.pair, r.count) == ((a, b), int(self.counts[k])), (k, r.pair, r.count, r.ties, (a, b), self.counts[k])
+        assert x == 256 + k
+        return r
+
+    def close(self):
+        self.e.close()
+
+
+def decode_np(merges: np.ndarray, tokens: np.ndarray) -> bytes:
+    """decode (basic_tokenizer.zig:90-138) vectorised: the byte expansion of every token id (first
+    merge with that new_token wins, like findMerge), gathered for the whole stream."""
+    first = {}
+    for i, (a, b, x) in enumerate(merges.tolist()):
+        first.setdefault(x, (a, b))
+    exp = {t: bytes([t]) for t in range(256)}
+    for x in sorted(first):
+        a, b = first[x]
+        exp[x] = exp[a] + exp[b]
+    vmax = max(exp) + 1
+    lens = np.zeros(vmax, np.int64)
+    offs = np.zeros(vmax, np.int64)
+    flat = bytearray()
+    for t in range(vmax):
+        if t in exp:
+            offs[t] = len(flat)
+            lens[t] = len(exp[t])
+            flat += exp[t]
+    flat = np.frombuffer(bytes(flat), np.uint8)
+    tk = tokens.astype(np.int64)
+    ln = lens[tk]
+    assert np.all(ln > 0), "token without a merge (InvalidToken)"
+    starts = np.cumsum(ln) - ln
+    idx = np.repeat(offs[tk] - starts, ln) + np.arange(int(ln.sum()))
+    return flat[idx].tobytes()
+
+
+@pytest.fixture(scope="module")
+def c4():
+    r = Run(1 << 30, C4_SEED, 32000)
+    yield r
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def c3():
+    r = Run(64 << 20, C3_SEED, 4096)
+    yield r
+    r.close()
+
+
+# --- C4: 1 GiB, vocab 32000 (the bench workload) -----------------------------------------------------
+def test_c4_full_run_properties(c4):
+    assert len(c4.merges) == 32000 - 256
+    assert c4.merges[:, 2].tolist() == list(range(256, 32000))
+    assert np.all(np.diff(c4.counts.astype(np.int64)) <= 0)  # the top count never increases
+    assert c4.mismatches == 0  # incremental counts == full recount of the final stream
+    assert c4.stats.final_tokens == c4.final_len
+
+
+@pytest.mark.parametrize("k", [0, 1, 1000, 5000, 15000, 31000])
+def test_c4_oracle_step(c4, k):
+    c4.check_step(k)
+
+
+def test_c4_encode_equals_training_stream(c4):
+    enc = c4.e.encode(c4.merges, c4.text)
+    assert len(enc) == c4.final_len
+    assert hashlib.sha256(enc.tobytes()).hexdigest() == c4.final_sha
+
+
+def test_c5_encode_slice_vs_oracle(c4):
+    """C5 (encode 100 M chars with the 31,744 C4 merges): a 1 MiB slice against the oracle's encode."""
+    text = zbpe.synth_corpus("words_utf8", C5_SEED, 100_000_000, threads=16)
+    piece = text[37_000_000:37_000_000 + (1 << 20)]
+    assert np.array_equal(c4.e.encode(c4.merges, piece), O.encode(c4.merges, piece))
+
+
+def test_c5_encode_full_round_trip(c4):
+    """C5 at full size: decode(encode(text)) == text, and the encoding is shorter than the text."""
+    text = zbpe.synth_corpus("words_utf8", C5_SEED, 100_000_000, threads=16)
+    enc = c4.e.encode(c4.merges, text)
+    assert 0 < len(enc) < len(text) // 2
+    assert decode_np(c4.merges, enc) == text
+
+
+# --- C3: 64 MiB, vocab 4096 -----------------------------------------------------------------------
+def test_c3_full_run_properties(c3):
+    assert len(c3.merges) == 4096 - 256
+    assert c3.merges[:, 2].tolist() == list(range(256, 4096))
+    assert all(int(a) < int(x) and int(b) < int(x) for a, b, x in c3.merges)
+    assert np.all(np.diff(c3.counts.astype(np.int64)) <= 0)
+    assert c3.mismatches == 0
+    # the first merge against the oracle's count of the whole 64 MiB byte stream
+    r = O.step(np.frombuffer(c3.text, np.uint8).astype(np.uint16))
+    assert (r.pair, r.count) == ((int(c3.merges[0, 0]), int(c3.merges[0, 1])), int(c3.counts[0]))
+
+
+@pytest.mark.parametrize("k", [1, 37, 500, 2000, 3839])
+def test_c3_oracle_step(c3, k):
+    c3.check_step(k)
+
+
+def test_c3_encode_and_decode(c3):
+    enc = c3.e.encode(c3.merges, c3.text)
+    assert len(enc) == c3.final_len
+    assert hashlib.sha256(enc.tobytes()).hexdigest() == c3.final_sha
+    assert decode_np(c3.merges, enc) == c3.text
+    t = zbpe.BasicTokenizer()
+    for a, b, x in c3.merges:
+        t.merges.put(zbpe.CharPair(int(a), int(b)), int(x))
+    pre = c3.text[: 1 << 18]
+    assert t.decode(c3.e.encode(c3.merges, pre)) == pre  # the API's own decode on a prefix

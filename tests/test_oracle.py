@@ -130,3 +130,24 @@ def test_incremental_model_matches_oracle(tmp_path):
         p.write_bytes(synth_text(g))
         out = subprocess.run([str(exe), str(p), str(g["vocab_size"])], capture_output=True, check=True).stdout
         assert out == O.serialize(np.array(g["merges"], dtype=np.uint16)), g["name"]
+
+
+@pytest.mark.parametrize("literal", [False, True])
+def test_step_matches_train(literal):
+    """oracle.step (one expandVocabulary iteration on a given stream, used by the C3/C4 GPU parity
+    tests) agrees with the full train: on the stream after k merges it picks merge k + 1, ties
+    included (C1 line 39 is a tie decided by the Zig slot order)."""
+    text = c1_text()
+    full = O.train(text, 300)
+    for k in (0, 1, 20, 38, 43):
+        r = O.train(text, 256 + k)
+        s = O.step(r.tokens, literal=literal)
+        a, b, _ = full.merges[k]
+        assert s.pair == (int(a), int(b)) and s.count == int(full.counts[k]) and s.ties == int(full.ties[k])
+        assert s.distinct == int(full.distinct[k])
+    for g in synth_goldens()[:3]:
+        t = synth_text(g)
+        r = O.train(t, 256 + 5)
+        s = O.step(r.tokens, literal=literal)
+        assert s.pair == tuple(g["merges"][5][:2]) and s.count == g["counts"][5]
+    assert O.step(np.zeros(1, np.uint16)) is None and O.step(np.zeros(0, np.uint16)) is None

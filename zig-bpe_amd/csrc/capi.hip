@@ -108,6 +108,11 @@ zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches) {
     return ctx->eng.verify_counts(mismatches);
 }
 
+zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_tokens) {
+    if (!ctx || !n_tokens || (!out && cap)) return ZBPE_INVALID_ARGUMENT;
+    return ctx->eng.tokens(out, cap, n_tokens);
+}
+
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     if (!ctx || !name) return ZBPE_INVALID_ARGUMENT;
     std::string k(name);

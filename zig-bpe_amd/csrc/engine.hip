@@ -1121,6 +1121,35 @@ zbpe_status Engine::verify_counts(uint64_t *mismatches) {
     return recount_check(mismatches, nullptr);
 }
 
+// Diagnostic download of the live token stream (holes squeezed out) into the spare stream buffer,
+// leaving the current buffer, its holes and the occurrence lists as they are. out == nullptr or a
+// short cap: only *n_tokens.
+zbpe_status Engine::tokens(uint16_t *out, size_t cap, size_t *n_tokens) {
+    if (!stream_ready && !trained && n_slots == 0) { *n_tokens = 0; return ZBPE_OK; }
+    HIP_OK(hipSetDevice(device));
+    const int64_t ntiles = (n_slots + COMPACT_TILE - 1) / COMPACT_TILE;
+    uint64_t total = 0;
+    if (ntiles > 0) {
+        CHECK(ensure(&d_tile_cnt, tile_cnt_cap, ntiles, "compaction tiles"));
+        CHECK(ensure(&d_tile_off, tile_off_cap, ntiles + 1, "compaction offsets"));
+        uint16_t *src = d_tok[cur], *dst = d_tok[cur ^ 1];
+        zbpe_compact_count<<<ntiles, 256, 0, stream>>>(src, n_slots, d_tile_cnt);
+        LAUNCH_OK();
+        zbpe_scan_u32<<<1, 1024, 0, stream>>>(d_tile_cnt, ntiles, d_tile_off, d_tile_off + ntiles);
+        LAUNCH_OK();
+        zbpe_compact_scatter<<<ntiles, 256, 0, stream>>>(src, n_slots, d_tile_off, dst);
+        LAUNCH_OK();
+        HIP_OK(hipMemcpyAsync(&total, d_tile_off + ntiles, 8, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+    }
+    *n_tokens = (size_t)total;
+    if (out && cap >= total && total) {
+        HIP_OK(hipMemcpyAsync(out, d_tok[cur ^ 1], (size_t)total * 2, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+    }
+    return ZBPE_OK;
+}
+
 // Full recount of the current stream against the incremental table. Multi-GPU: each shard
 // recounts the pairs it owns; ids differ between ranks but the key sets are identical, so the
 // per-rank recounts line up in key order and one all-reduce sums them.

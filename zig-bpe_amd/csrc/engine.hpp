@@ -165,6 +165,7 @@ struct Engine {
     zbpe_status encode(const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n, uint16_t *out,
                        size_t *out_len);
     zbpe_status verify_counts(uint64_t *mismatches);
+    zbpe_status tokens(uint16_t *out, size_t cap, size_t *n_tokens);
     zbpe_status set_scan_variant(int v);
     zbpe_status bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms, double *gbps);
 

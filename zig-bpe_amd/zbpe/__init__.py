@@ -140,7 +140,7 @@ class Stats(ctypes.Structure):
 
 EXPORTS = (
     "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_create_dist_host", "zbpe_destroy", "zbpe_last_error",
-    "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts",
+    "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts", "zbpe_tokens",
     "zbpe_set_option", "zbpe_bench_scan", "zbpe_trace", "zbpe_scan_log", "zbpe_zig_order_winner", "zbpe_version",
 )
 TRACE_COLUMNS = ("merge", "count", "live", "slots", "streamed", "scan_ms", "replace_ms", "select_ms", "wall_ms",
@@ -201,6 +201,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_train_resident.argtypes = [vp, ctypes.c_uint16, ctypes.c_int, u16p, u64p, ctypes.POINTER(sz), ctypes.POINTER(Stats)]
     L.zbpe_encode.argtypes = [vp, u16p, sz, vp, sz, u16p, ctypes.POINTER(sz)]
     L.zbpe_verify_counts.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+    L.zbpe_tokens.argtypes = [vp, u16p, sz, ctypes.POINTER(sz)]
     L.zbpe_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
     L.zbpe_bench_scan.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double)]
@@ -322,6 +323,14 @@ class Engine:
         if n.value:
             self._check(self._L.zbpe_scan_log(self._ctx, _ptr(out), n.value, ctypes.byref(n)), "zbpe_scan_log")
         return out
+
+    def tokens(self) -> np.ndarray:
+        """The current token stream (after the last train: expandVocabulary's currentTokens), as uint16."""
+        n = ctypes.c_size_t(0)
+        self._check(self._L.zbpe_tokens(self._ctx, None, 0, ctypes.byref(n)), "zbpe_tokens")
+        out = np.zeros(max(n.value, 1), dtype=np.uint16)
+        self._check(self._L.zbpe_tokens(self._ctx, _ptr(out), n.value, ctypes.byref(n)), "zbpe_tokens")
+        return out[: n.value]
 
     def verify_counts(self) -> int:
         mm = ctypes.c_uint64(0)
