@@ -107,7 +107,7 @@ def test_c4_full_run_properties(c4):
     assert c4.stats.final_tokens == c4.final_len
 
 
-@pytest.mark.parametrize("k", [0, 1, 1000, 5000, 15000, 31000])
+@pytest.mark.parametrize("k", [0, 1, 2, 100, 1000, 1400, 2500, 5000, 10000, 15000, 20000, 25000, 31000, 31743])
 def test_c4_oracle_step(c4, k):
     c4.check_step(k)
 
