@@ -125,13 +125,20 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * see engine.hip kScanVariants), "hot_target" (ids kept by the argmax hot list),
  * "block_skip" (0/1: stream only the 8192-slot blocks that hold the pair's rarer token),
  * "trace" (0/1: record per-merge timings, see zbpe_trace), "merge_batch" (merges enqueued per host
- * sync, 1 = synchronous loop), "merge_timing" (time every N-th merge of a batch with HIP events;
- * 0 = none), "replace_split" (profiling: apply and count update as separate launches), "list_mode"
+ * sync, 1 = synchronous loop), "merge_timing" (HIP events around every merge of a batch until the
+ * occurrence lists are on, then around every N-th; 0 = none), "sel_prof" (in-kernel wall-clock
+ * probes of the merge pipeline, printed to stderr after train), "replace_split" (profiling: apply and count update as separate launches), "list_mode"
  * (0: always stream the token stream; 1: token occurrence lists once counts are small), "list_ratio"
  * (list scan when list length * ratio < stream slots), "list_start" (build the lists at a compaction
  * once top count * list_start < live tokens; 0: at the first compaction), "compact_den_lists" (compact_den
  * once lists are on). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
+
+/* printTimeStats (src/utils/time_statistics.zig:36-60): the reference's "Time statistics" text for
+ * `stats` (sortCodePointPairs / replaceTopPairWithIndex / generateCodePointPairs / countPointPairs /
+ * Other operations). Writes up to cap-1 bytes + NUL to buf; *len receives the full length. The
+ * reference prints this to stderr at the end of every train (:141-145); the host shims do the same. */
+zbpe_status zbpe_format_time_stats(const zbpe_stats *stats, char *buf, size_t cap, size_t *len);
 
 /* Benchmark diagnostic: time `reps` launches of the pair-scan kernel for pair (a, b), a != b, over
  * the stream of the uploaded corpus (zbpe_upload) as it stands; the first launch is not timed.
@@ -139,7 +146,8 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, double *avg_ms, double *gbps);
 
 /* Profiling diagnostic: with option "trace" = 1, train records one row of ZBPE_TRACE_COLS floats per
- * merge: {merge index, count, live tokens, stream slots, slots streamed by the scan, scan ms,
+ * merge: {merge index, count, live tokens, stream slots, slots streamed by the scan (a list scan in a
+ * device-resident batch: entries of the walked list), scan ms,
  * replace ms, select ms, wall ms of the merge, self pair (0/1), ties}. Copies up to `cap_rows`
  * rows of the last train into `rows`; returns the number of rows recorded in *n_rows. */
 #define ZBPE_TRACE_COLS 11

@@ -142,6 +142,36 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     return ZBPE_OK;
 }
 
+// printTimeStats (time_statistics.zig:36-60): the reference's lines for the GPU buckets. The device
+// never materialises the pair array (the scan reads pairs in place), so generateCodePointPairs takes
+// 0 s over the count calls.
+zbpe_status zbpe_format_time_stats(const zbpe_stats *st, char *buf, size_t cap, size_t *len) {
+    if (!st || !len || (!buf && cap)) return ZBPE_INVALID_ARGUMENT;
+    std::string out = "\nTime statistics:\n";
+    auto line = [&](const char *name, double t, uint64_t calls) {
+        char b[256], avg[64];
+        if (calls) snprintf(avg, sizeof avg, "%.3f", t / (double)calls);
+        else snprintf(avg, sizeof avg, "nan");  // Zig prints 0.0 / 0.0 as nan
+        snprintf(b, sizeof b, "%s: %.3fs total, %llu calls, %ss avg\n", name, t, (unsigned long long)calls, avg);
+        out += b;
+    };
+    line("sortCodePointPairs", st->sort_pairs_s, st->sort_pairs_calls);
+    line("replaceTopPairWithIndex", st->replace_pair_s, st->replace_pair_calls);
+    line("generateCodePointPairs", 0.0, st->count_pairs_calls);
+    line("countPointPairs", st->count_pairs_s, st->count_pairs_calls);
+    char b[128];
+    snprintf(b, sizeof b, "Other operations: %.3fs\n",
+             st->total_s - st->sort_pairs_s - st->replace_pair_s - st->count_pairs_s);
+    out += b;
+    *len = out.size();
+    if (buf && cap) {
+        const size_t k = std::min(cap - 1, out.size());
+        memcpy(buf, out.data(), k);
+        buf[k] = 0;
+    }
+    return ZBPE_OK;
+}
+
 zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, double *avg_ms, double *gbps) {
     if (!ctx || !avg_ms || !gbps || reps < 1 || a == b) return ZBPE_INVALID_ARGUMENT;
     return ctx->eng.bench_scan(a, b, reps, avg_ms, gbps);

@@ -99,7 +99,7 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_list_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, PRES_MAX_VP * 4));
     HIP_OK(hipMalloc(&d_halo, sizeof(Halo)));
     h_log.resize(65536);
-    bev.resize(4 * MAX_BATCH);
+    bev.resize(BEV_PER_MERGE * MAX_BATCH + 2);  // per timed merge + the batch's first and last
     for (auto &e : bev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no L2 writeback
     HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
     HIP_OK(hipMalloc(&d_cand, ((size_t)NEXT_MAX_SEL * (NEXT_CAND + 1) + 64) * sizeof(uint32_t)));  // keys | pkey | lastpair
@@ -768,6 +768,14 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         X++;
     }
     const size_t merges = run.merges;
+    {  // device time of the batches, split into the stages by the shares of the timed merges
+        const double tm = run.tm_count + run.tm_select + run.tm_replace;
+        if (tm > 0) {
+            ev_count += run.batch_s * run.tm_count / tm;
+            ev_select += run.batch_s * run.tm_select / tm;
+            ev_replace += run.batch_s * run.tm_replace / tm;
+        }
+    }
     ev_count += run.ev_count;
     ev_select += run.ev_select;
     ev_replace += run.ev_replace;
@@ -808,6 +816,13 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                         "tie gather %.2f, decide %.2f; argmax blocks done %.2f, refresh blocks done %.2f\n",
                 P[7], P[0] * us / calls, P[1] * us / calls, P[2] * us / calls, P[3] * us / calls, P[4] * us / calls,
                 P[5] * us / calls, P[6] * us / calls);
+        const unsigned long long *Q = h_st->pipe_prof;
+        const double nl = std::max(1.0, (double)Q[4]), nr = std::max(1.0, (double)Q[7]), ns = std::max(1.0, (double)Q[9]);
+        fprintf(stderr, "pipe_prof: list scans %llu: avg us from the launch's block-0 start: LDS clear done %.2f, walk done %.2f, "
+                        "flush done %.2f, replace starts %.2f; replace (%llu): work done %.2f, select starts %.2f; "
+                        "select end -> scan start (%llu) %.2f\n",
+                Q[4], Q[0] * us / nl, Q[1] * us / nl, Q[2] * us / nl, Q[3] * us / nl, Q[7], Q[5] * us / nr, Q[6] * us / nr,
+                Q[9], Q[8] * us / ns);
     }
     stats.total_s = now_s() - t_start;
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
@@ -857,10 +872,12 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top0 / 256 + 1);
     const int64_t slots = n_slots;
     const double t0 = now_s();
+    lists_at_batch = lists_on;
+    if (merge_timing) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * MAX_BATCH], stream));
     for (uint32_t i = 0; i < K; i++) {
         const uint32_t X = X0 + i;
-        const bool timed = merge_timing && X % merge_timing == 0;
-        if (timed) HIP_OK(hipEventRecord(bev[4 * i], stream));
+        const bool timed = merge_timed(X);
+        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i], stream));
         uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
         // merge start (halt checks, tie_on, ties): done by the previous merge's zbpe_select_next,
         // else fused into the tie collection + refresh + decide
@@ -875,17 +892,17 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                 LAUNCH_OK();
             }
         }
-        if (timed) HIP_OK(hipEventRecord(bev[4 * i + 1], stream));
+        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 1], stream));
         ScanArgs A{d_tok[cur], slots, 0, 0, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
                    pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 1, dist() ? d_halo : nullptr,
-                   lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log};
+                   lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log, nullptr, (int)sel_prof};
         // a batch that follows one of list scans only launches a smaller grid (fewer idle workgroups
         // to dispatch); a stream scan still completes on it, only slower
         CHECK(launch_scan(A, list_streak ? list_grid : 0));
-        if (timed) HIP_OK(hipEventRecord(bev[4 * i + 2], stream));
+        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 2], stream));
         CHECK(comm_sum(d_delta, 2ull * X + 2));
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
-                      1, dist() ? d_halo : nullptr, 1};
+                      1, dist() ? d_halo : nullptr, 1, (int)sel_prof};
         if (!replace_split) {
             zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
         } else {  // profiling: apply and count update as two launches
@@ -902,6 +919,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             zbpe_halo_build<<<1, 1, 0, stream>>>(d_bnd_all, rank, world, d_halo, d_st);
             LAUNCH_OK();
         }
+        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 3], stream));
         if (fused_select) {
             if (hot_stale) CHECK(rebuild_hot());
             // about four hot entries per thread (the list grows by the new ids of the batch), and
@@ -917,13 +935,19 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         } else {
             CHECK(launch_argmax(X, 1));
         }
-        if (timed) HIP_OK(hipEventRecord(bev[4 * i + 3], stream));
+        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 4], stream));
     }
+    if (merge_timing) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * MAX_BATCH + 1], stream));
     if (dist()) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
     CHECK(sync_state());
     const double wall = now_s() - t0;
     batches++;
     const uint32_t m = h_st->halt ? h_st->halt_at - X0 : K;
+    if (merge_timing) {
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, bev[BEV_PER_MERGE * MAX_BATCH], bev[BEV_PER_MERGE * MAX_BATCH + 1]));
+        run.batch_s += ms * 1e-3;
+    }
     begun = fused_select && !h_st->halt;  // the last select started merge X0 + K
     if (h_st->halt) {
         *halted = true;
@@ -951,23 +975,28 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         stats.replace_pair_calls++;
         if (L.ties > 1) stats.tie_iterations++;
         if (L.mode) stats.list_scans++;
-        float ms_sel = 0, ms_scan = 0, ms_rep = 0;
-        if (merge_timing && X % merge_timing == 0) {
-            HIP_OK(hipEventElapsedTime(&ms_sel, bev[4 * i], bev[4 * i + 1]));
-            HIP_OK(hipEventElapsedTime(&ms_scan, bev[4 * i + 1], bev[4 * i + 2]));
-            HIP_OK(hipEventElapsedTime(&ms_rep, bev[4 * i + 2], bev[4 * i + 3]));
+        float ms_sel = 0, ms_scan = 0, ms_rep = 0, ms_begin = 0;
+        if (merge_timed(X)) {
+            const hipEvent_t *E = &bev[BEV_PER_MERGE * i];
+            const double w = lists_at_batch ? merge_timing : 1.0;  // the merges this one stands for
+            HIP_OK(hipEventElapsedTime(&ms_begin, E[0], E[1]));
+            HIP_OK(hipEventElapsedTime(&ms_scan, E[1], E[2]));
+            HIP_OK(hipEventElapsedTime(&ms_rep, E[2], E[3]));
+            HIP_OK(hipEventElapsedTime(&ms_sel, E[3], E[4]));
+            ms_sel += ms_begin;  // argmax + Zig-order tie decision: sortCodePointPairs + [0]
             if (!L.mode) {  // the roofline covers stream scans (a list scan reads no stream)
                 stats.scan_kernel_s += ms_scan * 1e-3;
                 stats.scan_timed_launches++;
                 stats.scan_timed_alg_bytes += 2ull * L.live;
             }
-            // stage totals are extrapolated from the sampled merges
-            run.ev_count += merge_timing * ms_scan * 1e-3;
-            run.ev_select += merge_timing * ms_sel * 1e-3;
-            run.ev_replace += merge_timing * ms_rep * 1e-3;
+            // the sampled merges give the shares of the stages; the batch's measured span is split by them
+            run.tm_count += w * ms_scan * 1e-3;
+            run.tm_select += w * ms_sel * 1e-3;
+            run.tm_replace += w * ms_rep * 1e-3;
         }
         if (trace_on) {
-            const float row[ZBPE_TRACE_COLS] = {(float)(X - 256), (float)L.count, (float)L.live, (float)slots, 0.f, ms_scan,
+            const float row[ZBPE_TRACE_COLS] = {(float)(X - 256), (float)L.count, (float)L.live, (float)slots,
+                                                L.mode ? (float)L.list_len : 0.f, ms_scan,
                                                 ms_rep, ms_sel, (float)(wall * 1e3 / K), 0.f, (float)L.ties};
             trace.insert(trace.end(), row, row + ZBPE_TRACE_COLS);
         }

@@ -18,6 +18,7 @@ namespace zbpe {
 constexpr int ARGMAX_MAX_BLOCKS = 1024;
 constexpr size_t DELTA_WORDS = 2 * 65536 + 64;  // left | right | xx | occurrences (+ scratch)
 constexpr uint32_t MAX_BATCH = 256;              // merges per device-resident batch (option "merge_batch")
+constexpr uint32_t BEV_PER_MERGE = 5;            // events of a timed batch merge: start, begun, scanned, replaced, selected
 constexpr uint32_t PRES_MAX_VP = 32768;          // presence bitset of a block group fits one workgroup LDS (128 KiB)
 
 struct Engine {
@@ -120,7 +121,12 @@ struct Engine {
     // device-resident merge loop
     uint32_t merge_batch = 32;      // merges enqueued per host sync (1: synchronous loop)
     uint32_t sel_prof = 0;          // phase timestamps inside zbpe_select_next (printed to stderr after train)
-    uint32_t merge_timing = 8;     // HIP events around every merge_timing-th merge of a batch (0: none)
+    // HIP events around the merges of a batch (0: none): every merge while the scans stream the token
+    // stream (a merge takes 100s of us there: the roofline covers every stream-form scan), every
+    // merge_timing-th once the occurrence lists are on (a late merge takes ~50 us; an event pair costs ~1)
+    uint32_t merge_timing = 32;
+    bool lists_at_batch = false;    // lists were on when the current batch was enqueued
+    bool merge_timed(uint32_t X) const { return merge_timing && (!lists_at_batch || X % merge_timing == 0); }
     bool replace_split = false;     // profiling: apply and count update as separate launches
     bool fused_select = true;       // zbpe_select_next: the select of merge X also starts merge X+1 (ties included)
     bool begun = false;             // the next batch's first merge was started by the last batch's final select
@@ -136,7 +142,9 @@ struct Engine {
         size_t merges = 0;
         int verbose = 0;
         uint16_t vocab = 0;
-        double ev_count = 0, ev_select = 0, ev_replace = 0;
+        double ev_count = 0, ev_select = 0, ev_replace = 0;  // measured directly (sync path, compactions)
+        double tm_count = 0, tm_select = 0, tm_replace = 0;  // stage times of the timed batch merges
+        double batch_s = 0;                                   // device span of the batches
     } run;
     uint64_t hot_target = 1u << 16;  // ids the hot list aims to hold after a rebuild
     uint64_t hot_rebuilds = 0, home_rebuilds = 0;

@@ -359,6 +359,7 @@ struct ScanArgs {
     int rec_arena;          // records at rec + st->arena_top (they become the new token's list)
     MergeLog *log;          // batch mode: the scan records its mode in log[X - 256]
     uint32_t *rec_ctr;      // record counter (nullptr: st->rec_count); batched encode: one per merge
+    int prof;               // option sel_prof: probe stamps into st->pp_t (batch mode)
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // the device-held parts of the arguments: pair (batch mode), halo (batch mode, multi-GPU), record
@@ -381,7 +382,7 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
     }
     return ScanArgs{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
                     A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
-                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count};
+                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof};
 }
 
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
@@ -724,7 +725,8 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
         if (len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n) {
             if (blockIdx.x == 0 && threadIdx.x == 0) {
                 A.st->scan_mode = 1;
-                if (A.log) A.log[A.X - 256].mode = 1;
+                if (A.log) { A.log[A.X - 256].mode = 1; A.log[A.X - 256].list_len = len; }
+                if (A.prof) A.st->pp_t[4] = 1;
             }
             scan_list_body(A, by_b, A.lists + (by_b ? ob : oa), len, S);
             return;
@@ -734,7 +736,13 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
     scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT>(A, S);
 }
 template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false>
-__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
+__global__ void __launch_bounds__(SCAN_THREADS, 4) zbpe_scan_pairs_t(ScanArgs A0) {
+    if (A0.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // the last select's end -> this scan's start
+        DevState *st = A0.st;
+        const unsigned long long now = wall_clock64();
+        if (st->pp_t[7]) { st->pipe_prof[8] += now - st->pp_t[7]; st->pipe_prof[9]++; st->pp_t[7] = 0; }
+        st->pp_t[0] = now;
+    }
     if (A0.dyn && A0.st->halt) return;
     __shared__ ScanLds S;
     const ScanArgs A = scan_args_resolve(A0);
@@ -833,6 +841,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     scan_lds_clear(S);
     if (threadIdx.x == 0) s_any = 0;
     __syncthreads();
+    if (A.prof && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{s_left, s_right, A.left, A.right, S.hleft, S.hright};
     const uint16_t *tok = A.tok;
     const uint32_t key = by_b ? A.b : A.a;
@@ -938,7 +947,12 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     if (lane == 0 && any) s_any = 1;
     __syncthreads();
+    if (A.prof && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
     if (s_any) scan_lds_flush(S, A.left, A.right);
+    if (A.prof) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(&A.st->pp_t[3], (unsigned long long)wall_clock64());
+    }
 }
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S) {
@@ -1518,6 +1532,7 @@ struct ReplaceArgs {
     int dyn;            // batch mode (see ScanArgs::dyn)
     const Halo *dhalo;
     int rec_arena;      // records at rec + st->arena_top (ScanArgs::rec_arena)
+    int prof;           // option sel_prof: probe stamps (st->pp_t)
 };
 // this thread's deltas of an update block, loaded before anything that waits on the state (they do
 // not depend on the merged pair: group and range follow from the block index)
@@ -1538,6 +1553,19 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
     const uint32_t per = update_per(R.X);
     if (blockIdx.x >= R.apply_blocks) update_preload(R.left, R.right, R.X, blockIdx.x - R.apply_blocks, per, dv);
     const uint32_t theta = st->theta;
+    if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the list scan's stamps
+        const unsigned long long now = wall_clock64();
+        if (st->pp_t[4]) {
+            const unsigned long long t0 = st->pp_t[0];
+            st->pipe_prof[0] += st->pp_t[1] - t0;
+            st->pipe_prof[1] += st->pp_t[2] - t0;
+            st->pipe_prof[2] += st->pp_t[3] - t0;
+            st->pipe_prof[3] += now - t0;
+            st->pipe_prof[4]++;
+        }
+        st->pp_t[1] = st->pp_t[2] = st->pp_t[3] = st->pp_t[4] = 0;
+        st->pp_t[5] = now;
+    }
     if (R.dyn) {
         if (st->halt) return;
         R.top_key = st->cur_key;
@@ -1563,6 +1591,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
         }
         made = wave_sum(made);
         if ((threadIdx.x & 63) == 0 && made) atomicAdd(&st->holes_made, made);
+        if (R.prof && threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->consumed = 0;
             if (R.dhalo) R.halo = *R.dhalo;
@@ -1586,6 +1615,10 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
     const uint32_t ublk = blockIdx.x - R.apply_blocks;
     if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != st->top_count) atomicOr(&st->error, 64u);  // occurrences != count
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta);
+    if (R.prof) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
+    }
 }
 
 // this shard's boundary record: first 3 / last 2 live tokens (holes skipped) and its live count
@@ -2663,7 +2696,7 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
 // start of merge X+1 and, on a tie, gathers the tied keys for zbpe_tie_decide (the next launch:
 // the decision's carry code needs 256 VGPRs, more than a 1024-thread block may hold).
 // ------------------------------------------------------------------------------------------
-constexpr int NEXT_THREADS = 512;  // (the fused tie decision needs > 128 VGPRs per lane)
+constexpr int NEXT_THREADS = 512;  // launch bounds: 4 waves per SIMD (two workgroups per CU; the decision spills a little)
 constexpr int NEXT_CAND = 64;          // keys kept per argmax block at the block's max
 constexpr int NEXT_MAX_SEL = 1024;     // argmax blocks (the reducer keeps one LDS entry per block)
 struct NextArgs {
@@ -2715,7 +2748,7 @@ __device__ inline MaxRec block_max(MaxRec r, MaxRec *sm) {
     __syncthreads();
     return q;
 }
-__global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevState *st, MaxRec *__restrict__ partial,
+__global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, DevState *st, MaxRec *__restrict__ partial,
                                                                  const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
                                                                  uint32_t X, NextArgs N) {
     // blocks [0, nref) refresh the home super-blocks (the longest role: dispatched first, one
@@ -2728,7 +2761,16 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
     __shared__ uint32_t s_key[NEXT_CAND];
     __shared__ uint32_t s_pc[NEXT_MAX_SEL], s_pt[NEXT_MAX_SEL];
     const uint32_t tid = threadIdx.x;
-    if (N.prof && blockIdx.x == 0 && tid == 0) st->sel_t0 = wall_clock64();
+    if (N.prof && blockIdx.x == 0 && tid == 0) {
+        const unsigned long long now = wall_clock64();
+        st->sel_t0 = now;
+        if (st->pp_t[5]) {  // the replace launch: its work span, its start -> this select's start
+            st->pipe_prof[5] += st->pp_t[6] - st->pp_t[5];
+            st->pipe_prof[6] += now - st->pp_t[5];
+            st->pipe_prof[7]++;
+            st->pp_t[5] = st->pp_t[6] = 0;
+        }
+    }
     const uint32_t bx = blockIdx.x - nref;  // argmax block index
     if (blockIdx.x >= nref) {
         const uint32_t G = N.sel_blocks * NEXT_THREADS;
@@ -2846,7 +2888,10 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
     }
     __syncthreads();
     if (N.prof && tid == 0) sel_tick(st, 2, &pt);
-    if (s_h || !s_tie) return;
+    if (s_h || !s_tie) {
+        if (N.prof && tid == 0) st->pp_t[7] = wall_clock64();
+        return;
+    }
     // ---- merge X+1 ties: gather the keys of the blocks whose max is the top count ----------------
     const uint32_t top = Q.cnt, total = Q.ties;
     for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
@@ -2919,7 +2964,7 @@ __global__ void __launch_bounds__(NEXT_THREADS) zbpe_select_next(Tables T, DevSt
     __syncthreads();
     if (N.prof && tid == 0) sel_tick(st, 3, &pt);
     decide_body<NEXT_THREADS>(st, N.tie_list, total, total, N.V, N.B.log, 1);
-    if (N.prof && tid == 0) sel_tick(st, 4, &pt);
+    if (N.prof && tid == 0) { sel_tick(st, 4, &pt); st->pp_t[7] = wall_clock64(); }
 }
 
 // rebuild the home histogram for a new Zig capacity

@@ -66,6 +66,11 @@ struct DevState {
     // option sel_prof: zbpe_select_next phase times (wall_clock64 ticks, summed over merges)
     unsigned long long sel_t0, sel_ta, sel_tr;  // start; latest argmax / refresh block finish
     unsigned long long sel_prof[8];
+    // option sel_prof, whole merge pipeline (batch mode): probe stamps of the current launches and the
+    // sums they fold into (Engine::train prints them): scan (list form) LDS clear / walk / flush done and
+    // the next kernel's start, replace work span and the select's start, select end -> scan start
+    unsigned long long pp_t[8];
+    unsigned long long pipe_prof[16];
 };
 // why a device-resident batch stopped (the host finishes that merge on the synchronous path)
 enum HaltReason : uint32_t {
@@ -81,7 +86,8 @@ enum HaltReason : uint32_t {
 struct MergeLog {
     uint32_t key, count, live, ties;
     uint32_t mode;     // 0: stream scan, 1: list scan
-    uint32_t pad[3];
+    uint32_t list_len; // list scan: entries of the walked occurrence list
+    uint32_t pad[2];
 };
 
 struct Tables {

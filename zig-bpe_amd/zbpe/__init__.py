@@ -26,7 +26,7 @@ from typing import Iterable, List, Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libzbpe.so")
+LIB_PATH = os.environ.get("ZBPE_LIB") or os.path.join(_HERE, "libzbpe.so")  # ZBPE_LIB: A/B of builds
 SYNTH_PATH = os.path.join(_HERE, "libzbpe_synth.so")
 
 vocabStart = 256  # basic_tokenizer.zig:50
@@ -141,7 +141,7 @@ class Stats(ctypes.Structure):
 EXPORTS = (
     "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_create_dist_host", "zbpe_destroy", "zbpe_last_error",
     "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts", "zbpe_tokens",
-    "zbpe_set_option", "zbpe_bench_scan", "zbpe_trace", "zbpe_scan_log", "zbpe_zig_order_winner", "zbpe_version",
+    "zbpe_set_option", "zbpe_format_time_stats", "zbpe_bench_scan", "zbpe_trace", "zbpe_scan_log", "zbpe_zig_order_winner", "zbpe_version",
 )
 TRACE_COLUMNS = ("merge", "count", "live", "slots", "streamed", "scan_ms", "replace_ms", "select_ms", "wall_ms",
                  "self_pair", "ties")
@@ -202,6 +202,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_encode.argtypes = [vp, u16p, sz, vp, sz, u16p, ctypes.POINTER(sz)]
     L.zbpe_verify_counts.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
     L.zbpe_tokens.argtypes = [vp, u16p, sz, ctypes.POINTER(sz)]
+    L.zbpe_format_time_stats.argtypes = [ctypes.POINTER(Stats), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.zbpe_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
     L.zbpe_bench_scan.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double)]
@@ -336,6 +337,16 @@ class Engine:
         mm = ctypes.c_uint64(0)
         self._check(self._L.zbpe_verify_counts(self._ctx, ctypes.byref(mm)), "zbpe_verify_counts")
         return int(mm.value)
+
+
+def format_time_stats(st: Stats) -> str:
+    """printTimeStats (time_statistics.zig:36-60) text for a train's Stats."""
+    L = load_library()
+    n = ctypes.c_size_t(0)
+    buf = ctypes.create_string_buffer(1024)
+    if L.zbpe_format_time_stats(ctypes.byref(st), buf, 1024, ctypes.byref(n)) != 0:
+        raise InvalidArgument("zbpe_format_time_stats")
+    return buf.value.decode()
 
 
 def comm_unique_id() -> bytes:
@@ -476,6 +487,7 @@ class BasicTokenizer:
         for a, b, x in tri:
             self.merges.put(CharPair(int(a), int(b)), int(x))
         self.timeStats = st
+        sys.stderr.write(format_time_stats(st))  # the reference prints it at the end of train (:141-145)
 
     # encode (:71-88)
     def encode(self, text: bytes) -> List[int]:
@@ -560,5 +572,5 @@ __all__ = [
     "BasicTokenizer", "CharPair", "Merge", "Merges", "Engine", "Stats", "TrainError", "InvalidVocabSize", "InvalidUtf8",
     "OutOfMemory", "DeviceError", "InvalidToken", "InvalidFormat", "InvalidCharacter", "Overflow", "StreamTooLong",
     "InvalidArgument", "InternalError", "load_library", "synth_corpus", "comm_unique_id", "zig_order_winner",
-    "merges_to_text", "vocabStart", "EXPORTS", "TRACE_COLUMNS", "torch_collective", "COLLECTIVE_FN",
+    "merges_to_text", "format_time_stats", "vocabStart", "EXPORTS", "TRACE_COLUMNS", "torch_collective", "COLLECTIVE_FN",
 ]
