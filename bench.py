@@ -7,22 +7,30 @@ a 1 GiB synthetic corpus, vocab_size 32000 (31,744 merges), token stream sharded
 A step = one complete BasicTokenizer.train() over the whole corpus (all merges), starting from
 the corpus bytes already resident in HBM (zbpe_upload is outside the timed region).
 Prints ONE JSON line on rank 0 (the driver's contract) with `roofline` (dominant kernel:
-zbpe_scan_pairs, HBM-read bound) and `cpu_baseline` (the oracle, timed on this host).
+zbpe_scan_pairs_t, stream form, HBM-read bound) and `cpu_baseline` (the oracle, timed on this host).
+
+After the K timed steps, one untimed *probe* train runs with HIP events around every merge of every
+batch that streams the token stream (option timing_full): `roofline` comes from it, so it covers
+nearly every stream-form scan launch, not a 1-in-8 sample (events add gaps, which is why the timed
+steps only sample). --scan-log-out writes the probe train's scan log, so a rocprofv3 kernel trace of
+this command can be matched launch by launch (tools/scan_forms.py, tools/pmc_traffic.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "zig-bpe_amd"))
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_c4_pmc_traffic.json")  # tools/pmc_traffic.py output
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_c4_pmc_traffic.json")  # tools/pmc_traffic.py output
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
 C4_SEED = 0x5EED0004
+LIST_ENTRY_BYTES = 4 + 16  # a list scan reads the entry's list word and its 16-B stream vector
 
 
 def parse():
@@ -34,42 +42,123 @@ def parse():
     p.add_argument("--vocab", type=int, default=32000)
     p.add_argument("--kind", default="words_utf8")
     p.add_argument("--seed", type=int, default=C4_SEED)
-    p.add_argument("--cpu-sample-bytes", type=int, default=128 << 20)
-    p.add_argument("--cpu-sample-merges", type=int, default=2)
+    p.add_argument("--cpu-late-merge", type=int, default=20000,
+                   help="cpu_baseline: the late sample is one reference iteration on the GPU's stream after this many merges")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-probe", action="store_true", help="skip the roofline probe train")
     p.add_argument("--stats-out", default="")
     p.add_argument("--scan-log-out", default="",
-                   help="write the per-launch scan log + per-merge live tokens of the last step (for tools/pmc_traffic.py)")
+                   help="write the probe train's per-launch scan log + per-merge live tokens (tools/pmc_traffic.py, tools/scan_forms.py)")
     p.add_argument("--share-gpu", action="store_true",
                    help="all ranks on cuda:0 with host (gloo) collectives -- rehearses N>1 on one GPU")
     return p.parse_args()
 
 
-def cpu_baseline(text: bytes, sample_bytes: int, sample_merges: int, vocab: int, sum_tokens: int, merges: int):
-    """Oracle (single-threaded C restatement of basic_tokenizer.zig, -O3) on a bounded sample:
-    the first `sample_merges` merges of the first `sample_bytes` bytes. Its cost per merge is
-    linear in the stream length (pairs hashed per merge = n_t - 1), so the full job is priced from
-    the measured seconds per token x the GPU run's exact trajectory sum_t n_t."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(eng, text: bytes, vocab: int, live, late_k: int):
+    """The oracle (single-threaded C restatement of basic_tokenizer.zig, gcc -O3) timed on this host for
+    ONE reference loop iteration (generateCodePointPairs + countCodePointPairs + sortCodePointPairs,
+    literally: materialised pairs, Zig map, stable sort) at two points of the C4 run:
+      early: the full 1 GiB initial stream (t = 0; few distinct pairs, the map stays in cache),
+      late:  the GPU's own stream after `late_k` merges (zbpe_tokens; ~5e7 distinct pairs, cache-miss bound).
+    Replace is O(n) and omitted (it is cheaper than the count). Every merge t costs n_t x ns_per_token(t);
+    ns_per_token is interpolated linearly in t between the two samples and held beyond them; the
+    GPU run's measured n_t trajectory (`live`) prices the whole job (an extrapolation, labelled so)."""
+    import numpy as np
+
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
-    sample = text[:sample_bytes]
-    r = oracle.train(sample, min(vocab, 256 + sample_merges))
-    st = r.stats
-    per_token = st.total_s / max(st.pair_tokens, 1)
-    full_s = per_token * sum_tokens
+    tok0 = np.frombuffer(text, np.uint8).astype(np.uint16)
+    r0 = oracle.step(tok0, literal=True)
+    del tok0
+    m, _, _ = eng.train_resident(min(vocab, 256 + late_k))
+    late_k = len(m)
+    tokl = eng.tokens()
+    r1 = oracle.step(tokl, literal=True)
+    ns0 = r0.stats.total_s / max(r0.stats.pair_tokens, 1) * 1e9
+    ns1 = r1.stats.total_s / max(r1.stats.pair_tokens, 1) * 1e9
+    t = np.arange(len(live), dtype=np.float64)
+    ns = np.where(t >= late_k, ns1, ns0 + (ns1 - ns0) * t / max(late_k, 1))
+    full_s = float(np.sum(np.asarray(live, dtype=np.float64) * ns) * 1e-9)
+    merges = len(live)
     return {
         "value": merges / full_s if full_s > 0 else None,
         "unit": "merges/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"oracle (C restatement, gcc -O3, 1 thread) trained {len(r.merges)} merges on the first "
-                   f"{len(sample)} B of the corpus in {st.total_s:.2f} s ({per_token * 1e9:.2f} ns per stream token per "
-                   f"merge); full job extrapolated over the GPU run's sum_t n_t = {sum_tokens} tokens "
-                   f"-> {full_s / 3600:.1f} h"),
-        "sample_seconds": st.total_s,
-        "ns_per_token_merge": per_token * 1e9,
+        "cpu_model": cpu_model(),
+        "nproc": os.cpu_count(),
+        "sample": (f"oracle (C restatement of basic_tokenizer.zig:183-204, gcc -O3, 1 thread) timed for one literal loop "
+                   f"iteration at merge 0 on the full {len(text)}-B stream ({r0.stats.total_s:.2f} s, "
+                   f"{r0.distinct} distinct pairs, {ns0:.2f} ns/token) and at merge {late_k} on the GPU's stream "
+                   f"({len(tokl)} tokens, {r1.distinct} distinct pairs, {r1.stats.total_s:.2f} s, {ns1:.2f} ns/token); "
+                   f"the {merges} merges priced over the GPU run's n_t trajectory (sum {int(np.sum(live))} tokens, "
+                   f"ns/token interpolated by merge index) -> {full_s / 3600:.1f} h (extrapolated)"),
+        "sample_seconds": r0.stats.total_s + r1.stats.total_s,
+        "ns_per_token_early": ns0,
+        "ns_per_token_late": ns1,
+        "late_merge": late_k,
+        "oracle_agrees_with_gpu": None,  # filled by the caller
         "extrapolated_full_job_s": full_s,
+        "_pairs": (r0.pair, r1.pair),
+    }
+
+
+def probe_roofline(eng, vocab: int, scan_log_out: str):
+    """One untimed train with events around (nearly) every stream-form scan: the roofline of the
+    stream form from HIP events on the engine's stream, plus the list form's rate."""
+    import numpy as np
+    import zbpe
+
+    eng.set_option("timing_full", 1)
+    eng.set_option("trace", 1)
+    m, c, st = eng.train_resident(vocab)
+    eng.set_option("timing_full", 0)
+    tr = eng.trace()
+    eng.set_option("trace", 0)
+    C = {k: i for i, k in enumerate(zbpe.TRACE_COLUMNS)}
+    log = eng.scan_log()
+    live = tr[:, C["live"]].astype(np.int64)
+    if scan_log_out:
+        with open(scan_log_out, "w") as f:
+            json.dump({"scan_log": log.tolist(), "live": live.tolist()}, f)
+    # list form: the timed list-scan merges (scan_ms > 0; the walked list length is in `streamed`)
+    forms = {}
+    for e in log:
+        if e >= 0:
+            forms[int(e) >> 1] = int(e) & 1
+    lms, lent = 0.0, 0.0
+    nl = 0
+    for i, r in enumerate(tr):
+        if forms.get(i) == 1 and r[C["scan_ms"]] > 0 and r[C["streamed"]] > 0:
+            lms += float(r[C["scan_ms"]])
+            lent += float(r[C["streamed"]])
+            nl += 1
+    achieved = st.scan_timed_alg_bytes / st.scan_kernel_s / 1e9 if st.scan_kernel_s > 0 else 0.0
+    n_stream = int(np.sum(np.array([f == 0 for f in forms.values()])))
+    return {
+        "achieved": achieved,
+        "timed_launches": int(st.scan_timed_launches),
+        "stream_launches": n_stream,
+        "avg_launch_us": st.scan_kernel_s / max(st.scan_timed_launches, 1) * 1e6,
+        "alg_bytes_per_launch": st.scan_timed_alg_bytes / max(st.scan_timed_launches, 1),
+        "list_form": {"timed_launches": nl, "avg_launch_us": lms / max(nl, 1) * 1e3,
+                      "avg_entries": lent / max(nl, 1),
+                      "GBps": lent * LIST_ENTRY_BYTES / max(lms * 1e-3, 1e-12) / 1e9,
+                      "note": "bytes = 4 B list word + 16 B stream vector per walked entry; latency-bound "
+                              "(a chain of dependent loads and atomics per entry), not bandwidth-bound"},
+        "merges": m, "counts": c, "live": live,
     }
 
 
@@ -109,8 +198,6 @@ def main():
     text = zbpe.synth_corpus(args.kind, args.seed, args.n_bytes, threads=16)
     gen_s = time.time() - t0
     eng.upload(text)  # HBM-resident before timing (this rank's shard)
-    if args.scan_log_out:
-        eng.set_option("trace", 1)
 
     def barrier():
         if dist is not None:
@@ -119,7 +206,6 @@ def main():
     for _ in range(args.warmup):
         eng.train_resident(args.vocab)
     times = []
-    scan_s = alg_bytes = all_alg_bytes = read_bytes = 0.0
     last = None
     for _ in range(args.steps):
         barrier()
@@ -128,10 +214,6 @@ def main():
         dt = time.perf_counter() - t
         barrier()
         times.append(dt)
-        scan_s += st.scan_kernel_s
-        alg_bytes += st.scan_timed_alg_bytes
-        all_alg_bytes += st.scan_alg_bytes
-        read_bytes += st.scan_read_bytes
         last = (m, c, st)
     total = sum(times)
     if dist is not None:
@@ -143,14 +225,20 @@ def main():
     m, c, st = last
     merges = len(m)
     value = merges * args.steps / total
-    achieved = alg_bytes / scan_s / 1e9 if scan_s > 0 else 0.0
+    sampled = st.scan_timed_alg_bytes / st.scan_kernel_s / 1e9 if st.scan_kernel_s > 0 else 0.0
+    probe = None if args.no_probe else probe_roofline(eng, args.vocab, args.scan_log_out if rank == 0 else "")
+    if probe is not None and not np.array_equal(probe["merges"], m):
+        raise SystemExit("probe train produced different merges than the timed steps")
+    achieved = probe["achieved"] if probe else sampled
     traffic, traffic_note = None, "no PMC pass for this configuration"
     if os.path.exists(PMC_TRAFFIC) and args.n_bytes == 1 << 30 and args.vocab == 32000 and world == 1:
-        t = json.load(open(PMC_TRAFFIC))["traffic"]["stream_timed"]
+        t = json.load(open(PMC_TRAFFIC))["traffic"]["stream"]
         traffic = t["hbm_bytes_per_launch"]
-        traffic_note = ("HBM bytes per timed stream-scan launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 PMC passes of this "
-                        "command, %s): %.3g x the algorithmic bytes" % (os.path.relpath(PMC_TRAFFIC, ROOT), t["hbm_over_alg"]))
+        traffic_note = ("HBM bytes per stream-form scan launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 PMC passes of "
+                        "`bench.py --steps 1 --warmup 0 --no-cpu`, %s): %.3g x the algorithmic bytes"
+                        % (os.path.relpath(PMC_TRAFFIC, ROOT), t["hbm_over_alg"]))
     if rank == 0:
+        stats = {k: v for k, v in st.as_dict().items()}
         res = {
             "metric": "merges/sec (BasicTokenizer.train, 1 GiB corpus, vocab 32000) + pair-count HBM GB/s",
             "value": value,
@@ -170,7 +258,7 @@ def main():
                        "parallelism": "single GPU" if world == 1 else f"token stream sharded x{world}",
                        "comm": comm_backend},
             "roofline": {
-                "kernel": "zbpe_scan_pairs",
+                "kernel": "zbpe_scan_pairs_t (stream form)",
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBPS,
@@ -178,24 +266,31 @@ def main():
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
                 "traffic_note": traffic_note,
-                "note": "per GPU (rank 0): achieved = sum over the timed scan launches (every 8th merge, HIP events on the engine "
-                        "stream) of 2 B x live tokens / sum of their durations; bytes actually streamed (block skipping, "
-                        "holes) / algorithmic bytes over all launches: %.3g" % (read_bytes / max(all_alg_bytes, 1)),
+                "note": ("per GPU (rank 0): achieved = algorithmic bytes (2 B x live tokens, SURVEY.md 8d) of the stream-form "
+                         "scan launches timed with HIP events on the engine stream in the probe train / their summed "
+                         "durations; %s" % (
+                             "%d of %d stream launches timed, %.1f us and %.3g GB per launch on average; the timed steps' "
+                             "1-in-8 sample gave %.0f GB/s" % (probe["timed_launches"], probe["stream_launches"],
+                                                                probe["avg_launch_us"], probe["alg_bytes_per_launch"] / 1e9,
+                                                                sampled) if probe else "timed steps' 1-in-8 sample")),
             },
             "pair_count_GBps": achieved,
-            "stats": {k: v for k, v in st.as_dict().items()},
+            "list_scan": probe["list_form"] if probe else None,
+            "time_stats": {k: stats[k] for k in ("count_pairs_s", "sort_pairs_s", "replace_pair_s", "other_s", "total_s")},
+            "stats": stats,
             "corpus_gen_s": gen_s,
         }
-        if not args.no_cpu:
-            res["cpu_baseline"] = cpu_baseline(text, args.cpu_sample_bytes, args.cpu_sample_merges, args.vocab,
-                                               int(st.sum_tokens), merges)
+        if world > 1:
+            res["phases"] = {k: stats.get(k) for k in ("sharded_s", "replicate_s", "replicated_s", "comm_s", "sharded_merges")}
+        if not args.no_cpu and world == 1 and probe is not None:
+            cb = cpu_baseline(eng, text, args.vocab, probe["live"], args.cpu_late_merge)
+            p0, p1 = cb.pop("_pairs")
+            k = cb["late_merge"]
+            cb["oracle_agrees_with_gpu"] = bool(p0 == tuple(int(v) for v in m[0, :2]) and
+                                                (k >= len(m) or p1 == tuple(int(v) for v in m[k, :2])))
+            res["cpu_baseline"] = cb
         else:
             res["cpu_baseline"] = None
-        if args.scan_log_out:
-            tr = eng.trace()
-            with open(args.scan_log_out, "w") as f:
-                json.dump({"scan_log": eng.scan_log().tolist(),
-                           "live": tr[:, zbpe.TRACE_COLUMNS.index("live")].astype(np.int64).tolist()}, f)
         if args.stats_out:
             with open(args.stats_out, "w") as f:
                 json.dump({"merges": m.tolist(), "counts": c.tolist()}, f)

@@ -125,8 +125,9 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * see engine.hip kScanVariants), "hot_target" (ids kept by the argmax hot list),
  * "block_skip" (0/1: stream only the 8192-slot blocks that hold the pair's rarer token),
  * "trace" (0/1: record per-merge timings, see zbpe_trace), "merge_batch" (merges enqueued per host
- * sync, 1 = synchronous loop), "merge_timing" (HIP events around every merge of a batch until the
- * occurrence lists are on, then around every N-th; 0 = none), "sel_prof" (in-kernel wall-clock
+ * sync, 1 = synchronous loop), "merge_timing" (HIP events around every N-th merge of a batch; 0 =
+ * none), "timing_full" (0/1: also around every merge of a batch that follows one with stream-form
+ * scans, so the scan roofline covers nearly every stream scan), "sel_prof" (in-kernel wall-clock
  * probes of the merge pipeline, printed to stderr after train), "replace_split" (profiling: apply and count update as separate launches), "list_mode"
  * (0: always stream the token stream; 1: token occurrence lists once counts are small), "list_ratio"
  * (list scan when list length * ratio < stream slots), "list_start" (build the lists at a compaction
@@ -145,6 +146,15 @@ zbpe_status zbpe_format_time_stats(const zbpe_stats *stats, char *buf, size_t ca
  * *gbps = 2 B per stream slot / average launch time. */
 zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, double *avg_ms, double *gbps);
 
+/* Benchmark diagnostic, after zbpe_train*: `reps` launches of the pair scan for the pair at the top of
+ * the current selection (the next merge's argmax, ties not broken), as training would launch it
+ * (the occurrence-list form when its list is short), on a grid of `grid` workgroups (0: training's).
+ * The per-merge counters are reset between launches; stream, lists and counts stay as they were.
+ * *avg_us: average launch time (HIP events); *pair: first | second << 16; *mode: 1 list, 0 stream;
+ * *list_len: entries of the walked list. */
+zbpe_status zbpe_bench_train_scan(zbpe_ctx *ctx, int reps, int grid, double *avg_us, uint32_t *pair, uint32_t *list_len,
+                                  int *mode);
+
 /* Profiling diagnostic: with option "trace" = 1, train records one row of ZBPE_TRACE_COLS floats per
  * merge: {merge index, count, live tokens, stream slots, slots streamed by the scan (a list scan in a
  * device-resident batch: entries of the walked list), scan ms,
@@ -152,6 +162,13 @@ zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, dou
  * rows of the last train into `rows`; returns the number of rows recorded in *n_rows. */
 #define ZBPE_TRACE_COLS 11
 zbpe_status zbpe_trace(zbpe_ctx *ctx, float *rows, size_t cap_rows, size_t *n_rows);
+
+/* Profiling diagnostic: the device's per-merge log of the last train, ZBPE_MERGE_LOG_COLS u32 per merge:
+ * {pair (first | second << 16), count, live tokens, tied pairs, scan form (1 list), walked list entries,
+ * live occurrences of the list's token, 0}. Rows of merges the synchronous path finished are zero
+ * beyond what it logs. Copies up to cap_rows rows; *n_rows = merges of the last train. */
+#define ZBPE_MERGE_LOG_COLS 8
+zbpe_status zbpe_merge_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_t *n_rows);
 
 /* Profiling diagnostic: one entry per pair-scan kernel launch (zbpe_scan_pairs_t) of the last
  * train, in launch order: 2 * (merge index) + form (0 stream scan, 1 list scan), or -1 for a launch

@@ -227,3 +227,65 @@ def test_oracle_prefix_first_merges_large(engine):
     m, c, st = _train(engine, text, 262)
     assert m.tolist() == r.merges.tolist()
     assert c.tolist() == r.counts.tolist()
+
+
+def test_c_abi_consumer_mirrors_main_zig(tmp_path):
+    """tests/c_abi/main (C, include/zbpe.h + libzbpe.so only) does what src/main.zig:8-43 does: train
+    taylorswift.txt at vocab 300, write merges.txt, encode and decode the main.zig:25 string. merges.txt
+    must be the reference's bytes and decode(encode(s)) == s; the tokens equal the oracle's encode."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "c_abi", "main")
+    assert os.access(exe, os.X_OK), "tests/c_abi/main not built (__graft_entry__.build())"
+    txt = tmp_path / "taylorswift.txt"
+    txt.write_bytes(c1_text())
+    out = tmp_path / "merges.txt"
+    r = subprocess.run([exe, str(txt), str(out)], capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode(errors="replace")
+    assert out.read_bytes() == c1_merges_txt()
+    msg = "hello world!!!? (안녕하세요!) lol123 😉".encode()
+    lines = r.stdout.decode().splitlines()
+    want = O.encode(np.asarray(c1_golden()["merges"], dtype=np.uint16), msg)
+    assert lines[1].split() == [str(int(t)) for t in want]
+    assert lines[2].encode() == msg
+    assert b"Time statistics:" in r.stderr and b"sortCodePointPairs:" in r.stderr
+
+
+def test_verbose_lines_match_print_merge_info(capfd):
+    """verbose=True prints printMergeInfo's line per merge (basic_tokenizer.zig:308-317), identical to
+    the oracle's, in merge order (the device-resident batches print theirs after each batch)."""
+    text = c1_text()
+    e = zbpe.Engine(0)
+    capfd.readouterr()
+    O.train(text, 300, verbose=True)
+    ref = [l for l in capfd.readouterr().err.splitlines() if l.startswith("merge ")]
+    e.train(text, 300, verbose=True)
+    got = [l for l in capfd.readouterr().err.splitlines() if l.startswith("merge ")]
+    e.close()
+    assert len(ref) == 44 and got == ref
+    text = synth_text(synth_goldens()[0])
+    e = zbpe.Engine(0)
+    O.train(text, 400, verbose=True)
+    ref = [l for l in capfd.readouterr().err.splitlines() if l.startswith("merge ")]
+    e.train(text, 400, verbose=True)
+    got = [l for l in capfd.readouterr().err.splitlines() if l.startswith("merge ")]
+    e.close()
+    assert got == ref
+
+
+def test_basic_tokenizer_prints_time_stats(capfd):
+    """BasicTokenizer.train prints printTimeStats' block at its end, like the reference's defer (:141-145);
+    the GPU buckets never exceed the call's wall time."""
+    t = zbpe.BasicTokenizer()
+    capfd.readouterr()
+    t.train(c1_text(), 300)
+    err = capfd.readouterr().err
+    for name in ("sortCodePointPairs", "replaceTopPairWithIndex", "generateCodePointPairs", "countPointPairs",
+                 "Other operations"):
+        assert name + ":" in err
+    st = t.timeStats
+    assert st.count_pairs_s + st.sort_pairs_s + st.replace_pair_s <= st.total_s + 1e-6
+    assert st.replace_pair_calls == 44 and st.sort_pairs_calls >= 44
+    t.deinit()

@@ -126,3 +126,12 @@ def test_deserialize_semantics(tmp_path):
     t.deserializeMerges(str(p))  # appends (:346)
     got = [(m.pair.first, m.pair.second, m.new_token) for m in t.merges.merges]
     assert got == [(9, 9, 300), (1, 2, 256), (3, 40, 257), (1, 2, 3), (5, 6, 0)]
+
+
+def test_c_abi_consumer_builds():
+    """tests/c_abi/main.c includes only include/zbpe.h and links only libzbpe.so: the header compiles
+    as C11 (-pedantic -Werror) and C++17, and every entry point main.zig's flow needs resolves."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "tests", "c_abi")], check=True)
+    assert os.access(os.path.join(root, "tests", "c_abi", "main"), os.X_OK)

@@ -127,6 +127,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "merge_batch" && value >= 1) e.merge_batch = (uint32_t)std::min<int64_t>(value, zbpe::MAX_BATCH);
     else if (k == "merge_timing" && value >= 0) e.merge_timing = (uint32_t)value;
     else if (k == "sel_prof" && value >= 0) e.sel_prof = (uint32_t)value;
+    else if (k == "timing_full") e.timing_full = value != 0;
     else if (k == "replace_split") e.replace_split = value != 0;
     else if (k == "fused_select") e.fused_select = value != 0;
     else if (k == "replicate_late") e.replicate_late = value != 0;
@@ -175,6 +176,25 @@ zbpe_status zbpe_format_time_stats(const zbpe_stats *st, char *buf, size_t cap, 
 zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, double *avg_ms, double *gbps) {
     if (!ctx || !avg_ms || !gbps || reps < 1 || a == b) return ZBPE_INVALID_ARGUMENT;
     return ctx->eng.bench_scan(a, b, reps, avg_ms, gbps);
+}
+
+zbpe_status zbpe_bench_train_scan(zbpe_ctx *ctx, int reps, int grid, double *avg_us, uint32_t *pair, uint32_t *list_len,
+                                  int *mode) {
+    if (!ctx || !avg_us || !pair || !list_len || !mode || reps < 0 || grid < 0) return ZBPE_INVALID_ARGUMENT;
+    return ctx->eng.bench_train_scan(reps, grid, avg_us, pair, list_len, mode);
+}
+
+zbpe_status zbpe_merge_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_t *n_rows) {
+    if (!ctx || !n_rows || (!rows && cap_rows)) return ZBPE_INVALID_ARGUMENT;
+    const auto &L = ctx->eng.h_log;
+    *n_rows = std::min(ctx->eng.run.merges, L.size());
+    const size_t k = std::min(cap_rows, *n_rows);
+    for (size_t i = 0; i < k; i++) {
+        const zbpe::MergeLog &m = L[i];
+        const uint32_t r[ZBPE_MERGE_LOG_COLS] = {m.key, m.count, m.live, m.ties, m.mode, m.list_len, m.key_live, 0};
+        memcpy(rows + i * ZBPE_MERGE_LOG_COLS, r, sizeof r);
+    }
+    return ZBPE_OK;
 }
 
 zbpe_status zbpe_trace(zbpe_ctx *ctx, float *rows, size_t cap_rows, size_t *n_rows) {

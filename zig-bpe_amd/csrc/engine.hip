@@ -597,6 +597,48 @@ zbpe_status Engine::bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms,
     return ZBPE_OK;
 }
 
+// Late-phase scan microbenchmark on a trained context: `reps` launches of the pair scan for the pair
+// at the top of the current selection, exactly as training would launch it for the next merge (list
+// form when its list is short), with the per-merge counters and deltas reset between launches. The
+// stream, the lists and the counts are left as they were (records land past the arena top).
+zbpe_status Engine::bench_train_scan(int reps, int grid, double *avg_us, uint32_t *pair, uint32_t *list_len, int *mode) {
+    if (!trained || world > 1) return fail(ZBPE_INVALID_ARGUMENT, "bench_train_scan needs a trained single-GPU context");
+    HIP_OK(hipSetDevice(device));
+    CHECK(sync_state());
+    const uint32_t key = h_st->top_key, a = key & 0xFFFF, b = key >> 16, X = 256 + (uint32_t)run.merges;
+    if (a == b || !h_st->top_count || X >= 65536) return fail(ZBPE_INVALID_ARGUMENT, "no scannable pair (self pair or exhausted)");
+    uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
+    ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
+               nullptr, pres_vp, X, T.tok_cnt, 0, nullptr, lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1,
+               d_log, nullptr, 0};
+    double total = 0;
+    for (int r = 0; r <= reps; r++) {
+        zbpe_reset_merge<<<(X + 255) / 256, 256, 0, stream>>>(d_st, left, right, X);
+        LAUNCH_OK();
+        HIP_OK(hipMemsetAsync(tail, 0, 8, stream));
+        HIP_OK(hipEventRecord(ev[0], stream));
+        CHECK(launch_scan(A, grid));
+        HIP_OK(hipEventRecord(ev[1], stream));
+        HIP_OK(hipEventSynchronize(ev[1]));
+        float ms;
+        HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        if (r) total += ms;  // the first launch warms up
+    }
+    zbpe_reset_merge<<<(X + 255) / 256, 256, 0, stream>>>(d_st, left, right, X);
+    LAUNCH_OK();
+    HIP_OK(hipMemsetAsync(tail, 0, 8, stream));
+    CHECK(sync_state());
+    MergeLog L{};
+    HIP_OK(hipMemcpy(&L, d_log + (X - 256), sizeof L, hipMemcpyDeviceToHost));
+    *avg_us = reps ? total * 1e3 / reps : 0;
+    *pair = key;
+    *mode = (int)h_st->scan_mode;
+    *list_len = h_st->scan_mode ? L.list_len : 0;
+    if (h_st->scan_mode) fprintf(stderr, "bench_train_scan: pair (%u,%u) count %u: walked list %u entries, %u live\n", a, b,
+                                 h_st->top_count, L.list_len, L.key_live);
+    return ZBPE_OK;
+}
+
 // a self pair (a, a) walks a's occurrence list when the lists describe the stream, no shard edge
 // is involved and the list is short against the stream (self_list_ratio; the stream form costs
 // three passes over it)
@@ -746,6 +788,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     run.vocab = vocab_size;
     trace.clear();
     scan_log.clear();
+    std::fill(h_log.begin(), h_log.end(), MergeLog{});
     uint32_t X = 256;
     while (X < vocab_size) {
         if (h_st->live <= 0) {  // sortedCodePointPairs.len == 0 (basic_tokenizer.zig:188-191)
@@ -816,13 +859,16 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                         "tie gather %.2f, decide %.2f; argmax blocks done %.2f, refresh blocks done %.2f\n",
                 P[7], P[0] * us / calls, P[1] * us / calls, P[2] * us / calls, P[3] * us / calls, P[4] * us / calls,
                 P[5] * us / calls, P[6] * us / calls);
-        const unsigned long long *Q = h_st->pipe_prof;
-        const double nl = std::max(1.0, (double)Q[4]), nr = std::max(1.0, (double)Q[7]), ns = std::max(1.0, (double)Q[9]);
-        fprintf(stderr, "pipe_prof: list scans %llu: avg us from the launch's block-0 start: LDS clear done %.2f, walk done %.2f, "
-                        "flush done %.2f, replace starts %.2f; replace (%llu): work done %.2f, select starts %.2f; "
-                        "select end -> scan start (%llu) %.2f\n",
-                Q[4], Q[0] * us / nl, Q[1] * us / nl, Q[2] * us / nl, Q[3] * us / nl, Q[7], Q[5] * us / nr, Q[6] * us / nr,
-                Q[9], Q[8] * us / ns);
+        static const char *bucket[3] = {"merges < 7936", "merges 7936-19743", "merges >= 19744"};
+        for (int k = 0; k < 3; k++) {
+            const unsigned long long *Q = h_st->pipe_prof[k];
+            const double nl = std::max(1.0, (double)Q[4]), nr = std::max(1.0, (double)Q[7]), ns = std::max(1.0, (double)Q[9]);
+            fprintf(stderr, "pipe_prof %s: list scans %llu: avg us from the launch's block-0 start: LDS clear done %.2f, walk "
+                            "done %.2f, flush done %.2f, replace starts %.2f; replace (%llu): work done %.2f, select starts %.2f; "
+                            "select end -> scan start (%llu) %.2f\n",
+                    bucket[k], Q[4], Q[0] * us / nl, Q[1] * us / nl, Q[2] * us / nl, Q[3] * us / nl, Q[7], Q[5] * us / nr,
+                    Q[6] * us / nr, Q[9], Q[8] * us / ns);
+        }
     }
     stats.total_s = now_s() - t_start;
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
@@ -872,7 +918,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top0 / 256 + 1);
     const int64_t slots = n_slots;
     const double t0 = now_s();
-    lists_at_batch = lists_on;
+    lists_at_batch = list_streak;  // the last batch only walked lists: sample this one
     if (merge_timing) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * MAX_BATCH], stream));
     for (uint32_t i = 0; i < K; i++) {
         const uint32_t X = X0 + i;
@@ -978,7 +1024,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         float ms_sel = 0, ms_scan = 0, ms_rep = 0, ms_begin = 0;
         if (merge_timed(X)) {
             const hipEvent_t *E = &bev[BEV_PER_MERGE * i];
-            const double w = lists_at_batch ? merge_timing : 1.0;  // the merges this one stands for
+            const double w = merge_weight();  // the merges this one stands for
             HIP_OK(hipEventElapsedTime(&ms_begin, E[0], E[1]));
             HIP_OK(hipEventElapsedTime(&ms_scan, E[1], E[2]));
             HIP_OK(hipEventElapsedTime(&ms_rep, E[2], E[3]));

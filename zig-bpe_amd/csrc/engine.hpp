@@ -121,12 +121,17 @@ struct Engine {
     // device-resident merge loop
     uint32_t merge_batch = 32;      // merges enqueued per host sync (1: synchronous loop)
     uint32_t sel_prof = 0;          // phase timestamps inside zbpe_select_next (printed to stderr after train)
-    // HIP events around the merges of a batch (0: none): every merge while the scans stream the token
-    // stream (a merge takes 100s of us there: the roofline covers every stream-form scan), every
-    // merge_timing-th once the occurrence lists are on (a late merge takes ~50 us; an event pair costs ~1)
-    uint32_t merge_timing = 32;
-    bool lists_at_batch = false;    // lists were on when the current batch was enqueued
-    bool merge_timed(uint32_t X) const { return merge_timing && (!lists_at_batch || X % merge_timing == 0); }
+    // HIP events around every merge_timing-th merge of a batch (0: none); with timing_full also around
+    // every merge of a batch that follows one with stream-form scans (those take 100s of us: the
+    // roofline then sees nearly every stream scan; each event adds ~1 us of gap, so the bench's timed
+    // steps sample and a separate probe train sets timing_full)
+    uint32_t merge_timing = 8;
+    bool timing_full = false;
+    bool lists_at_batch = false;    // the batch being enqueued follows a list-only batch
+    bool merge_timed(uint32_t X) const {
+        return merge_timing && ((timing_full && !lists_at_batch) || X % merge_timing == 0);
+    }
+    double merge_weight() const { return timing_full && !lists_at_batch ? 1.0 : (double)merge_timing; }
     bool replace_split = false;     // profiling: apply and count update as separate launches
     bool fused_select = true;       // zbpe_select_next: the select of merge X also starts merge X+1 (ties included)
     bool begun = false;             // the next batch's first merge was started by the last batch's final select
@@ -176,6 +181,7 @@ struct Engine {
     zbpe_status tokens(uint16_t *out, size_t cap, size_t *n_tokens);
     zbpe_status set_scan_variant(int v);
     zbpe_status bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms, double *gbps);
+    zbpe_status bench_train_scan(int reps, int grid, double *avg_us, uint32_t *pair, uint32_t *list_len, int *mode);
 
    private:
     zbpe_status sync_state();

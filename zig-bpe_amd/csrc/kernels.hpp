@@ -295,6 +295,9 @@ __device__ inline int64_t prev_live(const uint16_t *tok, int64_t i) {
 // ones, the common neighbours once merges are long) in a small LDS hash of (token << 16 | count)
 // with a few linear probes, and only the rest straight to HBM. Contended global atomics on a few hot
 // neighbour tokens cost more than the whole list walk of a late merge.
+#ifndef ZBPE_LIST_WIDE
+#define ZBPE_LIST_WIDE 0  // list scans: load each entry's neighbour words with its vector (A/B build switch)
+#endif
 constexpr int HASH_LOG = 9;
 constexpr int HASH_BINS = 1 << HASH_LOG;
 struct NeighbourHist {
@@ -330,6 +333,9 @@ struct NeighbourHist {
     __device__ inline void left(uint16_t t) { add(lds_left, h_left, g_left, t); }
     __device__ inline void right(uint16_t t) { add(lds_right, h_right, g_right, t); }
 };
+
+// option sel_prof: merge-index bucket of the pipeline probes (DevState::pipe_prof)
+__device__ inline int pp_bucket(uint32_t X) { return X < 8192 ? 0 : X < 20000 ? 1 : 2; }
 
 struct ScanArgs {
     const uint16_t *tok;
@@ -725,7 +731,11 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
         if (len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n) {
             if (blockIdx.x == 0 && threadIdx.x == 0) {
                 A.st->scan_mode = 1;
-                if (A.log) { A.log[A.X - 256].mode = 1; A.log[A.X - 256].list_len = len; }
+                if (A.log) {
+                    A.log[A.X - 256].mode = 1;
+                    A.log[A.X - 256].list_len = len;
+                    A.log[A.X - 256].key_live = A.tokcnt ? (uint32_t)A.tokcnt[by_b ? A.b : A.a] : 0u;
+                }
                 if (A.prof) A.st->pp_t[4] = 1;
             }
             scan_list_body(A, by_b, A.lists + (by_b ? ob : oa), len, S);
@@ -740,7 +750,8 @@ __global__ void __launch_bounds__(SCAN_THREADS, 4) zbpe_scan_pairs_t(ScanArgs A0
     if (A0.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // the last select's end -> this scan's start
         DevState *st = A0.st;
         const unsigned long long now = wall_clock64();
-        if (st->pp_t[7]) { st->pipe_prof[8] += now - st->pp_t[7]; st->pipe_prof[9]++; st->pp_t[7] = 0; }
+        unsigned long long *P = st->pipe_prof[pp_bucket(A0.X)];
+        if (st->pp_t[7]) { P[8] += now - st->pp_t[7]; P[9]++; st->pp_t[7] = 0; }
         st->pp_t[0] = now;
     }
     if (A0.dyn && A0.st->halt) return;
@@ -878,14 +889,36 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
         uint4 cvs[LU];
 #pragma unroll
         for (int u = 0; u < LU; u++) cvs[u] = tv[(ps[u] < 0 ? 0 : ps[u]) >> 3];
+#if ZBPE_LIST_WIDE
+        // the window's neighbour words with the vector (no second round trip for a candidate)
+        uint32_t pws[LU];
+        uint2 nvs[LU];
+#pragma unroll
+        for (int u = 0; u < LU; u++) {
+            const int64_t vi = (ps[u] < 0 ? 0 : ps[u]) >> 3;
+            pws[u] = tv[vi > 0 ? vi - 1 : 0].w;
+            nvs[u] = *reinterpret_cast<const uint2 *>(&tv[vi + 1 < nvec ? vi + 1 : vi]);
+        }
+#endif
 #pragma unroll 1
         for (int u = 0; u < LU; u++) {
             // this entry's values (selects, not an indexed private array)
             int64_t p = ps[0];
             uint4 cv = cvs[0];
+#if ZBPE_LIST_WIDE
+            uint32_t wpw = pws[0];
+            uint2 wnv = nvs[0];
+#endif
 #pragma unroll
             for (int k2 = 1; k2 < LU; k2++)
-                if (u == k2) { p = ps[k2]; cv = cvs[k2]; }
+                if (u == k2) {
+                    p = ps[k2];
+                    cv = cvs[k2];
+#if ZBPE_LIST_WIDE
+                    wpw = pws[k2];
+                    wnv = nvs[k2];
+#endif
+                }
             bool cand = false;
             if (p >= 0) {
                 const int k = (int)(p & 7);
@@ -897,12 +930,17 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
             uint32_t pw = 0xffffffffu, nx = 0xffffffffu, ny = 0xffffffffu;
             if (cand) {
                 const int64_t vi = p >> 3;
+#if ZBPE_LIST_WIDE
+                if (vi > 0) pw = wpw;
+                if (vi + 1 < nvec) { nx = wnv.x; ny = wnv.y; }
+#else
                 if (vi > 0) pw = tv[vi - 1].w;
                 if (vi + 1 < nvec) {
                     const uint2 nv = *reinterpret_cast<const uint2 *>(&tv[vi + 1]);
                     nx = nv.x;
                     ny = nv.y;
                 }
+#endif
             }
             bool hit = false;
             uint32_t pr = 0;
@@ -1556,12 +1594,13 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
     if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the list scan's stamps
         const unsigned long long now = wall_clock64();
         if (st->pp_t[4]) {
+            unsigned long long *P = st->pipe_prof[pp_bucket(R.X)];
             const unsigned long long t0 = st->pp_t[0];
-            st->pipe_prof[0] += st->pp_t[1] - t0;
-            st->pipe_prof[1] += st->pp_t[2] - t0;
-            st->pipe_prof[2] += st->pp_t[3] - t0;
-            st->pipe_prof[3] += now - t0;
-            st->pipe_prof[4]++;
+            P[0] += st->pp_t[1] - t0;
+            P[1] += st->pp_t[2] - t0;
+            P[2] += st->pp_t[3] - t0;
+            P[3] += now - t0;
+            P[4]++;
         }
         st->pp_t[1] = st->pp_t[2] = st->pp_t[3] = st->pp_t[4] = 0;
         st->pp_t[5] = now;
@@ -2765,9 +2804,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         const unsigned long long now = wall_clock64();
         st->sel_t0 = now;
         if (st->pp_t[5]) {  // the replace launch: its work span, its start -> this select's start
-            st->pipe_prof[5] += st->pp_t[6] - st->pp_t[5];
-            st->pipe_prof[6] += now - st->pp_t[5];
-            st->pipe_prof[7]++;
+            unsigned long long *P = st->pipe_prof[pp_bucket(X)];
+            P[5] += st->pp_t[6] - st->pp_t[5];
+            P[6] += now - st->pp_t[5];
+            P[7]++;
             st->pp_t[5] = st->pp_t[6] = 0;
         }
     }

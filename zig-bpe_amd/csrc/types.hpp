@@ -70,7 +70,7 @@ struct DevState {
     // sums they fold into (Engine::train prints them): scan (list form) LDS clear / walk / flush done and
     // the next kernel's start, replace work span and the select's start, select end -> scan start
     unsigned long long pp_t[8];
-    unsigned long long pipe_prof[16];
+    unsigned long long pipe_prof[3][16];  // by merge: [256, 8192), [8192, 20000), [20000, ...)
 };
 // why a device-resident batch stopped (the host finishes that merge on the synchronous path)
 enum HaltReason : uint32_t {
@@ -87,7 +87,8 @@ struct MergeLog {
     uint32_t key, count, live, ties;
     uint32_t mode;     // 0: stream scan, 1: list scan
     uint32_t list_len; // list scan: entries of the walked occurrence list
-    uint32_t pad[2];
+    uint32_t key_live; // list scan: live occurrences of the list's token (the walk's useful entries)
+    uint32_t pad;
 };
 
 struct Tables {

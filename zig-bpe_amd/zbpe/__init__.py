@@ -141,8 +141,9 @@ class Stats(ctypes.Structure):
 EXPORTS = (
     "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_create_dist_host", "zbpe_destroy", "zbpe_last_error",
     "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts", "zbpe_tokens",
-    "zbpe_set_option", "zbpe_format_time_stats", "zbpe_bench_scan", "zbpe_trace", "zbpe_scan_log", "zbpe_zig_order_winner", "zbpe_version",
+    "zbpe_set_option", "zbpe_format_time_stats", "zbpe_bench_scan", "zbpe_bench_train_scan", "zbpe_merge_log", "zbpe_trace", "zbpe_scan_log", "zbpe_zig_order_winner", "zbpe_version",
 )
+MERGE_LOG_COLUMNS = ("key", "count", "live", "ties", "list_scan", "list_len", "key_live", "zero")
 TRACE_COLUMNS = ("merge", "count", "live", "slots", "streamed", "scan_ms", "replace_ms", "select_ms", "wall_ms",
                  "self_pair", "ties")
 
@@ -201,8 +202,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_train_resident.argtypes = [vp, ctypes.c_uint16, ctypes.c_int, u16p, u64p, ctypes.POINTER(sz), ctypes.POINTER(Stats)]
     L.zbpe_encode.argtypes = [vp, u16p, sz, vp, sz, u16p, ctypes.POINTER(sz)]
     L.zbpe_verify_counts.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
-    L.zbpe_tokens.argtypes = [vp, u16p, sz, ctypes.POINTER(sz)]
-    L.zbpe_format_time_stats.argtypes = [ctypes.POINTER(Stats), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    if hasattr(L, "zbpe_tokens"):  # (absent from older builds loaded for A/B runs through ZBPE_LIB)
+        L.zbpe_tokens.argtypes = [vp, u16p, sz, ctypes.POINTER(sz)]
+        L.zbpe_format_time_stats.argtypes = [ctypes.POINTER(Stats), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    if hasattr(L, "zbpe_merge_log"):
+        L.zbpe_merge_log.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    if hasattr(L, "zbpe_bench_train_scan"):
+        L.zbpe_bench_train_scan.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                            ctypes.POINTER(ctypes.c_int)]
     L.zbpe_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
     L.zbpe_bench_scan.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double)]
@@ -211,7 +219,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_zig_order_winner.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
     L.zbpe_version.restype = ctypes.c_char_p
     for name in EXPORTS:
-        if name not in ("zbpe_destroy", "zbpe_last_error", "zbpe_version"):
+        if name not in ("zbpe_destroy", "zbpe_last_error", "zbpe_version") and hasattr(L, name):
             getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -305,6 +313,13 @@ class Engine:
         self._check(self._L.zbpe_bench_scan(self._ctx, a, b, reps, ctypes.byref(ms), ctypes.byref(gbps)), "zbpe_bench_scan")
         return ms.value, gbps.value
 
+    def bench_train_scan(self, reps: int = 20, grid: int = 0) -> dict:
+        """Late-phase scan microbenchmark on the trained state (zbpe_bench_train_scan)."""
+        us, pair, ln, mode = ctypes.c_double(0), ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_int(0)
+        self._check(self._L.zbpe_bench_train_scan(self._ctx, reps, grid, ctypes.byref(us), ctypes.byref(pair), ctypes.byref(ln),
+                                                  ctypes.byref(mode)), "zbpe_bench_train_scan")
+        return {"us": us.value, "pair": (pair.value & 0xFFFF, pair.value >> 16), "list_len": ln.value, "mode": mode.value}
+
     def trace(self):
         """Per-merge rows of the last train (option "trace" = 1): float32 array [merges, len(TRACE_COLUMNS)]."""
         import numpy as np
@@ -314,6 +329,15 @@ class Engine:
         out = np.zeros((n.value, len(TRACE_COLUMNS)), dtype=np.float32)
         if n.value:
             self._check(self._L.zbpe_trace(self._ctx, _ptr(out), n.value, ctypes.byref(n)), "zbpe_trace")
+        return out
+
+    def merge_log(self) -> np.ndarray:
+        """Device per-merge log of the last train: uint32 [merges, 8] (see MERGE_LOG_COLUMNS)."""
+        n = ctypes.c_size_t(0)
+        self._check(self._L.zbpe_merge_log(self._ctx, None, 0, ctypes.byref(n)), "zbpe_merge_log")
+        out = np.zeros((n.value, 8), dtype=np.uint32)
+        if n.value:
+            self._check(self._L.zbpe_merge_log(self._ctx, _ptr(out), n.value, ctypes.byref(n)), "zbpe_merge_log")
         return out
 
     def scan_log(self) -> np.ndarray:
