@@ -64,6 +64,12 @@ typedef struct zbpe_stats {
     uint64_t list_scans;      /* pair scans that walked a token occurrence list instead of the stream */
     uint64_t list_builds;     /* occurrence-list rebuilds (after compactions) */
     uint64_t replications;    /* multi-GPU: 1 once the ranks gathered the whole stream for the late phase */
+    /* multi-GPU phase split (wall, host clock): merges while the stream is sharded (per-merge
+     * collectives), the one-time replication (compaction + all-gather of the shards + list build), the
+     * merges after it (replicas, no collective); comm_s: device time of the per-merge count-delta
+     * all-reduce, from the HIP events of the timed merges, split like the stage buckets */
+    double sharded_s, replicate_s, replicated_s, comm_s;
+    uint64_t sharded_merges;
 } zbpe_stats;
 
 /* Create a single-GPU context on HIP device `device`. */
@@ -127,7 +133,10 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * "trace" (0/1: record per-merge timings, see zbpe_trace), "merge_batch" (merges enqueued per host
  * sync, 1 = synchronous loop), "merge_timing" (HIP events around every N-th merge of a batch; 0 =
  * none), "timing_full" (0/1: also around every merge of a batch that follows one with stream-form
- * scans, so the scan roofline covers nearly every stream scan), "sel_prof" (in-kernel wall-clock
+ * scans, so the scan roofline covers nearly every stream scan), "arena_cap" (tests: occurrence-arena entries to allocate;
+ * the arena grows when a merge needs more), "list_nb" (0/1: list entries carry their build-time
+ * neighbours and a list scan gathers the stream only at entries whose neighbour is the pair's other
+ * token), "sel_prof" (in-kernel wall-clock
  * probes of the merge pipeline, printed to stderr after train), "replace_split" (profiling: apply and count update as separate launches), "list_mode"
  * (0: always stream the token stream; 1: token occurrence lists once counts are small), "list_ratio"
  * (list scan when list length * ratio < stream slots), "list_start" (build the lists at a compaction

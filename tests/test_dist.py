@@ -31,6 +31,10 @@ CASES = [
     dict(kind="runs", seed=66, n=60000, vocab=500, options={"list_start": 0}, replicated=True),
     # the same without the late-phase replication (every merge sharded to the end)
     dict(kind="words_utf8", seed=65, n=200000, vocab=900, options={"list_start": 0, "replicate_late": 0}),
+    # a shrunken occurrence arena: halts and compactions are decided on replicated bounds (every rank
+    # alike), and a global top count above the arena grows it on every rank (run-heavy: skewed counts)
+    dict(kind="runs", seed=67, n=60000, vocab=450, options={"arena_cap": 3000, "replicate_late": 0}),
+    dict(text=b"ab" * 20000 + b"xy" * 3000, vocab=320, options={"arena_cap": 12000, "replicate_late": 0}),
 ]
 
 

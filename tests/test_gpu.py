@@ -289,3 +289,38 @@ def test_basic_tokenizer_prints_time_stats(capfd):
     assert st.count_pairs_s + st.sort_pairs_s + st.replace_pair_s <= st.total_s + 1e-6
     assert st.replace_pair_calls == 44 and st.sort_pairs_calls >= 44
     t.deinit()
+
+
+@pytest.mark.parametrize("cap", [2000, 50000])
+def test_small_arena_grows_and_matches_oracle(cap):
+    """A shrunken occurrence arena (option arena_cap): compactions and growth of the arena (keeping its
+    lists) when a merge needs more room; merges and counts still equal the oracle's."""
+    text = zbpe.synth_corpus("words_utf8", 71, 200000)
+    r = O.train(text, 700)
+    e = zbpe.Engine(0)
+    e.set_option("arena_cap", cap)
+    e.set_option("list_start", 0)
+    m, c, st = e.train(text, 700)
+    assert m.tolist() == r.merges.tolist() and c.tolist() == r.counts.tolist()
+    assert e.verify_counts() == 0
+    e.close()
+
+
+@pytest.mark.parametrize("nb", [0, 1])
+def test_list_neighbour_filter_agrees(nb):
+    """List scans with and without the build-time neighbour filter (option list_nb) give the oracle's
+    merges, with lists from the first compaction on and every scan that can use one walking it."""
+    for kind, seed, n, vocab in (("words_utf8", 72, 300000, 900), ("runs", 73, 60000, 500), ("uniform", 74, 20000, 700)):
+        text = zbpe.synth_corpus(kind, seed, n)
+        r = O.train(text, vocab)
+        e = zbpe.Engine(0)
+        e.set_option("list_nb", nb)
+        e.set_option("list_start", 0)
+        e.set_option("list_ratio", 1)
+        e.set_option("compact_den", 2)
+        m, c, st = e.train(text, vocab)
+        assert m.tolist() == r.merges.tolist() and c.tolist() == r.counts.tolist(), (kind, nb)
+        assert e.verify_counts() == 0
+        other = zbpe.synth_corpus(kind, seed + 100, n)
+        assert np.array_equal(e.encode(m, other), O.encode(m, other)), (kind, nb)
+        e.close()

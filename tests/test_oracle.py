@@ -151,3 +151,64 @@ def test_step_matches_train(literal):
         s = O.step(r.tokens, literal=literal)
         assert s.pair == tuple(g["merges"][5][:2]) and s.count == g["counts"][5]
     assert O.step(np.zeros(1, np.uint16)) is None and O.step(np.zeros(0, np.uint16)) is None
+
+
+def _apply_merges_with_holes(text: bytes, merges, on_merge):
+    """replaceTopPairWithNewToken (basic_tokenizer.zig:207-232) on a position-stable stream: merged-away
+    slots become holes instead of being squeezed out, as in the device stream. on_merge(k, toks, alive,
+    occ) sees each merge's occurrence starts before they are applied."""
+    toks = np.frombuffer(text, np.uint8).astype(np.int64)
+    alive = np.ones(len(toks), bool)
+    for k, (a, b, x) in enumerate(np.asarray(merges, dtype=np.int64)):
+        idx = np.flatnonzero(alive)
+        seq = toks[idx]
+        if a != b:
+            occ = idx[:-1][(seq[:-1] == a) & (seq[1:] == b)]
+        else:  # left-greedy over runs of a
+            occ, i = [], 0
+            while i + 1 < len(seq):
+                if seq[i] == a and seq[i + 1] == a:
+                    occ.append(idx[i])
+                    i += 2
+                else:
+                    i += 1
+            occ = np.asarray(occ, dtype=np.int64)
+        on_merge(k, toks, alive, occ)
+        nxt = {p: q for p, q in zip(idx[:-1], idx[1:])}
+        for p in occ:
+            toks[p] = x
+            alive[nxt[p]] = False
+
+
+@pytest.mark.parametrize("corpus", ["c1", "words_utf8"])
+def test_list_neighbour_filter_invariant(corpus):
+    """The filtered list walk (kernels.hpp scan_dispatch): after a list build at merge T, a position's
+    successor / predecessor only ever changes into a token created after T. So for a later merge (a, b)
+    with a, b both older than T, every occurrence start p had successor b at T, and its b had predecessor a."""
+    import zbpe
+    text = c1_text() if corpus == "c1" else zbpe.synth_corpus("words_utf8", 91, 120000)
+    merges = O.train(text, 300 if corpus == "c1" else 420).merges
+    builds = (5, 20)
+    snap = {}
+    checked = [0]
+
+    def on_merge(k, toks, alive, occ):
+        if k in builds:  # "build": each live position's live neighbours now
+            idx = np.flatnonzero(alive)
+            succ = np.full(len(toks), -1)
+            pred = np.full(len(toks), -1)
+            succ[idx[:-1]] = toks[idx[1:]]
+            pred[idx[1:]] = toks[idx[:-1]]
+            snap[k] = (succ, pred, 256 + k)
+        a, b, _ = merges[k]
+        nxt = np.flatnonzero(alive)
+        pos = {int(p): i for i, p in enumerate(nxt)}
+        for t, (succ, pred, lx) in snap.items():
+            if a < lx and b < lx and a != b:
+                assert np.all(succ[occ] == b), (k, t)
+                q = nxt[[pos[int(p)] + 1 for p in occ]]
+                assert np.all(pred[q] == a), (k, t)
+                checked[0] += len(occ)
+
+    _apply_merges_with_holes(text, merges, on_merge)
+    assert checked[0] > 1000

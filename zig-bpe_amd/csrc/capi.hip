@@ -128,6 +128,8 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "merge_timing" && value >= 0) e.merge_timing = (uint32_t)value;
     else if (k == "sel_prof" && value >= 0) e.sel_prof = (uint32_t)value;
     else if (k == "timing_full") e.timing_full = value != 0;
+    else if (k == "list_nb") e.list_nb = value != 0;
+    else if (k == "arena_cap" && value >= 0) e.arena_cap_opt = (uint64_t)value;
     else if (k == "replace_split") e.replace_split = value != 0;
     else if (k == "fused_select") e.fused_select = value != 0;
     else if (k == "replicate_late") e.replicate_late = value != 0;

@@ -57,7 +57,8 @@ void Engine::release() {
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_sizes);
-    f(d_enc_cnt); f(d_enc_ctr);
+    f(d_enc_cnt); f(d_enc_ctr); f(d_succ); f(d_pred);
+    d_succ = d_pred = nullptr; succ_cap = pred_cap = 0;
     d_enc_cnt = nullptr; d_enc_ctr = nullptr; enc_cnt_cap = enc_ctr_cap = 0;
     for (auto &e : bev) if (e) (void)hipEventDestroy(e);
     bev.clear();
@@ -257,15 +258,16 @@ zbpe_status Engine::compact() {
 
 // Compaction during training: positions move, so the occurrence lists are rebuilt (once they are
 // on, or once pair counts have become small against the stream), else the arena is emptied.
-zbpe_status Engine::compact_train() {
+zbpe_status Engine::compact_train(uint32_t X) {
     HIP_OK(hipEventRecord(ev[3], stream));
     CHECK(compact());
     const bool want = list_mode && pres_vp <= PRES_MAX_VP && (uint64_t)n_slots < 0xF0000000ull &&
                       (lists_on || list_start == 0 || (uint64_t)h_st->top_count * list_start < (uint64_t)n_live);
     if (want && !(dist() && replicate_late)) {  // sharded: lists come with the replication (run_batch)
-        CHECK(build_lists());
+        CHECK(build_lists(X));
     } else {
         HIP_OK(hipMemsetAsync(&d_st->arena_top, 0, 4, stream));
+        HIP_OK(hipMemsetAsync(&d_st->arena_rep, 0, 4, stream));
         HIP_OK(hipMemsetAsync(&d_st->lists_valid, 0, 4, stream));
     }
     HIP_OK(hipEventRecord(ev[4], stream));
@@ -323,8 +325,30 @@ zbpe_status Engine::replicate() {
 }
 
 // occurrence lists of the compacted stream (no holes): counting sort of positions by token
-zbpe_status Engine::build_lists() {
+// a larger occurrence arena, keeping [0, arena_top) (the lists and this batch's records); sharded, the
+// new limit follows from replicated values only
+zbpe_status Engine::grow_arena(uint64_t need) {
+    if (need > 0xFFFFFFF0u) return fail(ZBPE_OUT_OF_MEMORY, "occurrence arena of %llu entries exceeds 2^32", (unsigned long long)need);
+    if (need > lists_cap) {
+        uint32_t *grown = nullptr;
+        if (hipMalloc(&grown, need * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(ZBPE_OUT_OF_MEMORY, "occurrence arena (%llu entries)", (unsigned long long)need);
+        }
+        CHECK(sync_state());
+        if (h_st->arena_top) HIP_OK(hipMemcpyAsync(grown, d_lists, (size_t)h_st->arena_top * 4, hipMemcpyDeviceToDevice, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        (void)hipFree(d_lists);
+        d_lists = grown;
+        lists_cap = need;
+    }
+    if (dist()) arena_cap_rep = std::max<uint64_t>(arena_cap_rep, need);
+    return ZBPE_OK;
+}
+
+zbpe_status Engine::build_lists(uint32_t lists_x) {
     const int64_t n = n_slots;
+    if ((uint64_t)n + (1u << 20) > lists_cap) CHECK(grow_arena((uint64_t)n + (16u << 20)));  // lists <= n entries
     const uint32_t nchunks = (uint32_t)std::max<int64_t>(1, (n + LIST_CHUNK - 1) / LIST_CHUNK);
     CHECK(ensure(&d_list_cnt, list_cnt_cap, (size_t)nchunks * pres_vp, "list chunk histograms"));
     zbpe_list_hist<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt);
@@ -332,15 +356,27 @@ zbpe_status Engine::build_lists() {
     zbpe_list_colscan<<<(pres_vp + 255) / 256, 256, 0, stream>>>(d_list_cnt, nchunks, pres_vp, d_list_total);
     LAUNCH_OK();
     const uint32_t max_len = (uint32_t)std::min<uint64_t>(0xFFFFFFFEu, (uint64_t)n / list_ratio);
-    zbpe_list_offsets<<<1, 1024, 0, stream>>>(d_list_total, pres_vp, max_len, T.lst_off, T.lst_len, d_st);
+    zbpe_list_offsets<<<1, 1024, 0, stream>>>(d_list_total, pres_vp, max_len, T.lst_off, T.lst_len, d_st, lists_x);
     LAUNCH_OK();
+    if (list_nb) {  // the build-time neighbours of every list entry (the filtered list walk)
+        CHECK(ensure(&d_succ, succ_cap, (size_t)n + 64, "list successors"));
+        CHECK(ensure(&d_pred, pred_cap, (size_t)n + 64, "list predecessors"));
+    }
     zbpe_list_scatter<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt, T.lst_off,
-                                                                       T.lst_len, d_lists);
+                                                                       T.lst_len, d_lists, list_nb ? d_succ : nullptr,
+                                                                       list_nb ? d_pred : nullptr);
     LAUNCH_OK();
     lists_on = true;
+    nb_built = list_nb;
     pres_on = false;  // block skipping is not maintained once scans can bypass the stream
     stats.list_builds++;
     return ZBPE_OK;
+}
+
+// list scans may filter list entries by their build-time neighbours (kernels.hpp scan_dispatch)
+void Engine::set_list_nb(ScanArgs &A) const {
+    A.succ = lists_on && nb_built ? d_succ : nullptr;
+    A.pred = lists_on && nb_built ? d_pred : nullptr;
 }
 
 static uint32_t count_bin_lo(int b) {
@@ -563,7 +599,9 @@ zbpe_status Engine::set_scan_variant(int v) {
 zbpe_status Engine::launch_scan(const ScanArgs &A, int grid) {
     // default variant 0; when matches are dense (> 1/128 of the stream) the compacted phase 2
     const int v = scan_variant;
-    hipLaunchKernelGGL(kScanVariants[v], dim3(grid > 0 ? grid : scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, A);
+    // option sel_prof: the probed instantiation of the default variant
+    const ScanFn f = A.prof && v == 0 ? zbpe_scan_pairs_t<4, true, true, true, true, true> : kScanVariants[v];
+    hipLaunchKernelGGL(f, dim3(grid > 0 ? grid : scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, A);
     LAUNCH_OK();
     return ZBPE_OK;
 }
@@ -611,6 +649,7 @@ zbpe_status Engine::bench_train_scan(int reps, int grid, double *avg_us, uint32_
     ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
                nullptr, pres_vp, X, T.tok_cnt, 0, nullptr, lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1,
                d_log, nullptr, 0};
+    set_list_nb(A);
     double total = 0;
     for (int r = 0; r <= reps; r++) {
         zbpe_reset_merge<<<(X + 255) / 256, 256, 0, stream>>>(d_st, left, right, X);
@@ -724,7 +763,15 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     pres_on = block_skip && pres_vp <= PRES_MAX_VP;
     CHECK(build_presence());
     // arena: the occurrence lists (<= live tokens) + the records appended until the next compaction
-    CHECK(ensure(&d_lists, lists_cap, std::min<size_t>(0xFFFFFFF0u, n + n / 2 + (16u << 20)), "occurrence arena"));
+    {
+        const auto arena_for = [&](uint64_t m) -> uint64_t {
+            const uint64_t c = std::min<uint64_t>(0xFFFFFFF0u, m + m / 2 + (16u << 20));
+            return arena_cap_opt ? std::min<uint64_t>(c, arena_cap_opt) : c;
+        };
+        CHECK(ensure(&d_lists, lists_cap, arena_for(n), "occurrence arena"));
+        // the smallest shard's arena: a limit every rank computes alike
+        arena_cap_rep = std::min<uint64_t>(lists_cap, arena_for(sharded ? n_total / world : n));
+    }
     lists_on = false;
     list_streak = false;
     if (!T.id_key || T.id_cap < (1u << 20)) {
@@ -798,7 +845,11 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         if (merge_batch > 1 && !debug_checks && !force_exact_ties && vocab_size - X > 1) {
             uint32_t done = 0;
             bool halted = false;
+            const bool was_sharded = dist();
+            const double t_b = now_s();
             CHECK(run_batch(X, &done, &halted));
+            (was_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_b;
+            if (was_sharded) stats.sharded_merges += done;
             X += done;
             if (!halted) continue;
             // the device stopped at merge X: clear the flag, make the selection valid, finish X here
@@ -807,7 +858,11 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             CHECK(select_ready());
             if (h_st->live <= 0) continue;
         }
+        const bool was_sharded = dist();
+        const double t_m = now_s();
         CHECK(merge_sync(X));
+        (was_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_m;
+        if (was_sharded) stats.sharded_merges++;
         X++;
     }
     const size_t merges = run.merges;
@@ -817,6 +872,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             ev_count += run.batch_s * run.tm_count / tm;
             ev_select += run.batch_s * run.tm_select / tm;
             ev_replace += run.batch_s * run.tm_replace / tm;
+            stats.comm_s = run.batch_s * run.tm_comm / tm;
         }
     }
     ev_count += run.ev_count;
@@ -870,6 +926,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                     Q[6] * us / nr, Q[9], Q[8] * us / ns);
         }
     }
+    stats.sharded_s = std::max(0.0, stats.sharded_s - stats.replicate_s);
     stats.total_s = now_s() - t_start;
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
     stats.distinct_pairs = (uint64_t)std::max(h_st->live, 0);
@@ -892,24 +949,26 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // and continue as replicas
     if (dist() && replicate_late && list_mode && pres_vp <= PRES_MAX_VP &&
         (uint64_t)h_st->top_count * list_start * (uint64_t)world < global_live) {
+        const double t_rep = now_s();
         HIP_OK(hipEventRecord(ev[3], stream));
         CHECK(compact());  // this shard's live tokens, contiguous
         CHECK(replicate());
-        CHECK(build_lists());
+        CHECK(build_lists(X0));
         HIP_OK(hipEventRecord(ev[4], stream));
         HIP_OK(hipEventSynchronize(ev[4]));
         float ms;
         HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
         run.ev_replace += ms * 1e-3;
         CHECK(sync_state());
+        stats.replicate_s += now_s() - t_rep;  // (inside this batch's wall, taken out of sharded_s in train)
     }
     // headroom for K merges: ids, occurrence records (counts never grow), tie list; compaction
     CHECK(maybe_grow_tables(X0, K));
     if (hot_stale) CHECK(rebuild_hot());  // a table rebuild renumbered the ids the tie kernels read
     const uint32_t top0 = h_st->top_count;
     if ((uint64_t)(n_slots - n_live) * (lists_on ? compact_den_lists : compact_den) > (uint64_t)n_slots ||
-        (uint64_t)h_st->arena_top + (uint64_t)K * top0 > lists_cap)
-        CHECK(compact_train());
+        arena_used() + (uint64_t)K * top0 > arena_limit())
+        CHECK(compact_train(X0));
     CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
     if (dist()) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
     const uint64_t C = home_slots;
@@ -929,7 +988,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         // else fused into the tie collection + refresh + decide
         if (!fused_select || (i == 0 && !begun)) {
             zbpe_tie_collect<<<64, 256, 0, stream>>>(T, d_st, 0, (uint32_t)(C ? C - 1 : 0), d_tie_list, (uint32_t)tie_list_cap, 1,
-                                                     BeginArgs{X, C, (uint32_t)lists_cap, d_log});
+                                                     BeginArgs{X, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0});
             LAUNCH_OK();
             if (C) {
                 zbpe_home_refresh<<<nsb, REFRESH_THREADS, 0, stream>>>(T, d_st, (uint32_t)C, nb, d_summ, d_sup, 1);
@@ -942,11 +1001,13 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         ScanArgs A{d_tok[cur], slots, 0, 0, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
                    pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 1, dist() ? d_halo : nullptr,
                    lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log, nullptr, (int)sel_prof};
+        set_list_nb(A);
         // a batch that follows one of list scans only launches a smaller grid (fewer idle workgroups
         // to dispatch); a stream scan still completes on it, only slower
         CHECK(launch_scan(A, list_streak ? list_grid : 0));
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 2], stream));
         CHECK(comm_sum(d_delta, 2ull * X + 2));
+        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 3], stream));
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
                       1, dist() ? d_halo : nullptr, 1, (int)sel_prof};
         if (!replace_split) {
@@ -965,7 +1026,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             zbpe_halo_build<<<1, 1, 0, stream>>>(d_bnd_all, rank, world, d_halo, d_st);
             LAUNCH_OK();
         }
-        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 3], stream));
+        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 4], stream));
         if (fused_select) {
             if (hot_stale) CHECK(rebuild_hot());
             // about four hot entries per thread (the list grows by the new ids of the batch), and
@@ -973,7 +1034,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             const uint64_t hot_est = std::min<uint64_t>(T.hot_cap, (uint64_t)h_st->hot_len + (uint64_t)K * 1024 + 4096);
             const uint64_t work = std::max<uint64_t>(hot_est / 4, 2ull * X / 4);
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
-            NextArgs N{BeginArgs{X + 1, C, (uint32_t)lists_cap, d_log}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
+            NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
                        dist() ? world : 1, (int)sel_prof};
             zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, d_delta, X, N);
@@ -981,7 +1042,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         } else {
             CHECK(launch_argmax(X, 1));
         }
-        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 4], stream));
+        if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 5], stream));
     }
     if (merge_timing) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * MAX_BATCH + 1], stream));
     if (dist()) HIP_OK(hipMemcpyAsync(h_bnd, d_bnd_all, world * sizeof(Boundary), hipMemcpyDeviceToHost, stream));
@@ -1021,14 +1082,15 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         stats.replace_pair_calls++;
         if (L.ties > 1) stats.tie_iterations++;
         if (L.mode) stats.list_scans++;
-        float ms_sel = 0, ms_scan = 0, ms_rep = 0, ms_begin = 0;
+        float ms_sel = 0, ms_scan = 0, ms_rep = 0, ms_begin = 0, ms_comm = 0;
         if (merge_timed(X)) {
             const hipEvent_t *E = &bev[BEV_PER_MERGE * i];
             const double w = merge_weight();  // the merges this one stands for
             HIP_OK(hipEventElapsedTime(&ms_begin, E[0], E[1]));
             HIP_OK(hipEventElapsedTime(&ms_scan, E[1], E[2]));
-            HIP_OK(hipEventElapsedTime(&ms_rep, E[2], E[3]));
-            HIP_OK(hipEventElapsedTime(&ms_sel, E[3], E[4]));
+            HIP_OK(hipEventElapsedTime(&ms_comm, E[2], E[3]));
+            HIP_OK(hipEventElapsedTime(&ms_rep, E[3], E[4]));
+            HIP_OK(hipEventElapsedTime(&ms_sel, E[4], E[5]));
             ms_sel += ms_begin;  // argmax + Zig-order tie decision: sortCodePointPairs + [0]
             if (!L.mode) {  // the roofline covers stream scans (a list scan reads no stream)
                 stats.scan_kernel_s += ms_scan * 1e-3;
@@ -1036,7 +1098,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                 stats.scan_timed_alg_bytes += 2ull * L.live;
             }
             // the sampled merges give the shares of the stages; the batch's measured span is split by them
-            run.tm_count += w * ms_scan * 1e-3;
+            run.tm_count += w * (ms_scan + ms_comm) * 1e-3;  // the exchange of the count deltas is counting
+            run.tm_comm += w * ms_comm * 1e-3;
             run.tm_select += w * ms_sel * 1e-3;
             run.tm_replace += w * ms_rep * 1e-3;
         }
@@ -1084,14 +1147,16 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     CHECK(maybe_grow_tables(X, 1));
     const bool self = a == b;
     // records need room in the arena (self pairs treat holes as transparent: no compaction needed)
-    if ((uint64_t)h_st->arena_top + top > lists_cap) CHECK(compact_train());
-    if ((uint64_t)h_st->arena_top + top > lists_cap) return fail(ZBPE_OUT_OF_MEMORY, "occurrence arena full");
+    // (sharded: replicated quantities only, so every rank compacts / grows alike and the ranks' collectives stay in step)
+    if (arena_used() + top > arena_limit()) CHECK(compact_train(X));
+    if (arena_used() + top > arena_limit()) CHECK(grow_arena(arena_used() + top + (16u << 20)));
     // delta layout for this merge: left[0, X) | right[X, 2X) | xx | occurrences
     uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
     // ---- count: scan the stream for (a, b) -----------------------------------------------------
     ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
                pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 0, nullptr, lists_on ? d_lists : nullptr, T.lst_off,
                T.lst_len, list_ratio, 1, nullptr};
+    set_list_nb(A);
     HIP_OK(hipEventRecord(ev[0], stream));
     if (!self) {
         CHECK(launch_scan(A));
@@ -1187,7 +1252,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     const uint64_t gone = h_st->last_holes;  // slots of this shard that became holes
     n_live -= gone;
     (void)gone;
-    if ((uint64_t)(n_slots - n_live) * (lists_on ? compact_den_lists : compact_den) > (uint64_t)n_slots) CHECK(compact_train());
+    if ((uint64_t)(n_slots - n_live) * (lists_on ? compact_den_lists : compact_den) > (uint64_t)n_slots) CHECK(compact_train(X + 1));
     return ZBPE_OK;
 }
 
@@ -1309,7 +1374,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
     if (use_lists) {
         CHECK(ensure(&d_lists, lists_cap, 2 * n + 1024, "occurrence arena"));  // lists <= n, records <= n
         pres_vp = vp;
-        CHECK(build_lists());
+        CHECK(build_lists(256));  // the byte tokens exist at the build; every merge makes a new token >= 256
     } else {
         lists_on = false;
         CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(n / 2 + 1, 1), "occurrence records"));
@@ -1352,6 +1417,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
             }
             ScanArgs A{d_tok[cur], n_slots, 0, 0, d_delta, d_delta + 65536, d_st, d_rec, 0, 0, tail, tail + 1, Halo{},
                        nullptr, vp, 0, nullptr, 0, nullptr, d_lists, T.lst_off, T.lst_len, list_ratio, 0, nullptr};
+            set_list_nb(A);
             hipLaunchKernelGGL(zbpe_encode_scan_batch, dim3(scan_grid(n_slots), E.nb), dim3(SCAN_THREADS), 0, stream, A, E,
                                (const int32_t *)d_enc_cnt, d_enc_ctr, d_rec);
             LAUNCH_OK();
@@ -1366,6 +1432,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
         ScanArgs A{d_tok[cur], n_slots, a, b, d_delta, d_delta + 65536, d_st, recbuf, reccap, 0, tail, tail + 1, Halo{},
                    nullptr, vp, X, nullptr, 0, nullptr, use_lists ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio,
                    use_lists ? 1 : 0, nullptr};
+        set_list_nb(A);
         if (a != b) {
             CHECK(launch_scan(A));
         } else if (use_lists && self_list_ok(a, false)) {

@@ -18,7 +18,7 @@ namespace zbpe {
 constexpr int ARGMAX_MAX_BLOCKS = 1024;
 constexpr size_t DELTA_WORDS = 2 * 65536 + 64;  // left | right | xx | occurrences (+ scratch)
 constexpr uint32_t MAX_BATCH = 256;              // merges per device-resident batch (option "merge_batch")
-constexpr uint32_t BEV_PER_MERGE = 5;            // events of a timed batch merge: start, begun, scanned, replaced, selected
+constexpr uint32_t BEV_PER_MERGE = 6;  // events of a timed batch merge: start, begun, scanned, exchanged, replaced, selected
 constexpr uint32_t PRES_MAX_VP = 32768;          // presence bitset of a block group fits one workgroup LDS (128 KiB)
 
 struct Engine {
@@ -98,9 +98,19 @@ struct Engine {
     // token occurrence lists + this merge's records, in one arena (see kernels.hpp list kernels)
     uint32_t *d_lists = nullptr;
     size_t lists_cap = 0;
+    // sharded: the arena limit every rank decides halts and compactions on (from the smallest shard,
+    // the same on every rank; each rank's lists_cap is at least this) -- with DevState::arena_rep
+    uint64_t arena_cap_rep = 0;
+    uint64_t arena_cap_opt = 0;  // option "arena_cap": arena entries to allocate (tests; 0 = 1.5 n + 16 Mi)
+    uint64_t arena_limit() const { return dist() ? arena_cap_rep : lists_cap; }
+    uint64_t arena_used() const { return dist() ? h_st->arena_rep : h_st->arena_top; }
     uint32_t *d_list_cnt = nullptr, *d_list_total = nullptr;
     size_t list_cnt_cap = 0;
     bool lists_on = false;
+    // build-time neighbours of the list entries (the filtered list walk; option "list_nb")
+    uint16_t *d_succ = nullptr, *d_pred = nullptr;
+    size_t succ_cap = 0, pred_cap = 0;
+    bool list_nb = true, nb_built = false;
     bool list_streak = false;   // the last batch used list scans only
     int list_grid = 0;          // scan grid after such a batch (option "list_grid"; 0 = the full grid)
     int list_mode = 1;          // 0: never build lists, 1: once pair counts are small against the stream
@@ -148,7 +158,7 @@ struct Engine {
         int verbose = 0;
         uint16_t vocab = 0;
         double ev_count = 0, ev_select = 0, ev_replace = 0;  // measured directly (sync path, compactions)
-        double tm_count = 0, tm_select = 0, tm_replace = 0;  // stage times of the timed batch merges
+        double tm_count = 0, tm_select = 0, tm_replace = 0, tm_comm = 0;  // stage times of the timed batch merges
         double batch_s = 0;                                   // device span of the batches
     } run;
     uint64_t hot_target = 1u << 16;  // ids the hot list aims to hold after a rebuild
@@ -192,8 +202,10 @@ struct Engine {
     zbpe_status alloc_stream(size_t n);
     zbpe_status build_presence();
     zbpe_status compact();
-    zbpe_status compact_train();
-    zbpe_status build_lists();
+    zbpe_status compact_train(uint32_t X);
+    zbpe_status grow_arena(uint64_t need);
+    zbpe_status build_lists(uint32_t lists_x);
+    void set_list_nb(ScanArgs &A) const;
     zbpe_status replicate();
     zbpe_status launch_argmax(uint32_t X, int roll);
     int argmax_blocks(uint32_t X) const;

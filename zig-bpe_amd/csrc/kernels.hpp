@@ -366,6 +366,9 @@ struct ScanArgs {
     MergeLog *log;          // batch mode: the scan records its mode in log[X - 256]
     uint32_t *rec_ctr;      // record counter (nullptr: st->rec_count); batched encode: one per merge
     int prof;               // option sel_prof: probe stamps into st->pp_t (batch mode)
+    // the neighbours of every list entry when the lists were built (Engine::build_lists; nullptr:
+    // none): succ[e] / pred[e] = the live token after / before position lists[e] at that time
+    const uint16_t *succ, *pred;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // the device-held parts of the arguments: pair (batch mode), halo (batch mode, multi-GPU), record
@@ -388,7 +391,7 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
     }
     return ScanArgs{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
                     A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
-                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof};
+                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.succ, A0.pred};
 }
 
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
@@ -716,18 +719,30 @@ __device__ inline void scan_lds_flush(ScanLds &S, uint32_t *g_left, uint32_t *g_
 }
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S);
+template <bool PROF = false>
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
-                                                                     uint32_t len, ScanLds &S);
+                                                                     uint32_t len, ScanLds &S, const uint16_t *NB);
+template <bool PROF = false>
+__device__ __attribute__((always_inline)) inline void scan_list_filtered(const ScanArgs A, bool by_b, uint32_t off, uint32_t len,
+                                                                         ScanLds &S);
 // one pair scan with resolved arguments: the list form when the shorter token list is short
 // enough, else the stream form
-template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false>
 __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S) {
     // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
+    const uint32_t lists_x = A.st->lists_x;
     if (A.lists && A.a != A.b && A.st->lists_valid) {
         // lengths and offsets in one round trip
         const uint32_t la = A.lst_len[A.a], lb = A.lst_len[A.b], oa = A.lst_off[A.a], ob = A.lst_off[A.b];
         const bool by_b = lb < la;
         const uint32_t len = by_b ? lb : la;
+        // Both tokens existed when the lists were built: since then a position's successor (its
+        // predecessor) has only ever changed into a token created after the build (a merge at the
+        // successor turns it into the new token; a hole appears only where the position itself is
+        // merged), so every occurrence of (a, b) is an entry of a's list whose successor was b at the
+        // build (of b's list whose predecessor was a). The walk reads that neighbour with the entry
+        // (coalesced) and gathers the stream only where it matches: ~count gathers, not ~len.
+        const uint16_t *NB = A.succ && A.a < lists_x && A.b < lists_x ? (by_b ? A.pred + ob : A.succ + oa) : nullptr;
         if (len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n) {
             if (blockIdx.x == 0 && threadIdx.x == 0) {
                 A.st->scan_mode = 1;
@@ -736,18 +751,21 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
                     A.log[A.X - 256].list_len = len;
                     A.log[A.X - 256].key_live = A.tokcnt ? (uint32_t)A.tokcnt[by_b ? A.b : A.a] : 0u;
                 }
-                if (A.prof) A.st->pp_t[4] = 1;
+                if (PROF) A.st->pp_t[4] = 1;
             }
-            scan_list_body(A, by_b, A.lists + (by_b ? ob : oa), len, S);
+            if (NB) scan_list_filtered<PROF>(A, by_b, by_b ? ob : oa, len, S);
+            else scan_list_body<PROF>(A, by_b, A.lists + (by_b ? ob : oa), len, S, nullptr);
             return;
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
     scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT>(A, S);
 }
-template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false>
-__global__ void __launch_bounds__(SCAN_THREADS, 4) zbpe_scan_pairs_t(ScanArgs A0) {
-    if (A0.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // the last select's end -> this scan's start
+// PROF (option sel_prof): the pipeline probes; a separate instantiation, so the production kernel's
+// code and register allocation are untouched by them
+template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false, bool PROF = false>
+__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
+    if (PROF && blockIdx.x == 0 && threadIdx.x == 0) {  // the last select's end -> this scan's start
         DevState *st = A0.st;
         const unsigned long long now = wall_clock64();
         unsigned long long *P = st->pipe_prof[pp_bucket(A0.X)];
@@ -757,7 +775,7 @@ __global__ void __launch_bounds__(SCAN_THREADS, 4) zbpe_scan_pairs_t(ScanArgs A0
     if (A0.dyn && A0.st->halt) return;
     __shared__ ScanLds S;
     const ScanArgs A = scan_args_resolve(A0);
-    scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT>(A, S);
+    scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF>(A, S);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -841,10 +859,137 @@ __global__ void __launch_bounds__(256) zbpe_encode_apply_batch(uint16_t *tok, in
     st->ticket = 0;
 }
 
+// Filtered list scan (scan_dispatch: both tokens existed at the list build). Each thread reads the
+// build-time neighbours of LIST_EPT consecutive entries (two 16-B loads of the u16 neighbour array,
+// coalesced); only entries whose neighbour was the pair's other token can be occurrences (about the
+// pair's count of them, against the list's length). A wave compacts its matches in registers (a
+// shuffle binary search over the lanes' inclusive match counts) and resolves them 64 at a time with
+// the stream window loaded in one round trip. Few, fat workgroups: the per-wave record reservation
+// and the per-block histogram flush are atomics on shared counters, and their number is what bounds
+// a late merge's scan, not the bytes.
+constexpr int LIST_EPT = 16;
+template <bool PROF>
+__device__ __attribute__((always_inline)) inline void scan_list_filtered(const ScanArgs A, bool by_b, uint32_t off, uint32_t len,
+                                                                         ScanLds &S) {
+    const uint32_t per_block = SCAN_THREADS * LIST_EPT;
+    const uint32_t ab = off & ~7u;                    // 16-B aligned start of the neighbour words
+    const uint32_t span = off + len - ab;             // entries from ab to the list's end
+    if (blockIdx.x > 0 && (uint64_t)blockIdx.x * per_block >= span) return;
+    const uint16_t *NB = by_b ? A.pred : A.succ;
+    const uint32_t partner = by_b ? A.a : A.b, key = by_b ? A.b : A.a;
+    scan_lds_clear(S);
+    if (threadIdx.x == 0) S.any = 0;
+    __syncthreads();
+    if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
+    NeighbourHist H{S.left, S.right, A.left, A.right, S.hleft, S.hright};
+    const uint4 *tv = reinterpret_cast<const uint4 *>(A.tok);
+    const int64_t nvec = (A.n + 7) / 8;
+    const int lane = threadIdx.x & 63;
+    uint32_t xx = 0, any = 0;
+    const uint32_t gstride = gridDim.x * per_block;
+    // block-uniform trip count (every lane of a wave takes part in the shuffles and ballots)
+    for (uint32_t b0 = blockIdx.x * per_block; b0 < span; b0 += gstride) {
+        const uint32_t e0 = ab + b0 + threadIdx.x * LIST_EPT;  // this thread's first entry (absolute)
+        uint32_t mk = 0;
+        if (e0 < off + len) {
+            const uint4 w0 = *reinterpret_cast<const uint4 *>(NB + e0);
+            const uint4 w1 = *reinterpret_cast<const uint4 *>(NB + e0 + 8);
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint32_t t = k < 8 ? tok_at(w0, k) : tok_at(w1, k - 8);
+                const uint32_t e = e0 + k;
+                mk |= (t == partner && e >= off && e < off + len) ? (1u << k) : 0u;
+            }
+        }
+        const uint32_t c = (uint32_t)__popc(mk);
+        const uint32_t incl = wave_incl_scan(c);
+        const uint32_t M = (uint32_t)__shfl((int)incl, 63);
+        for (uint32_t r0 = 0; r0 < M; r0 += 64) {
+            const uint32_t j = r0 + lane;
+            int64_t p = -1;
+            int owner = 0;  // the lane holding match j: the first whose inclusive count exceeds j
+            {
+                int lo = 0, hi = 63;
+                const uint32_t jj = j < M ? j : 0u;
+#pragma unroll
+                for (int s2 = 0; s2 < 6; s2++) {
+                    const int mid = (lo + hi) >> 1;
+                    const uint32_t v = (uint32_t)__shfl((int)incl, mid);
+                    if (v > jj) hi = mid;
+                    else lo = mid + 1;
+                }
+                owner = lo;
+            }
+            const uint32_t o_incl = (uint32_t)__shfl((int)incl, owner), o_c = (uint32_t)__shfl((int)c, owner);
+            const uint32_t o_mk = (uint32_t)__shfl((int)mk, owner);
+            if (j < M) {
+                uint32_t rank = j - (o_incl - o_c), m = o_mk;  // the rank-th set bit of the owner's mask
+                for (uint32_t q = 0; q < rank; q++) m &= m - 1;
+                const uint32_t e = ab + b0 + (uint32_t)owner * LIST_EPT + (uint32_t)__ffs(m) - 1;
+                p = (int64_t)A.lists[e];
+            }
+            // the entry's stream window in one round trip (vector, the word before, the two after)
+            const int64_t vi = p < 0 ? 0 : (p >> 3);
+            const uint4 cv = tv[vi];
+            const uint32_t pw0 = tv[vi > 0 ? vi - 1 : 0].w;
+            const uint2 nv0 = *reinterpret_cast<const uint2 *>(&tv[vi + 1 < nvec ? vi + 1 : vi]);
+            bool hit = false;
+            uint32_t pr = 0;
+            if (p >= 0) {
+                const int k = (int)(p & 7);
+                if (tok_at(cv, k) == key) {
+                    const uint32_t pw = vi > 0 ? pw0 : 0xffffffffu;
+                    const uint32_t nx = vi + 1 < nvec ? nv0.x : 0xffffffffu, ny = vi + 1 < nvec ? nv0.y : 0xffffffffu;
+                    if (!by_b) {
+                        pr = (uint32_t)p;
+                        hit = occ_window(A, H, vi, 1u << k, xx, pw, cv, nx, ny) != 0;
+                    } else {
+                        int jb = k - 1;  // the live token before p inside the vector
+                        while (jb >= 0 && tok_at(cv, jb) == HOLE) jb--;
+                        if (jb >= 0) {
+                            if (tok_at(cv, jb) == A.a && occ_window(A, H, vi, 1u << jb, xx, pw, cv, nx, ny)) {
+                                pr = (uint32_t)(vi * 8 + jb);
+                                hit = true;
+                            }
+                        } else {
+                            hit = resolve_candidate(A, H, p, by_b, nvec, xx, pr);
+                        }
+                    }
+                }
+            }
+            const uint64_t hm = __ballot(hit);
+            if (!hm) continue;
+            any = 1;
+            uint32_t base = 0;
+            if (lane == 0) {
+                base = atomicAdd(A.rec_ctr, (uint32_t)__popcll(hm));
+                atomicAdd(A.occ_out, (uint32_t)__popcll(hm));
+            }
+            base = (uint32_t)__shfl((int)base, 0);
+            if (hit) {
+                const uint32_t jr = base + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));
+                if (jr < A.rec_cap) A.rec[jr] = pr;
+                else atomicOr(&A.st->error, 8u);
+            }
+        }
+    }
+    xx = wave_sum(xx);
+    if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
+    if (lane == 0 && any) S.any = 1;
+    __syncthreads();
+    if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
+    if (S.any) scan_lds_flush(S, A.left, A.right);
+    if (PROF) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(&A.st->pp_t[3], (unsigned long long)wall_clock64());
+    }
+}
+
 // List scan: every entry of the key token's list is a position that held the key when it was
 // listed; entries overwritten since (merged or turned into holes) fail the token check.
+template <bool PROF>
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
-                                                                     uint32_t len, ScanLds &S) {
+                                                                     uint32_t len, ScanLds &S, const uint16_t *NB) {
     // blocks past the list leave before touching LDS (the grid is sized for a stream scan)
     if (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len) return;
     uint32_t *s_left = S.left, *s_right = S.right;
@@ -852,7 +997,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     scan_lds_clear(S);
     if (threadIdx.x == 0) s_any = 0;
     __syncthreads();
-    if (A.prof && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
+    if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{s_left, s_right, A.left, A.right, S.hleft, S.hright};
     const uint16_t *tok = A.tok;
     const uint32_t key = by_b ? A.b : A.a;
@@ -878,14 +1023,20 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     // words too and is resolved. Most entries end after the one vector load.
     constexpr int LU = 3;
     const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
+    const uint32_t partner = by_b ? A.a : A.b;  // the neighbour a filtered entry must have had (NB)
     for (uint32_t i0 = blockIdx.x * SCAN_THREADS + threadIdx.x; i0 - lane < len64; i0 += LU * stride) {
         int64_t ps[LU];
 #pragma unroll
         for (int u = 0; u < LU; u++) {
-            const uint32_t i = i0 + u * stride;
-            const uint32_t e = L[i < len ? i : len - 1];
-            ps[u] = i < len ? (int64_t)e : -1;
+            const uint32_t i = i0 + u * stride, ic = i < len ? i : len - 1;
+            const uint32_t e = L[ic];
+            const bool keep = i < len && (!NB || NB[ic] == partner);
+            ps[u] = keep ? (int64_t)e : -1;
         }
+        bool anyp = false;
+#pragma unroll
+        for (int u = 0; u < LU; u++) anyp |= ps[u] >= 0;
+        if (NB && !__ballot(anyp)) continue;  // no entry of the wave can be an occurrence
         uint4 cvs[LU];
 #pragma unroll
         for (int u = 0; u < LU; u++) cvs[u] = tv[(ps[u] < 0 ? 0 : ps[u]) >> 3];
@@ -985,9 +1136,9 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     if (lane == 0 && any) s_any = 1;
     __syncthreads();
-    if (A.prof && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
+    if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
     if (s_any) scan_lds_flush(S, A.left, A.right);
-    if (A.prof) {
+    if (PROF) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&A.st->pp_t[3], (unsigned long long)wall_clock64());
     }
@@ -1374,7 +1525,7 @@ __global__ void __launch_bounds__(256) zbpe_list_colscan(uint32_t *__restrict__ 
 // one block: list offsets over tokens; tokens with total > max_len get NO_LIST
 __global__ void __launch_bounds__(1024) zbpe_list_offsets(const uint32_t *__restrict__ total, uint32_t vp, uint32_t max_len,
                                                           uint32_t *__restrict__ lst_off, uint32_t *__restrict__ lst_len,
-                                                          DevState *st) {
+                                                          DevState *st, uint32_t lists_x) {
     __shared__ uint32_t s_part[1024];
     const uint32_t per = (vp + 1023) / 1024, t0 = threadIdx.x * per, t1 = min(vp, t0 + per);
     uint32_t sum = 0;
@@ -1402,13 +1553,15 @@ __global__ void __launch_bounds__(1024) zbpe_list_offsets(const uint32_t *__rest
     if (threadIdx.x == 1023) {
         st->arena_top = s_part[1023];
         st->lists_valid = 1;
+        st->lists_x = lists_x;
     }
 }
 __global__ void __launch_bounds__(LIST_THREADS) zbpe_list_scatter(const uint16_t *__restrict__ tok, int64_t n, uint32_t vp,
                                                                   const uint32_t *__restrict__ colpre,
                                                                   const uint32_t *__restrict__ lst_off,
                                                                   const uint32_t *__restrict__ lst_len,
-                                                                  uint32_t *__restrict__ lists) {
+                                                                  uint32_t *__restrict__ lists, uint16_t *__restrict__ succ,
+                                                                  uint16_t *__restrict__ pred) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
     for (uint32_t t = threadIdx.x; t < vp; t += LIST_THREADS)
         cur[t] = lst_len[t] == NO_LIST ? NO_LIST : lst_off[t] + colpre[(uint64_t)blockIdx.x * vp + t];
@@ -1416,10 +1569,19 @@ __global__ void __launch_bounds__(LIST_THREADS) zbpe_list_scatter(const uint16_t
     const int64_t beg = (int64_t)blockIdx.x * LIST_CHUNK, end = min(n, beg + (int64_t)LIST_CHUNK);
     for (int64_t p = beg + 8 * threadIdx.x; p < end; p += 8 * LIST_THREADS) {
         const uint4 v = *reinterpret_cast<const uint4 *>(tok + p);
+        // the neighbours of the compacted stream (the padding past n reads as HOLE: no token)
+        const uint32_t before = p > 0 ? tok[p - 1] : HOLE, after = tok[p + 8];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             const uint32_t t = tok_at(v, k);
-            if (t < vp && p + k < end && cur[t] != NO_LIST) lists[atomicAdd(&cur[t], 1u)] = (uint32_t)(p + k);
+            if (t < vp && p + k < end && cur[t] != NO_LIST) {
+                const uint32_t j = atomicAdd(&cur[t], 1u);
+                lists[j] = (uint32_t)(p + k);
+                if (succ) {
+                    succ[j] = (uint16_t)(k < 7 ? (p + k + 1 < n ? tok_at(v, k + 1) : HOLE) : (p + 8 < n ? after : HOLE));
+                    pred[j] = (uint16_t)(k > 0 ? tok_at(v, k - 1) : before);
+                }
+            }
         }
     }
 }
@@ -2140,7 +2302,7 @@ __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, co
         // below may alias them as far as the compiler knows, which would serialise each load)
         uint32_t *tail = delta + 2 * X;
         const uint32_t rec_count = st->rec_count, total_occ = st->total_occ, holes_made = st->holes_made;
-        const uint32_t arena_top = st->arena_top, gocc = roll ? tail[1] : 0u;
+        const uint32_t arena_top = st->arena_top, arena_rep = st->arena_rep, gocc = roll ? tail[1] : 0u;
         const long long live_tokens = st->live_tokens;
         st->top_count = q.cnt;
         st->tie_count = q.cnt ? q.ties : 0;
@@ -2164,6 +2326,7 @@ __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, co
             st->last_occ = rec_count;
             st->total_occ = total_occ + rec_count;
             st->last_gocc = gocc;
+            st->arena_rep = arena_rep + gocc;
             st->last_holes = holes_made;
             st->live_tokens = live_tokens - holes_made;
             st->tie_len = 0;
@@ -2230,13 +2393,15 @@ __device__ inline uint64_t dev_zig_final_capacity(uint64_t D, bool call_after) {
 struct BeginArgs {
     uint32_t X;
     uint64_t home_cap;  // Zig capacity the home histogram is kept for
-    uint32_t rec_cap;   // arena entries (records go at st->arena_top)
+    uint32_t rec_cap;   // arena entries the halt test allows (records go at st->arena_top)
     MergeLog *log;
+    int rep;            // sharded: test the replicated bound st->arena_rep (every rank halts alike)
 };
 __device__ inline uint32_t merge_begin_eval(const Tables &T, const DevState *st, const BeginArgs &B, bool *tie) {
     *tie = false;
     const int32_t live = st->live;  // the words read, loaded together
-    const uint32_t hot_len = st->hot_len, top_count = st->top_count, arena_top = st->arena_top, tie_count = st->tie_count;
+    const uint32_t hot_len = st->hot_len, top_count = st->top_count, tie_count = st->tie_count;
+    const uint32_t arena_top = B.rep ? st->arena_rep : st->arena_top;
     const uint32_t lastpair = st->lastpair_count, key = st->top_key;
     if (live <= 0) return HALT_DONE;
     if (hot_len > T.hot_cap || top_count == 0) return HALT_SELECT;

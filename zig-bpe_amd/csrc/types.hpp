@@ -61,8 +61,10 @@ struct DevState {
     uint32_t lists_valid;    // 1: token occurrence lists describe the current stream
     long long live_tokens;   // live tokens of this shard (rolled by zbpe_select)
     uint32_t arena_top;      // arena entries in use (lists, then this merge's records)
+    uint32_t arena_rep;      // sum of the merges' global occurrence counts since the arena was emptied: the same on
+                             // every rank and >= any rank's arena_top, so halts decided on it keep ranks in step
     uint32_t scan_mode;      // last pair scan: 0 streamed the token stream, 1 walked an occurrence list
-    uint32_t pad4;
+    uint32_t lists_x;        // tokens < lists_x existed when the lists were built (their entries carry neighbours)
     // option sel_prof: zbpe_select_next phase times (wall_clock64 ticks, summed over merges)
     unsigned long long sel_t0, sel_ta, sel_tr;  // start; latest argmax / refresh block finish
     unsigned long long sel_prof[8];

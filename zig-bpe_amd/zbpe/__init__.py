@@ -132,6 +132,11 @@ class Stats(ctypes.Structure):
         ("list_scans", ctypes.c_uint64),
         ("list_builds", ctypes.c_uint64),
         ("replications", ctypes.c_uint64),
+        ("sharded_s", ctypes.c_double),
+        ("replicate_s", ctypes.c_double),
+        ("replicated_s", ctypes.c_double),
+        ("comm_s", ctypes.c_double),
+        ("sharded_merges", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
