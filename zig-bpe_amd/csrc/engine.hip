@@ -88,8 +88,8 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIP_OK(hipHostMalloc((void **)&h_st, sizeof(DevState), hipHostMallocDefault));
     HIP_OK(hipMalloc(&d_st, sizeof(DevState)));
-    HIP_OK(hipMalloc(&d_delta, DELTA_WORDS * sizeof(uint32_t)));
-    HIP_OK(hipMemset(d_delta, 0, DELTA_WORDS * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_delta, 2 * DELTA_WORDS * sizeof(uint32_t)));  // two: merges alternate (delta_of)
+    HIP_OK(hipMemset(d_delta, 0, 2 * DELTA_WORDS * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&T.tok_cnt, 65536 * sizeof(int32_t)));
     HIP_OK(hipMalloc(&d_log, 65536 * sizeof(MergeLog)));
@@ -433,7 +433,7 @@ int Engine::argmax_blocks(uint32_t X) const {
 zbpe_status Engine::launch_argmax(uint32_t X, int roll) {
     if (hot_stale) CHECK(rebuild_hot());
     const int blocks = argmax_blocks(X);
-    zbpe_select<<<blocks, ARGMAX_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], n_slots, d_delta, X, roll, d_bnd_all,
+    zbpe_select<<<blocks, ARGMAX_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], n_slots, delta_of(X), X, roll, d_bnd_all,
                                                        dist() ? world : 1);
     LAUNCH_OK();
     return ZBPE_OK;
@@ -645,7 +645,7 @@ zbpe_status Engine::bench_train_scan(int reps, int grid, double *avg_us, uint32_
     CHECK(sync_state());
     const uint32_t key = h_st->top_key, a = key & 0xFFFF, b = key >> 16, X = 256 + (uint32_t)run.merges;
     if (a == b || !h_st->top_count || X >= 65536) return fail(ZBPE_INVALID_ARGUMENT, "no scannable pair (self pair or exhausted)");
-    uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
+    uint32_t *left = delta_of(X), *right = left + X, *tail = left + 2 * X;
     ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
                nullptr, pres_vp, X, T.tok_cnt, 0, nullptr, lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1,
                d_log, nullptr, 0};
@@ -795,7 +795,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     if (T.home_dirty) { (void)hipFree(T.home_dirty); T.home_dirty = nullptr; dirty_bits_cap = 0; }
     hot_stale = true;
     halo = halo0;
-    HIP_OK(hipMemsetAsync(d_delta, 0, DELTA_WORDS * 4, stream));
+    HIP_OK(hipMemsetAsync(d_delta, 0, 2 * DELTA_WORDS * 4, stream));
     HIP_OK(hipMemsetAsync(d_hist, 0, 65536 * 4, stream));
     HIP_OK(hipEventRecord(ev[0], stream));
     if (n + (next_byte >= 0 ? 1 : 0) >= 2) {
@@ -983,7 +983,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         const uint32_t X = X0 + i;
         const bool timed = merge_timed(X);
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i], stream));
-        uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
+        uint32_t *left = delta_of(X), *right = left + X, *tail = left + 2 * X;
         // merge start (halt checks, tie_on, ties): done by the previous merge's zbpe_select_next,
         // else fused into the tie collection + refresh + decide
         if (!fused_select || (i == 0 && !begun)) {
@@ -1006,7 +1006,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         // to dispatch); a stream scan still completes on it, only slower
         CHECK(launch_scan(A, list_streak ? list_grid : 0));
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 2], stream));
-        CHECK(comm_sum(d_delta, 2ull * X + 2));
+        CHECK(comm_sum(left, 2ull * X + 2));
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 3], stream));
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
                       1, dist() ? d_halo : nullptr, 1, (int)sel_prof};
@@ -1037,7 +1037,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
                        dist() ? world : 1, (int)sel_prof};
-            zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, d_delta, X, N);
+            zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, left, X, N);
             LAUNCH_OK();
         } else {
             CHECK(launch_argmax(X, 1));
@@ -1151,7 +1151,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     if (arena_used() + top > arena_limit()) CHECK(compact_train(X));
     if (arena_used() + top > arena_limit()) CHECK(grow_arena(arena_used() + top + (16u << 20)));
     // delta layout for this merge: left[0, X) | right[X, 2X) | xx | occurrences
-    uint32_t *left = d_delta, *right = d_delta + X, *tail = d_delta + 2 * X;
+    uint32_t *left = delta_of(X), *right = left + X, *tail = left + 2 * X;
     // ---- count: scan the stream for (a, b) -----------------------------------------------------
     ScanArgs A{d_tok[cur], n_slots, a, b, left, right, d_st, d_lists, (uint32_t)lists_cap, 1, tail, tail + 1, halo,
                pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 0, nullptr, lists_on ? d_lists : nullptr, T.lst_off,
@@ -1188,7 +1188,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     }
     HIP_OK(hipEventRecord(ev[1], stream));
     // ---- exchange: sum the count deltas of all shards (one RCCL all-reduce per merge) ---------------
-    CHECK(comm_sum(d_delta, 2ull * X + 2));
+    CHECK(comm_sum(left, 2ull * X + 2));
     // ---- replace: apply + count update ---------------------------------------------------------
     {
         const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top / 256 + 1);

@@ -40,7 +40,10 @@ struct Engine {
 
     // pair table and per-merge scratch
     Tables T{};
+    // per-merge neighbour deltas, two buffers of DELTA_WORDS: merge X uses delta_of(X) (a select may then
+    // scan merge X + 1 into the other buffer while its own merge's words are still being cleared)
     uint32_t *d_delta = nullptr, *d_hist = nullptr;
+    uint32_t *delta_of(uint32_t X) const { return d_delta + (size_t)(X & 1) * DELTA_WORDS; }
 
     // multi-GPU: this rank's shard and its neighbours' boundary tokens
     int rank = 0, world = 1;

@@ -719,12 +719,13 @@ __device__ inline void scan_lds_flush(ScanLds &S, uint32_t *g_left, uint32_t *g_
 }
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S);
-template <bool PROF = false>
+template <bool PROF = false, int NT = SCAN_THREADS>
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
-                                                                     uint32_t len, ScanLds &S, const uint16_t *NB);
-template <bool PROF = false>
+                                                                     uint32_t len, ScanLds &S, const uint16_t *NB,
+                                                                     uint32_t vb, uint32_t vg);
+template <bool PROF = false, int NT = SCAN_THREADS>
 __device__ __attribute__((always_inline)) inline void scan_list_filtered(const ScanArgs A, bool by_b, uint32_t off, uint32_t len,
-                                                                         ScanLds &S);
+                                                                         ScanLds &S, uint32_t vb, uint32_t vg);
 // one pair scan with resolved arguments: the list form when the shorter token list is short
 // enough, else the stream form
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false>
@@ -753,8 +754,8 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
                 }
                 if (PROF) A.st->pp_t[4] = 1;
             }
-            if (NB) scan_list_filtered<PROF>(A, by_b, by_b ? ob : oa, len, S);
-            else scan_list_body<PROF>(A, by_b, A.lists + (by_b ? ob : oa), len, S, nullptr);
+            if (NB) scan_list_filtered<PROF>(A, by_b, by_b ? ob : oa, len, S, blockIdx.x, gridDim.x);
+            else scan_list_body<PROF>(A, by_b, A.lists + (by_b ? ob : oa), len, S, nullptr, blockIdx.x, gridDim.x);
             return;
         }
     }
@@ -867,14 +868,20 @@ __global__ void __launch_bounds__(256) zbpe_encode_apply_batch(uint16_t *tok, in
 // the stream window loaded in one round trip. Few, fat workgroups: the per-wave record reservation
 // and the per-block histogram flush are atomics on shared counters, and their number is what bounds
 // a late merge's scan, not the bytes.
-constexpr int LIST_EPT = 16;
-template <bool PROF>
+constexpr int LIST_EPT = 16;  // the most entries a thread filters
+// (vb, vg: this workgroup's index among the vg workgroups that walk the list; NT threads each)
+template <bool PROF, int NT>
 __device__ __attribute__((always_inline)) inline void scan_list_filtered(const ScanArgs A, bool by_b, uint32_t off, uint32_t len,
-                                                                         ScanLds &S) {
-    const uint32_t per_block = SCAN_THREADS * LIST_EPT;
+                                                                         ScanLds &S, uint32_t vb, uint32_t vg) {
+    // entries per thread: about one match per two lanes (a wave resolves its matches 64 at a time, one
+    // latency chain per round): the list's length over the pair's count (training; encode: 4)
+    const uint32_t cnt = A.count_deltas ? A.st->top_count : 0u;
+    const uint32_t ratio = cnt ? len / cnt : 8u;
+    const uint32_t ept = ratio >= 32 ? 16u : ratio >= 16 ? 8u : ratio >= 8 ? 4u : ratio >= 4 ? 2u : 1u;
+    const uint32_t per_block = NT * ept;
     const uint32_t ab = off & ~7u;                    // 16-B aligned start of the neighbour words
     const uint32_t span = off + len - ab;             // entries from ab to the list's end
-    if (blockIdx.x > 0 && (uint64_t)blockIdx.x * per_block >= span) return;
+    if (vb > 0 && (uint64_t)vb * per_block >= span) return;
     const uint16_t *NB = by_b ? A.pred : A.succ;
     const uint32_t partner = by_b ? A.a : A.b, key = by_b ? A.b : A.a;
     scan_lds_clear(S);
@@ -886,19 +893,30 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     const int64_t nvec = (A.n + 7) / 8;
     const int lane = threadIdx.x & 63;
     uint32_t xx = 0, any = 0;
-    const uint32_t gstride = gridDim.x * per_block;
+    const uint32_t gstride = vg * per_block;
     // block-uniform trip count (every lane of a wave takes part in the shuffles and ballots)
-    for (uint32_t b0 = blockIdx.x * per_block; b0 < span; b0 += gstride) {
-        const uint32_t e0 = ab + b0 + threadIdx.x * LIST_EPT;  // this thread's first entry (absolute)
+    for (uint32_t b0 = vb * per_block; b0 < span; b0 += gstride) {
+        const uint32_t e0 = ab + b0 + threadIdx.x * ept;  // this thread's first entry (absolute)
         uint32_t mk = 0;
         if (e0 < off + len) {
-            const uint4 w0 = *reinterpret_cast<const uint4 *>(NB + e0);
-            const uint4 w1 = *reinterpret_cast<const uint4 *>(NB + e0 + 8);
+            if (ept >= 8) {  // 16-B aligned (ab and ept are multiples of 8)
+                const uint4 w0 = *reinterpret_cast<const uint4 *>(NB + e0);
+                const uint4 w1 = ept == 16 ? *reinterpret_cast<const uint4 *>(NB + e0 + 8) : make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const uint32_t t = k < 8 ? tok_at(w0, k) : tok_at(w1, k - 8);
-                const uint32_t e = e0 + k;
-                mk |= (t == partner && e >= off && e < off + len) ? (1u << k) : 0u;
+                for (int k = 0; k < 16; k++) {
+                    const uint32_t t = k < 8 ? tok_at(w0, k) : tok_at(w1, k - 8);
+                    const uint32_t e = e0 + k;
+                    mk |= (t == partner && e >= off && e < off + len && (uint32_t)k < ept) ? (1u << k) : 0u;
+                }
+            } else {
+                uint32_t t[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) t[k] = (uint32_t)k < ept ? NB[e0 + k] : HOLE;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t e = e0 + k;
+                    mk |= (t[k] == partner && e >= off && e < off + len) ? (1u << k) : 0u;
+                }
             }
         }
         const uint32_t c = (uint32_t)__popc(mk);
@@ -925,7 +943,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
             if (j < M) {
                 uint32_t rank = j - (o_incl - o_c), m = o_mk;  // the rank-th set bit of the owner's mask
                 for (uint32_t q = 0; q < rank; q++) m &= m - 1;
-                const uint32_t e = ab + b0 + (uint32_t)owner * LIST_EPT + (uint32_t)__ffs(m) - 1;
+                const uint32_t e = ab + b0 + ((threadIdx.x & ~63u) + (uint32_t)owner) * ept + (uint32_t)__ffs(m) - 1;
                 p = (int64_t)A.lists[e];
             }
             // the entry's stream window in one round trip (vector, the word before, the two after)
@@ -987,11 +1005,12 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
 
 // List scan: every entry of the key token's list is a position that held the key when it was
 // listed; entries overwritten since (merged or turned into holes) fail the token check.
-template <bool PROF>
+template <bool PROF, int NT>
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
-                                                                     uint32_t len, ScanLds &S, const uint16_t *NB) {
+                                                                     uint32_t len, ScanLds &S, const uint16_t *NB,
+                                                                     uint32_t vb, uint32_t vg) {
     // blocks past the list leave before touching LDS (the grid is sized for a stream scan)
-    if (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len) return;
+    if (vb > 0 && (uint64_t)vb * NT >= len) return;
     uint32_t *s_left = S.left, *s_right = S.right;
     uint32_t &s_any = S.any;
     scan_lds_clear(S);
@@ -1003,7 +1022,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     const uint32_t key = by_b ? A.b : A.a;
     uint32_t xx = 0, any = 0;
     const int lane = threadIdx.x & 63;
-    if (by_b && blockIdx.x == 0 && threadIdx.x == 0 && A.halo.nright > 0 && halo_right(A.halo, 0) == A.b) {
+    if (by_b && vb == 0 && threadIdx.x == 0 && A.halo.nright > 0 && halo_right(A.halo, 0) == A.b) {
         // the occurrence leaving the shard: its b is the next shard's, in no list here
         const int64_t p = prev_live(tok, A.n);
         if (p >= 0 && tok[p] == A.a && occ_slow(A, H, p, xx)) {
@@ -1014,7 +1033,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
             any = 1;
         }
     }
-    const uint32_t stride = gridDim.x * SCAN_THREADS;
+    const uint32_t stride = vg * NT;
     const int64_t nvec = (A.n + 7) / 8;
     const uint32_t len64 = (len + 63) & ~63u;  // wave-uniform trip count (wave_append)
     // LU entries per thread in flight: their list words, then their 16-B vectors (one request each,
@@ -1024,7 +1043,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     constexpr int LU = 3;
     const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
     const uint32_t partner = by_b ? A.a : A.b;  // the neighbour a filtered entry must have had (NB)
-    for (uint32_t i0 = blockIdx.x * SCAN_THREADS + threadIdx.x; i0 - lane < len64; i0 += LU * stride) {
+    for (uint32_t i0 = vb * NT + threadIdx.x; i0 - lane < len64; i0 += LU * stride) {
         int64_t ps[LU];
 #pragma unroll
         for (int u = 0; u < LU; u++) {
