@@ -42,8 +42,11 @@ def per_dispatch(d, counter):
 
 
 def summarise(values, log, live, scale):
-    if len(values) != len(log):
+    # bench.py trains several times (warm-up, timed steps, the probe train); the scan log is the probe
+    # train's, the last train of the command: its launches are the last len(log) dispatches
+    if len(values) < len(log):
         sys.exit(f"{len(values)} profiled scan dispatches but {len(log)} scan-log entries: cannot match")
+    values = values[len(values) - len(log):]
     groups = {"stream": [], "stream_timed": [], "list": [], "noop": []}
     for v, e in zip(values, log):
         if e < 0:
@@ -76,7 +79,7 @@ def main():
     p.add_argument("--write", default="")
     p.add_argument("--write-log", default="")
     a = p.parse_args()
-    res = {"kernel": "zbpe_scan_pairs_t", "source": "rocprofv3 --pmc, one pass per counter, bench.py --steps 1 --warmup 0",
+    res = {"kernel": "zbpe_scan_pairs_t", "source": "rocprofv3 --pmc, one pass per counter, bench.py --steps 1 --warmup 0 --no-cpu (the probe train: the last train of the command)",
            "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read undercount); WRITE_SIZE KiB x 1024"}
     fl = json.load(open(a.fetch_log))
     res["read"] = summarise(per_dispatch(a.fetch, "FETCH_SIZE"), fl["scan_log"], fl["live"], 2 * 1024)
