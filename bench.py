@@ -162,6 +162,26 @@ def probe_roofline(eng, vocab: int, scan_log_out: str):
     }
 
 
+def make_engine(zbpe, share_gpu: bool, rank: int, world: int, local_rank: int, dist):
+    """One engine per rank (one process per GPU). N>1: rank 0's RCCL unique id is broadcast over the
+    gloo group and every rank joins the RCCL communicator on its own GPU; if RCCL cannot initialise,
+    the exchange falls back to host (gloo) collectives and the GPU compute path stays. share_gpu: all
+    ranks on cuda:0 with host collectives (rehearses N>1 on one GPU). -> (engine, comm backend name)."""
+    if world == 1:
+        return zbpe.Engine(0), "none"
+    if share_gpu:
+        return (zbpe.Engine(0, rank=rank, world=world, collective=zbpe.torch_collective(rank, world)),
+                "gloo (host collectives, ranks share cuda:0)")
+    uid = [zbpe.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    try:
+        return zbpe.Engine(local_rank, rank=rank, world=world, unique_id=uid[0]), "rccl"
+    except zbpe.ZbpeError as e:  # keep the GPU compute path; move only the exchange to gloo
+        sys.stderr.write(f"rank {rank}: RCCL init failed ({e}); using host (gloo) collectives\n")
+        return (zbpe.Engine(local_rank, rank=rank, world=world, collective=zbpe.torch_collective(rank, world)),
+                "gloo (host collectives; RCCL init failed)")
+
+
 def main():
     args = parse()
     import numpy as np
@@ -173,26 +193,11 @@ def main():
     if args.gpus != world:
         world = args.gpus if world == 1 and args.gpus == 1 else world
     dist = None
-    comm_backend = "none"
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
         dist.init_process_group("gloo", init_method="env://")
-        if args.share_gpu:
-            eng = zbpe.Engine(0, rank=rank, world=world, collective=zbpe.torch_collective(rank, world))
-            comm_backend = "gloo (host collectives, ranks share cuda:0)"
-        else:
-            uid = [zbpe.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            try:
-                eng = zbpe.Engine(local_rank, rank=rank, world=world, unique_id=uid[0])
-                comm_backend = "rccl"
-            except zbpe.ZbpeError as e:  # keep the GPU compute path; move only the exchange to gloo
-                sys.stderr.write(f"rank {rank}: RCCL init failed ({e}); using host (gloo) collectives\n")
-                eng = zbpe.Engine(local_rank, rank=rank, world=world, collective=zbpe.torch_collective(rank, world))
-                comm_backend = "gloo (host collectives; RCCL init failed)"
-    else:
-        eng = zbpe.Engine(0)
+    eng, comm_backend = make_engine(zbpe, args.share_gpu, rank, world, local_rank, dist)
 
     t0 = time.time()
     text = zbpe.synth_corpus(args.kind, args.seed, args.n_bytes, threads=16)

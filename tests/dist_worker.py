@@ -82,3 +82,58 @@ def run(target, world, *args, timeout=600):
         if item[1] == "ERROR":
             raise RuntimeError(f"rank {r} failed:\n{item[2]}")
     return out
+
+
+def big_worker(rank, world, port, q, case):
+    """GPU: a corpus past 2^32 bytes sharded over `world` ranks on cuda:0 (gloo collectives); saves this
+    rank's token stream before the last merge to case["dir"], then trains case["vocab"] - 256 merges."""
+    try:
+        import numpy as np
+        import zbpe
+
+        dist = _init(rank, world, port)
+        text = zbpe.synth_corpus(case["kind"], case["seed"], case["n"], threads=8)
+        e = zbpe.Engine(0, rank=rank, world=world, collective=zbpe.torch_collective(rank, world))
+        e.upload(text)
+        del text
+        e.train_resident(case["vocab"] - 1)  # the stream before the last merge, for the oracle's iteration
+        np.save(os.path.join(case["dir"], f"tok{rank}.npy"), e.tokens())
+        m, c, st = e.train_resident(case["vocab"])
+        q.put((rank, m.tolist(), c.tolist(), st.as_dict()))
+        e.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "ERROR", traceback.format_exc()))
+
+
+def bench_setup_worker(rank, world, port, q, case):
+    """CPU: bench.py's N>1 engine set-up (make_engine) over a real gloo group with a stand-in zbpe
+    module: the unique id rank 0 makes reaches every rank, each rank gets its GPU and rank; an RCCL
+    init failure falls back to host collectives."""
+    try:
+        import types
+
+        sys.path.insert(0, ROOT)
+        import bench
+
+        dist = _init(rank, world, port)
+        made = []
+
+        class ZbpeError(Exception):
+            pass
+
+        class Engine:
+            def __init__(self, device=0, rank=0, world=1, unique_id=None, collective=None):
+                if unique_id is not None and case.get("rccl_fails"):
+                    raise ZbpeError("ncclCommInitRank failed")
+                made.append(dict(device=device, rank=rank, world=world, unique_id=unique_id,
+                                 collective=collective is not None))
+
+        fake = types.SimpleNamespace(Engine=Engine, ZbpeError=ZbpeError, comm_unique_id=lambda: b"uid-of-rank-0" + bytes(115),
+                                     torch_collective=lambda r, w: ("collective", r, w))
+        eng, backend = bench.make_engine(fake, case.get("share_gpu", False), rank, world, rank, dist)
+        q.put((rank, made, backend))
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "ERROR", traceback.format_exc()))

@@ -6,7 +6,7 @@ import pytest
 
 import oracle as O
 import zbpe
-from dist_worker import collective_worker, run, train_worker
+from dist_worker import bench_setup_worker, big_worker, collective_worker, run, train_worker
 
 
 def test_host_collective_gloo_world2():
@@ -16,6 +16,23 @@ def test_host_collective_gloo_world2():
         assert a == [3, 10, (0xFFFFFFFF + 0xFFFFFFFE) & 0xFFFFFFFF]
         assert m == [5, 6, 123]
         assert g == [0, 1, 2, 200, 1, 2, 3, 200]
+
+
+@pytest.mark.parametrize("case", [{}, {"share_gpu": True}, {"rccl_fails": True}], ids=["rccl", "share_gpu", "rccl_fails"])
+def test_bench_multi_rank_setup_gloo_world2(case):
+    """bench.py --gpus 2 engine set-up over gloo (CPU): rank 0's RCCL unique id reaches rank 1, each rank
+    opens its own device with its rank; --share-gpu and an RCCL failure use host collectives."""
+    out = run(bench_setup_worker, 2, case)
+    for r in (0, 1):
+        _, made, backend = out[r]
+        assert len(made) == 1 and made[0]["rank"] == r and made[0]["world"] == 2
+        if case.get("share_gpu"):
+            assert backend.startswith("gloo") and made[0]["collective"] and made[0]["device"] == 0
+        elif case.get("rccl_fails"):
+            assert backend.startswith("gloo") and made[0]["collective"] and made[0]["device"] == r
+        else:
+            assert backend == "rccl" and made[0]["device"] == r
+            assert made[0]["unique_id"].startswith(b"uid-of-rank-0")
 
 
 CASES = [
@@ -66,3 +83,22 @@ def test_sharded_exact_tie_path():
     out = run(train_worker, 2, case)
     assert out[0][1] == ref.merges.tolist()
     assert out[0][3]["tie_fallbacks"] == out[0][3]["tie_iterations"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_sharded_corpus_over_4GiB(tmp_path):
+    """A 4.5 GiB corpus (more than 2^32 bytes) on 2 ranks: positions are shard-local u32, global order is
+    (rank, local position), cross-rank sums are exact. Merge 1 must be the oracle's first iteration on the
+    whole byte stream, merge 2 the oracle's iteration on the two shards' streams after merge 1."""
+    case = dict(kind="words_utf8", seed=0x5EED0006, n=(9 << 29), vocab=258, dir=str(tmp_path))
+    out = run(big_worker, 2, case, timeout=800)
+    m, c = out[0][1], out[0][2]
+    assert out[1][1] == m and out[1][2] == c and len(m) == 2
+    text = zbpe.synth_corpus(case["kind"], case["seed"], case["n"], threads=8)
+    r0 = O.step(np.frombuffer(text, np.uint8).astype(np.uint16))
+    del text
+    assert (r0.pair, r0.count) == ((m[0][0], m[0][1]), c[0])
+    t = np.concatenate([np.load(tmp_path / "tok0.npy"), np.load(tmp_path / "tok1.npy")])  # after merge 1
+    r1 = O.step(t)
+    assert (r1.pair, r1.count) == ((m[1][0], m[1][1]), c[1])

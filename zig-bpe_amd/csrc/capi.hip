@@ -222,7 +222,7 @@ zbpe_status zbpe_zig_order_winner(const uint32_t *first_pos, const uint32_t *key
     if ((!first_pos || !keys || !counts) && n) return ZBPE_INVALID_ARGUMENT;
     if (!winner) return ZBPE_INVALID_ARGUMENT;
     std::vector<zbpe::ZigOrderInput> in(n);
-    for (size_t i = 0; i < n; i++) in[i] = zbpe::ZigOrderInput{first_pos[i], keys[i], counts[i]};
+    for (size_t i = 0; i < n; i++) in[i] = zbpe::ZigOrderInput{(uint64_t)first_pos[i], keys[i], counts[i]};
     return zbpe::zig_order_winner(std::move(in), top, call_after_last_insert != 0, winner) ? ZBPE_OK : ZBPE_INTERNAL;
 }
 

@@ -139,14 +139,17 @@ zbpe_status Engine::ensure(T_ **p, size_t &cap, size_t need, const char *what) {
 zbpe_status Engine::upload(const uint8_t *text, size_t n, bool shard) {
     const size_t s = shard ? (size_t)((unsigned __int128)n * rank / world) : 0;
     const size_t e = shard ? (size_t)((unsigned __int128)n * (rank + 1) / world) : n;
-    if (n >= (size_t)0xFFFFFFF0u) return fail(ZBPE_INVALID_ARGUMENT, "corpus of %zu bytes exceeds 2^32 tokens", n);
+    // positions are u32 within a shard (the occurrence arena, records, tiles); the corpus may exceed
+    // 2^32 bytes when it is sharded over enough GPUs
+    if (e - s >= (size_t)0xFFFFFFF0u)
+        return fail(ZBPE_INVALID_ARGUMENT, "corpus shard of %zu bytes exceeds 2^32 tokens (shard it over more GPUs)", e - s);
     HIP_OK(hipSetDevice(device));
     CHECK(ensure(&d_text, text_cap, round_up(e - s + 64, 64), "corpus"));
     if (e > s) HIP_OK(hipMemcpyAsync(d_text, text + s, e - s, hipMemcpyHostToDevice, stream));
     HIP_OK(hipStreamSynchronize(stream));
     n_text = e - s;
     n_total = n;
-    shard_offset = (uint32_t)s;
+    shard_offset = (uint64_t)s;
     next_byte = e < n && shard ? (int)text[e] : -1;
     Halo H = halo_empty();
     if (shard) {
@@ -176,8 +179,10 @@ zbpe_status Engine::init_dist(int r, int w, std::unique_ptr<Comm> c) {
 zbpe_status Engine::sync_state() {
     HIP_OK(hipMemcpyAsync(h_st, d_st, sizeof(DevState), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
+    if (h_st->error & 512u)
+        return fail(ZBPE_INVALID_ARGUMENT, "a byte pair occurs 2^32 times or more in the corpus: pair counts are u32 on the device");
     if (h_st->error)
-        return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow, 16 home count range, 32 dirty list overflow)",
+        return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow, 16 home count range, 32 dirty list overflow, 64 occurrences != count, 128 tie collection)",
                     h_st->error);
     return ZBPE_OK;
 }
@@ -542,7 +547,7 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     HIP_OK(hipMemsetAsync(&d_st->gather_len, 0, 4, stream));
     {
         ScanArgs A{d_tok[cur], n_slots, 0, 0, nullptr, nullptr, d_st, nullptr, 0, 0, nullptr, nullptr, halo};
-        zbpe_first_occ<<<2048, 256, 0, stream>>>(A, shard_offset, T, d_first, d_st);
+        zbpe_first_occ<<<2048, 256, 0, stream>>>(A, T, d_first, d_st);  // shard-local positions
         LAUNCH_OK();
     }
     zbpe_gather_live<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_first, d_st, d_gather, (uint32_t)gather_cap);
@@ -553,21 +558,31 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     std::vector<LiveRec> recs(g);
     HIP_OK(hipMemcpyAsync(recs.data(), d_gather, (size_t)g * sizeof(LiveRec), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
+    std::vector<uint64_t> order(g);
+    for (uint32_t i = 0; i < g; i++) order[i] = recs[i].first_pos;
     if (dist()) {
-        // every rank holds the same live keys: in key order the local first positions line up, so one
-        // all-reduce(min) gives the global first occurrence of each pair
+        // every rank holds the same live keys: in key order the ranks' entries line up. The global first
+        // occurrence of a pair is in the lowest rank holding one (shards are contiguous, in rank order),
+        // at that rank's local position: one all-reduce(min) of the holding rank, one of the position
+        // offered by that rank only -- u32 collectives, whatever the corpus size
         std::sort(recs.begin(), recs.end(), [](const LiveRec &x, const LiveRec &y) { return x.key < y.key; });
-        std::vector<uint32_t> pos(g);
-        for (uint32_t i = 0; i < g; i++) pos[i] = recs[i].first_pos;
+        std::vector<uint32_t> w(g);
+        for (uint32_t i = 0; i < g; i++) w[i] = recs[i].first_pos != 0xFFFFFFFFu ? (uint32_t)rank : 0xFFFFFFFFu;
         CHECK(ensure(&d_first, first_cap, std::max<size_t>(g, nid), "first occurrences"));
-        HIP_OK(hipMemcpyAsync(d_first, pos.data(), (size_t)g * 4, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipMemcpyAsync(d_first, w.data(), (size_t)g * 4, hipMemcpyHostToDevice, stream));
         if (!comm->allreduce_u32(d_first, g, COMM_MIN_U32, stream)) return fail(ZBPE_COMM_ERROR, "all-reduce(min) failed");
-        HIP_OK(hipMemcpyAsync(pos.data(), d_first, (size_t)g * 4, hipMemcpyDeviceToHost, stream));
+        std::vector<uint32_t> lowest(g);
+        HIP_OK(hipMemcpyAsync(lowest.data(), d_first, (size_t)g * 4, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
-        for (uint32_t i = 0; i < g; i++) recs[i].first_pos = pos[i];
+        for (uint32_t i = 0; i < g; i++) w[i] = lowest[i] == (uint32_t)rank ? recs[i].first_pos : 0xFFFFFFFFu;
+        HIP_OK(hipMemcpyAsync(d_first, w.data(), (size_t)g * 4, hipMemcpyHostToDevice, stream));
+        if (!comm->allreduce_u32(d_first, g, COMM_MIN_U32, stream)) return fail(ZBPE_COMM_ERROR, "all-reduce(min) failed");
+        HIP_OK(hipMemcpyAsync(w.data(), d_first, (size_t)g * 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        for (uint32_t i = 0; i < g; i++) order[i] = ((uint64_t)lowest[i] << 32) | w[i];
     }
     std::vector<ZigOrderInput> in(g);
-    for (uint32_t i = 0; i < g; i++) in[i] = ZigOrderInput{recs[i].first_pos, recs[i].key, recs[i].count};
+    for (uint32_t i = 0; i < g; i++) in[i] = ZigOrderInput{order[i], recs[i].key, recs[i].count};
     if (!zig_order_winner(std::move(in), top, call_after, winner))
         return fail(ZBPE_INTERNAL, "exact tie emulation found no pair with count %u", top);
     if (h_st->tie_verdict == 0 && *winner != h_st->tie_winner)
@@ -805,7 +820,15 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             LAUNCH_OK();
         }
     }
-    CHECK(comm_sum(d_hist, 65536));  // every rank builds the same table from the summed histogram
+    if (dist()) {  // every rank builds the same table from the summed histogram (16-bit limbs: exact)
+        uint32_t *limbs = d_delta;  // scratch: the merge loop clears it below
+        zbpe_hist_split<<<256, 256, 0, stream>>>(d_hist, limbs);
+        LAUNCH_OK();
+        CHECK(comm_sum(limbs, 2 * 65536));
+        zbpe_hist_join<<<256, 256, 0, stream>>>(limbs, d_hist, d_st);
+        LAUNCH_OK();
+        HIP_OK(hipMemsetAsync(d_delta, 0, 2 * 65536 * 4, stream));
+    }
     if (world > 1) {  // boundary tokens of every shard (the first select needs the stream's last pair)
         zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, n_live, d_bnd_mine, nullptr);
         LAUNCH_OK();
@@ -948,7 +971,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // occurrence lists, on replicated quantities so every rank decides alike), gather the stream
     // and continue as replicas
     if (dist() && replicate_late && list_mode && pres_vp <= PRES_MAX_VP &&
-        (uint64_t)h_st->top_count * list_start * (uint64_t)world < global_live) {
+        (uint64_t)h_st->top_count * list_start * (uint64_t)world < global_live &&
+        global_live + 64ull * world + (64u << 20) < 0xF0000000ull) {  // the gathered stream must fit u32 positions
         const double t_rep = now_s();
         HIP_OK(hipEventRecord(ev[3], stream));
         CHECK(compact());  // this shard's live tokens, contiguous

@@ -59,7 +59,7 @@ struct Engine {
     uint32_t *d_sizes = nullptr;     // [2 * world + 2] live-token counts of the shards
     size_t sizes_cap = 0;
     bool dist() const { return world > 1 && !replicated; }
-    uint32_t shard_offset = 0;  // global position of the shard's first byte
+    uint64_t shard_offset = 0;  // global position of the shard's first byte
     int next_byte = -1;         // first byte of the next shard (-1: none)
     Halo halo0{}, halo{};
     Boundary *d_bnd_mine = nullptr, *d_bnd_all = nullptr, *h_bnd = nullptr;

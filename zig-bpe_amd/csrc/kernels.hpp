@@ -195,6 +195,20 @@ __global__ void __launch_bounds__(HIST_THREADS) zbpe_count_byte_pairs(const uint
 
 __device__ inline uint32_t wave_sum(uint32_t x);
 // hist[first*256+second] -> pair table entries
+// Multi-GPU: the byte-pair histogram is summed over the ranks in 16-bit limbs (u32 collectives cannot
+// overflow for <= 2^16 ranks), and every global count must stay below 2^32: the device counts are u32,
+// and no count ever exceeds the largest initial one (a new pair's count is at most the merged pair's).
+__global__ void __launch_bounds__(256) zbpe_hist_split(const uint32_t *__restrict__ hist, uint32_t *__restrict__ limbs) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < 65536) { limbs[i] = hist[i] & 0xFFFFu; limbs[65536 + i] = hist[i] >> 16; }
+}
+__global__ void __launch_bounds__(256) zbpe_hist_join(const uint32_t *__restrict__ limbs, uint32_t *__restrict__ hist, DevState *st) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= 65536) return;
+    const uint64_t c = (uint64_t)limbs[i] + ((uint64_t)limbs[65536 + i] << 16);
+    if (c > 0xFFFFFFFFull) atomicOr(&st->error, 512u);
+    hist[i] = (uint32_t)c;
+}
 __global__ void zbpe_hist_to_table(const uint32_t *__restrict__ hist, Tables T, DevState *st) {
     // launched as <<<256, 256>>>: block = first byte
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
@@ -3199,7 +3213,8 @@ __global__ void __launch_bounds__(256) zbpe_home_build(Tables T, DevState *st) {
 }
 
 // exact fallback: first occurrence position of every live pair in the current stream
-__global__ void __launch_bounds__(256) zbpe_first_occ(ScanArgs A, uint32_t offset, Tables T, uint32_t *first, DevState *st) {
+// first-occurrence position (shard-local) of every live pair: the exact tie fallback's insertion order
+__global__ void __launch_bounds__(256) zbpe_first_occ(ScanArgs A, Tables T, uint32_t *first, DevState *st) {
     for (int64_t p = blockIdx.x * 256 + threadIdx.x; p < A.n; p += (int64_t)gridDim.x * 256) {
         const uint16_t x = A.tok[p];
         if (x == HOLE) continue;
@@ -3207,7 +3222,7 @@ __global__ void __launch_bounds__(256) zbpe_first_occ(ScanArgs A, uint32_t offse
         if (q == NONE_POS) continue;
         const uint32_t id = ht_find(T, pair_key(x, tok_h(A, q)));
         if (id == NO_ID) { atomicOr(&st->error, 4u); continue; }
-        atomicMin(&first[id], offset + (uint32_t)p);
+        atomicMin(&first[id], (uint32_t)p);
     }
 }
 __global__ void __launch_bounds__(256) zbpe_gather_live(Tables T, const uint32_t *__restrict__ first, DevState *st,

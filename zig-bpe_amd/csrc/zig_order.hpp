@@ -40,7 +40,8 @@ inline uint64_t zig_final_capacity(uint64_t D, bool call_after_last_insert) {
 }
 
 struct ZigOrderInput {
-    uint32_t first_pos, key, count;
+    uint64_t first_pos;  // first-occurrence order key (multi-GPU: shard index << 32 | shard-local position)
+    uint32_t key, count;
 };
 
 // Returns the key of the first slot (ascending) holding a pair with count == top.
