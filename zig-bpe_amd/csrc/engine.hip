@@ -947,6 +947,9 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                             "select end -> scan start (%llu) %.2f\n",
                     bucket[k], Q[4], Q[0] * us / nl, Q[1] * us / nl, Q[2] * us / nl, Q[3] * us / nl, Q[7], Q[5] * us / nr,
                     Q[6] * us / nr, Q[9], Q[8] * us / ns);
+            fprintf(stderr, "pipe_prof %s: replace phases, avg us from its block-0 start (latest block): deltas in %.2f, "
+                            "gathered %.2f, ids/hot reserved %.2f, table updated %.2f; apply blocks done %.2f\n",
+                    bucket[k], Q[10] * us / nr, Q[11] * us / nr, Q[12] * us / nr, Q[13] * us / nr, Q[14] * us / nr);
         }
     }
     stats.sharded_s = std::max(0.0, stats.sharded_s - stats.replicate_s);

@@ -1651,7 +1651,11 @@ __host__ __device__ inline uint32_t update_per(uint32_t X) {
 __device__ inline void update_block(const Tables &T, DevState *st, const uint32_t *__restrict__ left,
                                     const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
                                     uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per,
-                                    const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta) {
+                                    const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta, int prof = 0) {
+    // option sel_prof: the latest stamp of each phase over the update blocks (st->pp_t[8..11])
+    const auto stamp = [&](int k) {
+        if (prof && threadIdx.x == 0) atomicMax(&st->pp_t[k], (unsigned long long)wall_clock64());
+    };
     __shared__ uint32_t s_t[UPD_THREADS * UPD_MAX_PER], s_c[UPD_THREADS * UPD_MAX_PER];
     __shared__ uint32_t s_hot[UPD_THREADS * UPD_MAX_PER];
     __shared__ uint32_t s_n, s_nhot, s_base, s_hbase;
@@ -1685,6 +1689,14 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
     const uint32_t g = ublk / nch, beg = (ublk - g * nch) * UPD_THREADS * per;
     if (tid == 0) { s_n = 0; s_nhot = 0; s_live = 0; }
     __syncthreads();
+    if (prof) {  // the deltas arrived (every thread's loads)
+        uint32_t any = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < UPD_MAX_PER; k++) any |= dv[k];
+        if (any == 0xFFFFFFFFu) atomicOr(&st->error, 0u);  // (keeps the loads ahead of the stamp)
+        __syncthreads();
+        stamp(8);
+    }
 #pragma unroll
     for (uint32_t k = 0; k < UPD_MAX_PER; k++) {
         const uint32_t t = beg + k * UPD_THREADS + tid;
@@ -1696,6 +1708,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
         }
     }
     __syncthreads();
+    stamp(9);
     const uint32_t n = s_n;
     if (n == 0) return;
     const bool create = g == 1 || g == 3;
@@ -1714,6 +1727,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
             s_hbase = hb;
         }
         __syncthreads();
+        stamp(10);
         const uint32_t base = s_base, hbase = s_hbase;
         for (uint32_t j = tid; j < s_nhot; j += UPD_THREADS)
             if (hbase + j < T.hot_cap && base + s_hot[j] < T.id_cap) T.hot[hbase + j] = base + s_hot[j];
@@ -1741,6 +1755,10 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 ht_insert_new(T, key, id);
             }
         }
+    }
+    if (prof) {
+        __syncthreads();
+        stamp(11);
     }
     if (create) return;  // creating blocks kill no pair
     if (live_delta) atomicAdd(&s_live, live_delta);
@@ -1825,7 +1843,11 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
         }
         made = wave_sum(made);
         if ((threadIdx.x & 63) == 0 && made) atomicAdd(&st->holes_made, made);
-        if (R.prof && threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
+        if (R.prof) {
+            __syncthreads();
+            if (threadIdx.x == 0) atomicMax(&st->pp_t[12], (unsigned long long)wall_clock64());
+            if (threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
+        }
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->consumed = 0;
             if (R.dhalo) R.halo = *R.dhalo;
@@ -1848,7 +1870,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
     }
     const uint32_t ublk = blockIdx.x - R.apply_blocks;
     if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != st->top_count) atomicOr(&st->error, 64u);  // occurrences != count
-    update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta);
+    update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof);
     if (R.prof) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
@@ -3001,11 +3023,16 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     if (N.prof && blockIdx.x == 0 && tid == 0) {
         const unsigned long long now = wall_clock64();
         st->sel_t0 = now;
-        if (st->pp_t[5]) {  // the replace launch: its work span, its start -> this select's start
+        if (st->pp_t[5]) {  // the replace launch: its work span, its start -> this select's start, its phases
             unsigned long long *P = st->pipe_prof[pp_bucket(X)];
-            P[5] += st->pp_t[6] - st->pp_t[5];
-            P[6] += now - st->pp_t[5];
+            const unsigned long long t5 = st->pp_t[5];
+            P[5] += st->pp_t[6] - t5;
+            P[6] += now - t5;
             P[7]++;
+            for (int k = 8; k <= 12; k++) {
+                if (st->pp_t[k]) P[k + 2] += st->pp_t[k] - t5;
+                st->pp_t[k] = 0;
+            }
             st->pp_t[5] = st->pp_t[6] = 0;
         }
     }

@@ -71,7 +71,7 @@ struct DevState {
     // option sel_prof, whole merge pipeline (batch mode): probe stamps of the current launches and the
     // sums they fold into (Engine::train prints them): scan (list form) LDS clear / walk / flush done and
     // the next kernel's start, replace work span and the select's start, select end -> scan start
-    unsigned long long pp_t[8];
+    unsigned long long pp_t[16];  // [8..12]: replace phases (update blocks: deltas in, gathered, reserved, table done; apply done)
     unsigned long long pipe_prof[3][16];  // by merge: [256, 8192), [8192, 20000), [20000, ...)
 };
 // why a device-resident batch stopped (the host finishes that merge on the synchronous path)
