@@ -1,8 +1,12 @@
 #!/bin/bash
-# GPU box: fused-scan parity tests, A/B.
+# GPU box: parity subset (incl. the >4 GiB sharded corpus), A/B vs the previous build, pipeline probes.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu.py -x -q --timeout 200 --timeout-method thread -k "fused or c1 or synth_goldens" > gpurun_out/gt.log 2>&1 || { tail -40 gpurun_out/gt.log; exit 1; }
+AB=zig-bpe_amd/zbpe/ab
+timeout -k 10 900 python -u -m pytest tests/test_gpu.py tests/test_dist.py -x -q --timeout 200 --timeout-method thread -k "neighbour or arena or c1 or synth_goldens or random_corpora or encode or sharded or bench" > gpurun_out/gt.log 2>&1 || { tail -40 gpurun_out/gt.log; exit 1; }
 tail -2 gpurun_out/gt.log
-timeout -k 10 250 python -u tools/ab_run.py --reps 2 --cfg "" --cfg "fused_scan=1" > gpurun_out/ab_head.jsonl 2> gpurun_out/ab_head.err || { tail gpurun_out/ab_head.err; exit 3; }
-cat gpurun_out/ab_head.jsonl
+ZBPE_LIB=$PWD/$AB/libzbpe_head.so timeout -k 10 150 python -u tools/ab_run.py --reps 2 --cfg "" > gpurun_out/ab_prev.jsonl 2> gpurun_out/ab_prev.err || exit 2
+timeout -k 10 150 python -u tools/ab_run.py --reps 2 --cfg "" > gpurun_out/ab_head.jsonl 2> gpurun_out/ab_head.err || exit 3
+cat gpurun_out/ab_prev.jsonl gpurun_out/ab_head.jsonl
+timeout -k 10 150 python -u tools/trace_run.py --opt sel_prof=1 > gpurun_out/trace.txt 2>&1 || exit 5
+grep prof gpurun_out/trace.txt

@@ -57,8 +57,8 @@ void Engine::release() {
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_sizes);
-    f(d_enc_cnt); f(d_enc_ctr); f(d_succ); f(d_pred);
-    d_succ = d_pred = nullptr; succ_cap = pred_cap = 0;
+    f(d_enc_cnt); f(d_enc_ctr); f(d_nb);
+    d_nb = nullptr; nb_cap = 0;
     d_enc_cnt = nullptr; d_enc_ctr = nullptr; enc_cnt_cap = enc_ctr_cap = 0;
     for (auto &e : bev) if (e) (void)hipEventDestroy(e);
     bev.clear();
@@ -364,12 +364,10 @@ zbpe_status Engine::build_lists(uint32_t lists_x) {
     zbpe_list_offsets<<<1, 1024, 0, stream>>>(d_list_total, pres_vp, max_len, T.lst_off, T.lst_len, d_st, lists_x);
     LAUNCH_OK();
     if (list_nb) {  // the build-time neighbours of every list entry (the filtered list walk)
-        CHECK(ensure(&d_succ, succ_cap, (size_t)n + 64, "list successors"));
-        CHECK(ensure(&d_pred, pred_cap, (size_t)n + 64, "list predecessors"));
+        CHECK(ensure(&d_nb, nb_cap, (size_t)n + 64, "list neighbours"));
     }
     zbpe_list_scatter<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt, T.lst_off,
-                                                                       T.lst_len, d_lists, list_nb ? d_succ : nullptr,
-                                                                       list_nb ? d_pred : nullptr);
+                                                                       T.lst_len, d_lists, list_nb ? d_nb : nullptr);
     LAUNCH_OK();
     lists_on = true;
     nb_built = list_nb;
@@ -380,8 +378,7 @@ zbpe_status Engine::build_lists(uint32_t lists_x) {
 
 // list scans may filter list entries by their build-time neighbours (kernels.hpp scan_dispatch)
 void Engine::set_list_nb(ScanArgs &A) const {
-    A.succ = lists_on && nb_built ? d_succ : nullptr;
-    A.pred = lists_on && nb_built ? d_pred : nullptr;
+    A.nb = lists_on && nb_built ? d_nb : nullptr;
 }
 
 static uint32_t count_bin_lo(int b) {

@@ -111,8 +111,8 @@ struct Engine {
     size_t list_cnt_cap = 0;
     bool lists_on = false;
     // build-time neighbours of the list entries (the filtered list walk; option "list_nb")
-    uint16_t *d_succ = nullptr, *d_pred = nullptr;
-    size_t succ_cap = 0, pred_cap = 0;
+    uint32_t *d_nb = nullptr;  // pred << 16 | succ of every list entry at the build
+    size_t nb_cap = 0;
     bool list_nb = true, nb_built = false;
     bool list_streak = false;   // the last batch used list scans only
     int list_grid = 0;          // scan grid after such a batch (option "list_grid"; 0 = the full grid)

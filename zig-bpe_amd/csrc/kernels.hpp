@@ -381,8 +381,8 @@ struct ScanArgs {
     uint32_t *rec_ctr;      // record counter (nullptr: st->rec_count); batched encode: one per merge
     int prof;               // option sel_prof: probe stamps into st->pp_t (batch mode)
     // the neighbours of every list entry when the lists were built (Engine::build_lists; nullptr:
-    // none): succ[e] / pred[e] = the live token after / before position lists[e] at that time
-    const uint16_t *succ, *pred;
+    // none): nb[e] = pred << 16 | succ, the live tokens before / after position lists[e] at that time
+    const uint32_t *nb;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // the device-held parts of the arguments: pair (batch mode), halo (batch mode, multi-GPU), record
@@ -405,7 +405,7 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
     }
     return ScanArgs{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
                     A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
-                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.succ, A0.pred};
+                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb};
 }
 
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
@@ -757,7 +757,7 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
         // merged), so every occurrence of (a, b) is an entry of a's list whose successor was b at the
         // build (of b's list whose predecessor was a). The walk reads that neighbour with the entry
         // (coalesced) and gathers the stream only where it matches: ~count gathers, not ~len.
-        const uint16_t *NB = A.succ && A.a < lists_x && A.b < lists_x ? (by_b ? A.pred + ob : A.succ + oa) : nullptr;
+        const bool NB = A.nb && A.a < lists_x && A.b < lists_x;
         if (len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n) {
             if (blockIdx.x == 0 && threadIdx.x == 0) {
                 A.st->scan_mode = 1;
@@ -896,7 +896,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     const uint32_t ab = off & ~7u;                    // 16-B aligned start of the neighbour words
     const uint32_t span = off + len - ab;             // entries from ab to the list's end
     if (vb > 0 && (uint64_t)vb * per_block >= span) return;
-    const uint16_t *NB = by_b ? A.pred : A.succ;
+    const uint32_t *NB = A.nb, sh = by_b ? 16u : 0u;  // the build-time neighbour on the partner's side
     const uint32_t partner = by_b ? A.a : A.b, key = by_b ? A.b : A.a;
     scan_lds_clear(S);
     if (threadIdx.x == 0) S.any = 0;
@@ -913,23 +913,25 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
         const uint32_t e0 = ab + b0 + threadIdx.x * ept;  // this thread's first entry (absolute)
         uint32_t mk = 0;
         if (e0 < off + len) {
-            if (ept >= 8) {  // 16-B aligned (ab and ept are multiples of 8)
-                const uint4 w0 = *reinterpret_cast<const uint4 *>(NB + e0);
-                const uint4 w1 = ept == 16 ? *reinterpret_cast<const uint4 *>(NB + e0 + 8) : make_uint4(~0u, ~0u, ~0u, ~0u);
+            if (ept >= 8) {  // 16-B aligned words (ab and ept are multiples of 8)
+                const uint4 *q = reinterpret_cast<const uint4 *>(NB + e0);
+                const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+                const uint4 w[4] = {q[0], q[1], ept == 16 ? q[2] : none, ept == 16 ? q[3] : none};
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
-                    const uint32_t t = k < 8 ? tok_at(w0, k) : tok_at(w1, k - 8);
+                    const uint4 v = w[k >> 2];
+                    const uint32_t word = (k & 3) == 0 ? v.x : (k & 3) == 1 ? v.y : (k & 3) == 2 ? v.z : v.w;
                     const uint32_t e = e0 + k;
-                    mk |= (t == partner && e >= off && e < off + len && (uint32_t)k < ept) ? (1u << k) : 0u;
+                    mk |= (((word >> sh) & 0xFFFFu) == partner && e >= off && e < off + len && (uint32_t)k < ept) ? (1u << k) : 0u;
                 }
             } else {
                 uint32_t t[4];
 #pragma unroll
-                for (int k = 0; k < 4; k++) t[k] = (uint32_t)k < ept ? NB[e0 + k] : HOLE;
+                for (int k = 0; k < 4; k++) t[k] = (uint32_t)k < ept ? NB[e0 + k] : ~0u;
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const uint32_t e = e0 + k;
-                    mk |= (t[k] == partner && e >= off && e < off + len) ? (1u << k) : 0u;
+                    mk |= (((t[k] >> sh) & 0xFFFFu) == partner && e >= off && e < off + len) ? (1u << k) : 0u;
                 }
             }
         }
@@ -1593,8 +1595,7 @@ __global__ void __launch_bounds__(LIST_THREADS) zbpe_list_scatter(const uint16_t
                                                                   const uint32_t *__restrict__ colpre,
                                                                   const uint32_t *__restrict__ lst_off,
                                                                   const uint32_t *__restrict__ lst_len,
-                                                                  uint32_t *__restrict__ lists, uint16_t *__restrict__ succ,
-                                                                  uint16_t *__restrict__ pred) {
+                                                                  uint32_t *__restrict__ lists, uint32_t *__restrict__ nb) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
     for (uint32_t t = threadIdx.x; t < vp; t += LIST_THREADS)
         cur[t] = lst_len[t] == NO_LIST ? NO_LIST : lst_off[t] + colpre[(uint64_t)blockIdx.x * vp + t];
@@ -1610,9 +1611,10 @@ __global__ void __launch_bounds__(LIST_THREADS) zbpe_list_scatter(const uint16_t
             if (t < vp && p + k < end && cur[t] != NO_LIST) {
                 const uint32_t j = atomicAdd(&cur[t], 1u);
                 lists[j] = (uint32_t)(p + k);
-                if (succ) {
-                    succ[j] = (uint16_t)(k < 7 ? (p + k + 1 < n ? tok_at(v, k + 1) : HOLE) : (p + 8 < n ? after : HOLE));
-                    pred[j] = (uint16_t)(k > 0 ? tok_at(v, k - 1) : before);
+                if (nb) {
+                    const uint32_t sc = k < 7 ? (p + k + 1 < n ? tok_at(v, k + 1) : HOLE) : (p + 8 < n ? after : HOLE);
+                    const uint32_t pd = k > 0 ? tok_at(v, k - 1) : before;
+                    nb[j] = pd << 16 | sc;
                 }
             }
         }
