@@ -190,7 +190,7 @@ zbpe_status Engine::sync_state() {
 // tables sized for `need_ids`; rebuild keeps live ids only
 zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     size_t ht_cap_new = 1;
-    while (ht_cap_new < 2 * id_cap_new) ht_cap_new <<= 1;
+    while (ht_cap_new < 2 * id_cap_new || ht_cap_new < 64) ht_cap_new <<= 1;  // >= 8 buckets of 8
     Tables N{};
     N.hot = T.hot; N.hot_cap = T.hot_cap; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
     N.home_dirty = T.home_dirty;

@@ -44,13 +44,35 @@ __device__ inline uint32_t fmix32(uint32_t h) {
     h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
     return h;
 }
+// Open addressing over 64-byte buckets (8 slots of key<<32 | id, ~0 = empty): a lookup reads its
+// home bucket's cache line in one go (4 x 16 B loads in flight) instead of chasing slot by slot,
+// and moves to the next bucket only when the home bucket is full (~2 % of buckets at the table's
+// <= 1/2 load). A SIMT wave waits for its slowest lane, so the probe chain's tail is what counts.
+// Buckets fill as a prefix (an insert claims the first slot it sees empty) and keys are never
+// removed, so an empty slot ends a lookup.
+constexpr uint32_t HT_BUCKET = 8;
+__device__ inline uint32_t ht_home(const Tables &T, uint32_t key) {
+    return fmix32(key) & T.ht_mask & ~(HT_BUCKET - 1);
+}
+__device__ inline void ht_load_bucket(const Tables &T, uint32_t s, unsigned long long (&e)[HT_BUCKET]) {
+    const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(T.ht + s);
+    const ulonglong2 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+    e[0] = v0.x; e[1] = v0.y; e[2] = v1.x; e[3] = v1.y; e[4] = v2.x; e[5] = v2.y; e[6] = v3.x; e[7] = v3.y;
+}
 __device__ inline uint32_t ht_find(const Tables &T, uint32_t key) {
-    uint32_t s = fmix32(key) & T.ht_mask;
-    for (uint32_t probes = 0; probes <= T.ht_mask; ++probes) {
-        const unsigned long long e = T.ht[s];
-        if ((uint32_t)(e >> 32) == key) return (uint32_t)e;
-        if (e == ~0ull) return NO_ID;
-        s = (s + 1) & T.ht_mask;
+    uint32_t s = ht_home(T, key);
+    for (uint32_t probes = 0; probes <= T.ht_mask; probes += HT_BUCKET) {
+        unsigned long long e[HT_BUCKET];
+        ht_load_bucket(T, s, e);
+        uint32_t id = NO_ID;
+        bool empty = false;
+#pragma unroll
+        for (uint32_t k = 0; k < HT_BUCKET; k++) {
+            if ((uint32_t)(e[k] >> 32) == key) id = (uint32_t)e[k];
+            empty |= e[k] == ~0ull;
+        }
+        if (id != NO_ID || empty) return id;
+        s = (s + HT_BUCKET) & T.ht_mask;
     }
     return NO_ID;
 }
@@ -58,13 +80,22 @@ __device__ inline uint32_t ht_find_count(const Tables &T, uint32_t key) {
     uint32_t id = ht_find(T, key);
     return id == NO_ID ? 0 : T.id_cnt[id];
 }
-// Insert a key known to be absent (callers guarantee uniqueness within a launch).
+// Insert a key known to be absent (callers guarantee uniqueness within a launch). A lost race
+// moves to the next slot on the CAS's own answer, never re-reading the bucket: a plain re-read
+// could return this XCD's stale L2 copy of the line forever.
 __device__ inline void ht_insert_new(const Tables &T, uint32_t key, uint32_t id) {
-    uint32_t s = fmix32(key) & T.ht_mask;
+    uint32_t s = ht_home(T, key);
     const unsigned long long e = ((unsigned long long)key << 32) | id;
-    for (;;) {
-        if (atomicCAS(&T.ht[s], ~0ull, e) == ~0ull) return;
-        s = (s + 1) & T.ht_mask;
+    for (uint32_t probes = 0; probes <= T.ht_mask; probes += HT_BUCKET) {
+        unsigned long long v[HT_BUCKET];
+        ht_load_bucket(T, s, v);
+        uint32_t k = HT_BUCKET;
+#pragma unroll
+        for (int j = HT_BUCKET - 1; j >= 0; j--)
+            if (v[j] == ~0ull) k = (uint32_t)j;
+        for (; k < HT_BUCKET; k++)
+            if (atomicCAS(&T.ht[s + k], ~0ull, e) == ~0ull) return;
+        s = (s + HT_BUCKET) & T.ht_mask;
     }
 }
 // Live keys per home slot of the Zig map: kept incrementally once a tie
