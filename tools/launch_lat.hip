@@ -12,6 +12,20 @@
 
 __global__ void empty_k(int *p) { if (p && threadIdx.x == 1023) p[0] = 1; }
 
+// kernels that differ only in what the dispatcher must set up: private (scratch) memory, a large LDS
+// allocation; launched in alternating pairs to see which one a kernel boundary charges for
+__global__ void scratch_k(int *p, int idx) {
+    int a[256];
+    for (int k = 0; k < 256; k++) a[k] = k * (int)threadIdx.x;
+    if (p && a[(idx + threadIdx.x) & 255] == -1) p[0] = 1;
+}
+__global__ void lds_k(int *p) {
+    __shared__ uint32_t l[9728];  // 38 KB, like the scan kernel
+    l[threadIdx.x] = threadIdx.x;
+    __syncthreads();
+    if (p && l[(threadIdx.x + 1) & 255] == 999999u) p[0] = 1;
+}
+
 __global__ void chase_k(const uint32_t *next, int steps, uint32_t *out) {
     uint32_t i = 0;
     for (int s = 0; s < steps; s++) i = __builtin_nontemporal_load(&next[i]);
@@ -103,6 +117,24 @@ int main() {
         CK(hipEventElapsedTime(&ms, e0, e1));
         printf("{\"test\": \"empty_launch\", \"grid\": %d, \"us_per_launch\": %.3f}\n", grid, ms * 1e3 / R);
     }
+    // kernel pairs: which setup does a boundary charge for
+    for (int pa = 0; pa < 2; pa++)
+        for (int pb = 0; pb < 2; pb++) {
+            for (int w = 0; w < 2; w++) {
+                CK(hipEventRecord(e0, s));
+                for (int r = 0; r < R; r++) {
+                    if (pa) scratch_k<<<256, 256, 0, s>>>(nullptr, r);
+                    else empty_k<<<256, 256, 0, s>>>(nullptr);
+                    if (pb) lds_k<<<256, 256, 0, s>>>(nullptr);
+                    else empty_k<<<256, 256, 0, s>>>(nullptr);
+                }
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+            }
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("{\"test\": \"pair\", \"first\": \"%s\", \"second\": \"%s\", \"us_per_pair\": %.3f}\n", pa ? "scratch" : "empty",
+                   pb ? "lds38k" : "empty", ms * 1e3 / R);
+        }
     // pointer chase: random cycle over n words
     for (size_t bytes : {(size_t)1 << 20, (size_t)64 << 20, (size_t)512 << 20}) {
         const size_t n = bytes / 4;

@@ -2705,6 +2705,15 @@ __device__ inline Summ wave_compose(uint32_t lo, uint32_t hi, F f) {
     r.m = __shfl(x.m, 0);
     return r;
 }
+// write-through (sc1) loads of bytes another workgroup of the same launch stored write-through and
+// handed over through block_ticket_last: they bypass this CU's L1, so no acquire is needed
+// (MI355X_MICROARCH.md, valid hand-off forms, first table row)
+__device__ inline uint32_t ld_wt(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ inline Summ ld_wt(const Summ *p) {
+    const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    return Summ{(int32_t)(uint32_t)v, (int32_t)(uint32_t)(v >> 32)};
+}
 struct HomeView {
     const uint32_t *hc;
     const Summ *summ, *sup;
@@ -2777,7 +2786,7 @@ __device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const H
         for (int k = 0; k < 16; k++) w[k] = 0;
     }
     const uint32_t bi = sb * SUPER_BLOCKS + lane;
-    const Summ bs = bi < V.nb ? V.summ[bi] : Summ{0, 0};
+    const Summ bs = bi < V.nb ? ld_wt(V.summ + bi) : Summ{0, 0};
     const uint32_t nsup = V.nsb - 1, per = (nsup + 63) / 64, i0 = min(nsup, lane * per), i1 = min(nsup, i0 + per);
     Summ x3{0, 0};
     if (per <= 8) {  // up to 512 super-blocks (C <= 2^27): every load issued at once
@@ -2787,12 +2796,12 @@ __device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const H
             const uint32_t i = i0 + k;
             uint32_t j = sb + 1 + i;
             j = j >= V.nsb ? j - V.nsb : j;
-            sv[k] = i < i1 ? V.sup[j] : Summ{0, 0};
+            sv[k] = i < i1 ? ld_wt(V.sup + j) : Summ{0, 0};
         }
 #pragma unroll
         for (int k = 0; k < 8; k++) x3 = summ_cat(x3, sv[k]);
     } else {
-        for (uint32_t i = i0; i < i1; i++) x3 = summ_cat(x3, V.sup[(sb + 1 + i) % V.nsb]);
+        for (uint32_t i = i0; i < i1; i++) x3 = summ_cat(x3, ld_wt(V.sup + (sb + 1 + i) % V.nsb));
     }
     Summ x1{0, 0}, x5{0, 0};
 #pragma unroll
@@ -3014,19 +3023,16 @@ __device__ inline void sel_tick(DevState *st, int k, unsigned long long *t) {
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
 // relaxed atomic stores) and is drained here, so no release fence (an L2 writeback, 1.7-6.5 us on
-// the critical path) is needed; the last block's acquire drops its CU's stale L1 lines
-// (cdna_hip_programming.md section 6 G16; MI355X_MICROARCH.md fence table)
+// the critical path) is needed; the last block reads those bytes with sc1 loads (ld_wt), which
+// bypass its CU's L1, so no acquire either (MI355X_MICROARCH.md, valid hand-off forms: one lane of
+// each storing workgroup adds to one counter after the workgroup's vmcnt(0) and barrier; the
+// workgroup whose add came last loads after its add has returned, its other waves after a barrier)
 __device__ inline bool block_ticket_last(uint32_t *ticket, uint32_t nblocks, uint32_t *s_flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = t == nblocks - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *s_flag = last ? 1u : 0u;
+        *s_flag = t == nblocks - 1 ? 1u : 0u;
     }
     __syncthreads();
     return *s_flag != 0;
@@ -3148,8 +3154,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     unsigned long long pt = 0;
     if (N.prof && tid == 0) {
         pt = st->sel_t0;
-        atomicAdd(&st->sel_prof[5], st->sel_ta - pt);
-        if (st->sel_tr) atomicAdd(&st->sel_prof[6], st->sel_tr - pt);
+        const unsigned long long ta = __hip_atomic_load(&st->sel_ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long tr = __hip_atomic_load(&st->sel_tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&st->sel_prof[5], ta - pt);
+        if (tr) atomicAdd(&st->sel_prof[6], tr - pt);
         st->sel_ta = st->sel_tr = 0;
         sel_tick(st, 0, &pt);
         atomicAdd(&st->sel_prof[7], 1ull);
@@ -3157,7 +3165,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     // ---- the last block: argmax, roll of merge X -------------------------------------------------
     MaxRec q{0, 0, NO_ID};
     for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
-        const MaxRec p = partial[b];
+        const MaxRec p{ld_wt(&partial[b].cnt), ld_wt(&partial[b].ties), ld_wt(&partial[b].id)};
         s_pc[b] = p.cnt;
         s_pt[b] = p.ties;
         q = max_combine(q, p);
@@ -3165,13 +3173,13 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     const MaxRec Q = block_max(q, sm);  // (its barriers also publish s_pc / s_pt)
     if (Q.ties == 1 && Q.cnt) {  // the unique max: its block kept its key
         for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS)
-            if (s_pc[b] == Q.cnt) s_key[0] = N.pkey[b];
+            if (s_pc[b] == Q.cnt) s_key[0] = ld_wt(N.pkey + b);
     }
     __syncthreads();
     if (N.prof && tid == 0) sel_tick(st, 1, &pt);
     if (tid == 0) {
         select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, Q.ties == 1 && Q.cnt ? s_key[0] : NO_ID,
-                      N.world == 1 ? N.lastpair[0] : NO_ID);
+                      N.world == 1 ? ld_wt(N.lastpair) : NO_ID);
         s_h = HALT_DONE;
         s_tie = 0;
         if (N.B.X < N.x_end) {
@@ -3252,7 +3260,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
             const uint32_t mid = (lo + hi) >> 1;
             if (s_to[mid] <= e) lo = mid; else hi = mid;
         }
-        const uint32_t key = N.cand[s_tb[lo] * NEXT_CAND + (e - s_to[lo])];
+        const uint32_t key = ld_wt(N.cand + s_tb[lo] * NEXT_CAND + (e - s_to[lo]));
         N.tie_list[e] = ((uint64_t)(zig_pair_hash(key) & cap_mask) << 32) | key;
     }
     if (tid == 0) st->tie_len = total;
