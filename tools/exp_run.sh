@@ -10,3 +10,6 @@ timeout -k 10 150 python -u tools/ab_run.py --reps 2 --cfg "" > gpurun_out/ab_he
 cat gpurun_out/ab_prev.jsonl gpurun_out/ab_head.jsonl
 timeout -k 10 150 python -u tools/trace_run.py --opt sel_prof=1 > gpurun_out/trace.txt 2>&1 || exit 5
 grep prof gpurun_out/trace.txt
+rm -rf gpurun_out/prof && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 tools/ab_run.py --reps 1 --cfg "" > gpurun_out/prof_ab.jsonl 2> gpurun_out/prof.err || { tail gpurun_out/prof.err; exit 7; }
+python3 tools/prof_summary.py gpurun_out/prof > gpurun_out/prof_summary.txt; head -24 gpurun_out/prof_summary.txt
+find gpurun_out/prof -name "*kernel_trace.csv" -size +20M -delete

@@ -14,10 +14,14 @@ __global__ void empty_k(int *p) { if (p && threadIdx.x == 1023) p[0] = 1; }
 
 // kernels that differ only in what the dispatcher must set up: private (scratch) memory, a large LDS
 // allocation; launched in alternating pairs to see which one a kernel boundary charges for
+// private memory allocated (the dynamically indexed array) but never touched: idx >= 0 always
+template <int N>
 __global__ void scratch_k(int *p, int idx) {
-    int a[256];
-    for (int k = 0; k < 256; k++) a[k] = k * (int)threadIdx.x;
-    if (p && a[(idx + threadIdx.x) & 255] == -1) p[0] = 1;
+    if (idx < 0) {
+        int a[N];
+        for (int k = 0; k < N; k++) a[k] = k * (int)threadIdx.x;
+        p[0] = a[(-idx + threadIdx.x) % N];
+    }
 }
 __global__ void lds_k(int *p) {
     __shared__ uint32_t l[9728];  // 38 KB, like the scan kernel
@@ -118,12 +122,13 @@ int main() {
         printf("{\"test\": \"empty_launch\", \"grid\": %d, \"us_per_launch\": %.3f}\n", grid, ms * 1e3 / R);
     }
     // kernel pairs: which setup does a boundary charge for
-    for (int pa = 0; pa < 2; pa++)
+    for (int pa = 0; pa < 3; pa++)
         for (int pb = 0; pb < 2; pb++) {
             for (int w = 0; w < 2; w++) {
                 CK(hipEventRecord(e0, s));
                 for (int r = 0; r < R; r++) {
-                    if (pa) scratch_k<<<256, 256, 0, s>>>(nullptr, r);
+                    if (pa == 1) scratch_k<64><<<256, 256, 0, s>>>(nullptr, r);
+                    else if (pa == 2) scratch_k<256><<<256, 256, 0, s>>>(nullptr, r);
                     else empty_k<<<256, 256, 0, s>>>(nullptr);
                     if (pb) lds_k<<<256, 256, 0, s>>>(nullptr);
                     else empty_k<<<256, 256, 0, s>>>(nullptr);
@@ -132,7 +137,7 @@ int main() {
                 CK(hipEventSynchronize(e1));
             }
             CK(hipEventElapsedTime(&ms, e0, e1));
-            printf("{\"test\": \"pair\", \"first\": \"%s\", \"second\": \"%s\", \"us_per_pair\": %.3f}\n", pa ? "scratch" : "empty",
+            printf("{\"test\": \"pair\", \"first\": \"%s\", \"second\": \"%s\", \"us_per_pair\": %.3f}\n", pa == 1 ? "scratch256B" : pa == 2 ? "scratch1KB" : "empty",
                    pb ? "lds38k" : "empty", ms * 1e3 / R);
         }
     // pointer chase: random cycle over n words

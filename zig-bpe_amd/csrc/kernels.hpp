@@ -83,12 +83,12 @@ __device__ inline uint32_t ht_find_count(const Tables &T, uint32_t key) {
 // Insert a key known to be absent (callers guarantee uniqueness within a launch). A lost race
 // moves to the next slot on the CAS's own answer, never re-reading the bucket: a plain re-read
 // could return this XCD's stale L2 copy of the line forever.
-__device__ inline void ht_insert_new(const Tables &T, uint32_t key, uint32_t id) {
+// v: the home bucket of `key`, already loaded (ht_load_bucket(T, ht_home(T, key), v))
+__device__ inline void ht_insert_loaded(const Tables &T, uint32_t key, uint32_t id, unsigned long long (&v)[HT_BUCKET]) {
     uint32_t s = ht_home(T, key);
     const unsigned long long e = ((unsigned long long)key << 32) | id;
     for (uint32_t probes = 0; probes <= T.ht_mask; probes += HT_BUCKET) {
-        unsigned long long v[HT_BUCKET];
-        ht_load_bucket(T, s, v);
+        if (probes) ht_load_bucket(T, s, v);
         uint32_t k = HT_BUCKET;
 #pragma unroll
         for (int j = HT_BUCKET - 1; j >= 0; j--)
@@ -97,6 +97,11 @@ __device__ inline void ht_insert_new(const Tables &T, uint32_t key, uint32_t id)
             if (atomicCAS(&T.ht[s + k], ~0ull, e) == ~0ull) return;
         s = (s + HT_BUCKET) & T.ht_mask;
     }
+}
+__device__ inline void ht_insert_new(const Tables &T, uint32_t key, uint32_t id) {
+    unsigned long long v[HT_BUCKET];
+    ht_load_bucket(T, ht_home(T, key), v);
+    ht_insert_loaded(T, key, id, v);
 }
 // Live keys per home slot of the Zig map: kept incrementally once a tie
 // has asked for it, so later ties need no pass over every key.
@@ -1745,6 +1750,11 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
     const uint32_t n = s_n;
     if (n == 0) return;
     const bool create = g == 1 || g == 3;
+    // a creating thread's first new key: its home bucket is read while the ids are reserved (the
+    // insert's CAS then follows the reservation directly instead of a second memory round trip)
+    unsigned long long pre[HT_BUCKET];
+    const uint32_t key0 = create && tid < n ? (g == 1 ? pair_key(s_t[tid], X) : pair_key(X, s_t[tid])) : 0u;
+    if (create && tid < n) ht_load_bucket(T, ht_home(T, key0), pre);
     if (create) {
         // the new ids that reach theta join the hot list: their slots are reserved by the same
         // thread and at the same time as the ids (two returning atomics in flight, not in series)
@@ -1785,7 +1795,8 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 T.id_key[id] = key;
                 T.id_cnt[id] = c;
                 home_add(T, st, key, true);
-                ht_insert_new(T, key, id);
+                if (i == tid) ht_insert_loaded(T, key, id, pre);
+                else ht_insert_new(T, key, id);
             }
         }
     }
@@ -1991,37 +2002,80 @@ constexpr int SELF_THREADS = 256;
 constexpr int SELF_PER_THREAD = 32;
 constexpr int SELF_TILE = SELF_THREADS * SELF_PER_THREAD;  // 8192
 static_assert(SELF_TILE == PRES_BLK, "a self-pair tile is one presence block");
-// run-parity function of SELF_PER_THREAD slots: bit0 = no live non-a (x -> x ^ p), bit1 = p
-__device__ inline uint8_t self_segment(const uint16_t *tok, int64_t p0, int64_t end, uint32_t a) {
-    uint8_t all = 1, par = 0;
-    for (int i = 0; i < SELF_PER_THREAD; i++) {
-        const int64_t p = p0 + i;
-        if (p >= end) break;
-        const uint32_t t = tok[p];
-        if (t == HOLE) continue;
-        if (t != a) { all = 0; par = 0; }
-        else par ^= 1;
+// run-parity function of a segment: bit0 = no live non-a (x -> x ^ p), bit1 = p
+__device__ inline uint8_t self_apply(uint8_t f, uint8_t x) { return (f & 1) ? (uint8_t)(x ^ ((f >> 1) & 1)) : (uint8_t)((f >> 1) & 1); }
+// g after f
+__device__ inline uint8_t self_compose(uint8_t f, uint8_t g) { return (g & 1) ? (uint8_t)((f & 1) | ((f ^ g) & 2)) : g; }
+// a thread's SELF_PER_THREAD slots [p0, p0 + 32) in registers, two tokens a word (HOLE past end):
+// four 16-B loads, not 32 two-byte ones
+__device__ inline void self_load(const uint16_t *tok, int64_t p0, int64_t end, uint32_t (&w)[16]) {
+    if (p0 + SELF_PER_THREAD <= end) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(tok + p0);
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const uint4 x = q[v];
+            w[4 * v] = x.x; w[4 * v + 1] = x.y; w[4 * v + 2] = x.z; w[4 * v + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t lo = p0 + 2 * k < end ? tok[p0 + 2 * k] : HOLE;
+            const uint32_t hi = p0 + 2 * k + 1 < end ? tok[p0 + 2 * k + 1] : HOLE;
+            w[k] = lo | (hi << 16);
+        }
     }
+}
+// the run-parity function of the 32 slots, and (when x_in >= 0) the mask of the slots holding an a
+// at an even offset of its live run given the parity x_in of the run entering them
+__device__ inline uint8_t self_walk(const uint32_t (&w)[16], uint32_t a, int x_in, uint32_t *even_a) {
+    uint8_t all = 1, par = 0, x = (uint8_t)(x_in & 1);
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < SELF_PER_THREAD; i++) {
+        const uint32_t t = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        if (t == HOLE) continue;
+        if (t != a) { all = 0; par = 0; x = 0; continue; }
+        par ^= 1;
+        if (!x) m |= 1u << i;
+        x ^= 1;
+    }
+    if (even_a) *even_a = m;
     return (uint8_t)(all | (par << 1));
 }
-__device__ inline uint8_t self_apply(uint8_t f, uint8_t x) { return (f & 1) ? (uint8_t)(x ^ ((f >> 1) & 1)) : (uint8_t)((f >> 1) & 1); }
+// exclusive composition of the threads' functions in thread order (wave shuffles, then the waves
+// through LDS); *total: the whole block's function
+__device__ inline uint8_t self_block_scan(uint8_t f, uint8_t *s_wave, uint8_t *total) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint8_t inc = f;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint8_t y = (uint8_t)__shfl_up((int)inc, off);
+        if ((int)lane >= off) inc = self_compose(y, inc);
+    }
+    uint8_t ex = (uint8_t)__shfl_up((int)inc, 1);
+    if (lane == 0) ex = 1;  // identity
+    if (lane == 63) s_wave[wv] = inc;
+    __syncthreads();
+    uint8_t pre = 1;
+    for (uint32_t j = 0; j < wv; j++) pre = self_compose(pre, s_wave[j]);
+    if (total) {
+        uint8_t t = 1;
+        for (uint32_t j = 0; j < SELF_THREADS / 64; j++) t = self_compose(t, s_wave[j]);
+        *total = t;
+    }
+    return self_compose(pre, ex);
+}
 __global__ void __launch_bounds__(SELF_THREADS) zbpe_self_tiles(const uint16_t *__restrict__ tok, int64_t n, uint32_t a,
                                                                 uint8_t *__restrict__ tile_fn) {
     // tile_fn bit0: the tile holds no live non-a; bit1: parity of its trailing live a-run
     const int64_t beg = blockIdx.x * (int64_t)SELF_TILE;
     const int64_t end = min(n, beg + SELF_TILE);
-    __shared__ uint8_t s_fn[SELF_THREADS];
-    s_fn[threadIdx.x] = self_segment(tok, beg + threadIdx.x * SELF_PER_THREAD, end, a);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint8_t all = 1, par = 0;  // identity
-        for (int t = 0; t < SELF_THREADS; t++) {
-            const uint8_t f = s_fn[t];
-            if (f & 1) par ^= (f >> 1) & 1;
-            else { all = 0; par = (f >> 1) & 1; }
-        }
-        tile_fn[blockIdx.x] = (uint8_t)(all | (par << 1));
-    }
+    __shared__ uint8_t s_wave[SELF_THREADS / 64];
+    uint32_t w[16];
+    self_load(tok, beg + threadIdx.x * SELF_PER_THREAD, end, w);
+    uint8_t total;
+    (void)self_block_scan(self_walk(w, a, -1, nullptr), s_wave, &total);
+    if (threadIdx.x == 0) tile_fn[blockIdx.x] = total;
 }
 // carry_in[t] = parity of the a-run entering tile t. One block; each thread composes a segment.
 // carry_in[t] = parity of the a-run entering tile t, starting from *x0 (the run entering the shard
@@ -2075,7 +2129,7 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
     const ScanArgs A = scan_args_resolve(A0);
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
     __shared__ uint32_t s_rec[SELF_TILE / 2];
-    __shared__ uint8_t s_fn[SELF_THREADS];
+    __shared__ uint8_t s_wave[SELF_THREADS / 64];
     __shared__ uint32_t s_nrec, s_base;
     for (int i = threadIdx.x; i < LDS_BINS; i += SELF_THREADS) { s_left[i] = 0; s_right[i] = 0; }
     if (threadIdx.x == 0) s_nrec = 0;
@@ -2085,21 +2139,17 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
     const int64_t beg = blockIdx.x * (int64_t)SELF_TILE;
     const int64_t end = min(A.n, beg + SELF_TILE);
     const int64_t t0 = beg + threadIdx.x * SELF_PER_THREAD;
-    s_fn[threadIdx.x] = self_segment(tok, t0, end, a);
-    __syncthreads();
-    // parity of the live a-run entering my segment: the tile's carry through the segments before mine
-    uint8_t x = carry_in[blockIdx.x] & 1;
-    for (int t = 0; t < (int)threadIdx.x; t++) x = self_apply(s_fn[t], x);
+    uint32_t w[16];
+    self_load(tok, t0, end, w);
+    // parity of the live a-run entering my slots: the tile's carry through the threads before mine
+    const uint8_t pre = self_block_scan(self_walk(w, a, -1, nullptr), s_wave, nullptr);
+    uint32_t cand;
+    (void)self_walk(w, a, self_apply(pre, carry_in[blockIdx.x] & 1), &cand);
     uint32_t xx = 0;
-    for (int i = 0; i < SELF_PER_THREAD; i++) {
+    while (cand) {  // a's at even offsets of their runs: occurrences when the next live token is an a
+        const int i = __builtin_ctz(cand);
+        cand &= cand - 1;
         const int64_t p = t0 + i;
-        if (p >= end) break;
-        const uint32_t tp = tok[p];
-        if (tp == HOLE) continue;
-        if (tp != a) { x = 0; continue; }
-        const uint8_t off_par = x;
-        x ^= 1;
-        if (off_par) continue;  // odd offset in its run: the b of an occurrence (or a lone trailing a)
         const int64_t q = next_live_h(A, p);
         if (q == NONE_POS || tok_h(A, q) != a) continue;
         // occurrence (p, q)
@@ -2335,9 +2385,35 @@ __global__ void __launch_bounds__(256) zbpe_hot_build(Tables T, DevState *st) {
 // (agent-scope release/acquire around the ticket, cdna_hip_programming.md Guideline 16), the
 // stream's last-pair count, and the end-of-merge resets (neighbour histograms, counters) when
 // roll != 0. One launch per merge instead of three.
+// the state words merge_begin_eval / merge_begin_commit read, as select_finish left them (the fused
+// select passes them on in registers instead of reloading what the same thread just stored)
+struct FinishOut {
+    int32_t live;
+    uint32_t hot_len, top_count, tie_count, arena_top, arena_rep, lastpair, key;
+    long long live_tokens;
+};
+// the state words the roll reads (select_finish), in the order of RollIn's slots
+enum RollIn : int { RI_REC, RI_TOTAL_OCC, RI_HOLES, RI_ARENA_TOP, RI_ARENA_REP, RI_GOCC, RI_LIVE_TOK_LO, RI_LIVE_TOK_HI,
+                    RI_LIVE, RI_HOT_LEN, RI_LASTPAIR, RI_WORDS };
+// The fused select's roll words, loaded at kernel start straight into LDS by lanes [0, RI_WORDS) of
+// wave 0 (global_load_lds: no registers held across the kernel); they are stable until the last
+// block rolls, and block_ticket_last's vmcnt(0) + barrier publishes them to the block.
+__device__ inline void roll_preload(const DevState *st, const uint32_t *delta, uint32_t X, uint32_t *s_pre) {
+    const uint32_t lane = threadIdx.x;
+    if (lane >= RI_WORDS) return;
+    const uint32_t *w = lane == RI_REC ? &st->rec_count : lane == RI_TOTAL_OCC ? &st->total_occ
+                        : lane == RI_HOLES ? &st->holes_made : lane == RI_ARENA_TOP ? &st->arena_top
+                        : lane == RI_ARENA_REP ? &st->arena_rep : lane == RI_GOCC ? delta + 2 * X + 1
+                        : lane == RI_LIVE_TOK_LO ? reinterpret_cast<const uint32_t *>(&st->live_tokens)
+                        : lane == RI_LIVE_TOK_HI ? reinterpret_cast<const uint32_t *>(&st->live_tokens) + 1
+                        : lane == RI_LIVE ? reinterpret_cast<const uint32_t *>(&st->live)
+                        : lane == RI_HOT_LEN ? &st->hot_len : &st->lastpair_count;
+    __builtin_amdgcn_global_load_lds(w, (__attribute__((address_space(3))) void *)s_pre, 4, 0, 0);
+}
 __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, const uint16_t *tok, int64_t n,
                                      uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world,
-                                     uint32_t key_hint = NO_ID, uint32_t lastpair_hint = NO_ID);
+                                     uint32_t key_hint = NO_ID, uint32_t lastpair_hint = NO_ID, FinishOut *fo = nullptr,
+                                     const uint32_t *pre = nullptr, bool defer_key = false);
 __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState *st, MaxRec *__restrict__ partial,
                                                               const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
                                                               uint32_t X, int roll, const Boundary *__restrict__ bnd, int world) {
@@ -2384,20 +2460,37 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
 // and at roll the end-of-merge bookkeeping (occurrence list of X, counters, deltas' tail)
 __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, const uint16_t *tok, int64_t n,
                                      uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world,
-                                     uint32_t key_hint, uint32_t lastpair_hint) {
+                                     uint32_t key_hint, uint32_t lastpair_hint, FinishOut *fo, const uint32_t *pre,
+                                     bool defer_key) {
     {
         // every state word the roll reads, loaded together before the first store (the stores
-        // below may alias them as far as the compiler knows, which would serialise each load)
+        // below may alias them as far as the compiler knows, which would serialise each load), or
+        // preloaded (pre: roll_preload's LDS words)
         uint32_t *tail = delta + 2 * X;
-        const uint32_t rec_count = st->rec_count, total_occ = st->total_occ, holes_made = st->holes_made;
-        const uint32_t arena_top = st->arena_top, arena_rep = st->arena_rep, gocc = roll ? tail[1] : 0u;
-        const long long live_tokens = st->live_tokens;
+        uint32_t rec_count, total_occ, holes_made, arena_top, arena_rep, gocc, hot_len, lastpair_old;
+        long long live_tokens;
+        int32_t live;
+        if (pre) {
+            rec_count = pre[RI_REC]; total_occ = pre[RI_TOTAL_OCC]; holes_made = pre[RI_HOLES];
+            arena_top = pre[RI_ARENA_TOP]; arena_rep = pre[RI_ARENA_REP]; gocc = roll ? pre[RI_GOCC] : 0u;
+            live_tokens = (long long)(((uint64_t)pre[RI_LIVE_TOK_HI] << 32) | pre[RI_LIVE_TOK_LO]);
+            live = (int32_t)pre[RI_LIVE]; hot_len = pre[RI_HOT_LEN]; lastpair_old = pre[RI_LASTPAIR];
+        } else {
+            rec_count = st->rec_count; total_occ = st->total_occ; holes_made = st->holes_made;
+            arena_top = st->arena_top; arena_rep = st->arena_rep; gocc = roll ? tail[1] : 0u;
+            live_tokens = st->live_tokens;
+            live = st->live; hot_len = st->hot_len; lastpair_old = st->lastpair_count;
+        }
+        // defer_key: the caller stores top_key itself later (its load is off the critical path; the
+        // key matters to merge_begin only without a tie, when key_hint has it)
+        const uint32_t top_key = q.id == NO_ID ? EMPTY_KEY : key_hint != NO_ID ? key_hint : defer_key ? NO_ID : T.id_key[q.id];
+        uint32_t lastpair = lastpair_old;
         st->top_count = q.cnt;
         st->tie_count = q.cnt ? q.ties : 0;
         st->top_id = q.id;
-        st->top_key = q.id == NO_ID ? EMPTY_KEY : key_hint != NO_ID ? key_hint : T.id_key[q.id];
+        if (top_key != NO_ID) st->top_key = top_key;
         if (q.ties > 1 && lastpair_hint != NO_ID) {
-            st->lastpair_count = lastpair_hint;
+            st->lastpair_count = lastpair = lastpair_hint;
         } else if (q.ties > 1) {
             uint32_t lt[2];  // last live token of the whole stream, then the one before
             int got = 0;
@@ -2408,7 +2501,18 @@ __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, co
                 for (int64_t p = n - 1; p >= 0 && got < 2; p--)
                     if (tok[p] != HOLE) lt[got++] = tok[p];
             }
-            st->lastpair_count = got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0;
+            st->lastpair_count = lastpair = got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0;
+        }
+        if (fo) {
+            fo->live = live;
+            fo->hot_len = hot_len;
+            fo->top_count = q.cnt;
+            fo->tie_count = q.cnt ? q.ties : 0;
+            fo->arena_top = roll && T.lst_off ? arena_top + rec_count : arena_top;
+            fo->arena_rep = roll ? arena_rep + gocc : arena_rep;
+            fo->lastpair = lastpair;
+            fo->key = top_key;
+            fo->live_tokens = roll ? live_tokens - holes_made : live_tokens;
         }
         if (roll) {
             st->last_occ = rec_count;
@@ -2485,12 +2589,12 @@ struct BeginArgs {
     MergeLog *log;
     int rep;            // sharded: test the replicated bound st->arena_rep (every rank halts alike)
 };
-__device__ inline uint32_t merge_begin_eval(const Tables &T, const DevState *st, const BeginArgs &B, bool *tie) {
+__device__ inline uint32_t merge_begin_eval_v(const Tables &T, const FinishOut &f, const BeginArgs &B, bool *tie) {
     *tie = false;
-    const int32_t live = st->live;  // the words read, loaded together
-    const uint32_t hot_len = st->hot_len, top_count = st->top_count, tie_count = st->tie_count;
-    const uint32_t arena_top = B.rep ? st->arena_rep : st->arena_top;
-    const uint32_t lastpair = st->lastpair_count, key = st->top_key;
+    const int32_t live = f.live;
+    const uint32_t hot_len = f.hot_len, top_count = f.top_count, tie_count = f.tie_count;
+    const uint32_t arena_top = B.rep ? f.arena_rep : f.arena_top;
+    const uint32_t lastpair = f.lastpair, key = f.key;
     if (live <= 0) return HALT_DONE;
     if (hot_len > T.hot_cap || top_count == 0) return HALT_SELECT;
     if ((uint64_t)arena_top + top_count > B.rec_cap) return HALT_RECORDS;
@@ -2501,9 +2605,26 @@ __device__ inline uint32_t merge_begin_eval(const Tables &T, const DevState *st,
     }
     return (key & 0xFFFF) == (key >> 16) ? HALT_SELF : HALT_NONE;
 }
-__device__ inline void merge_begin_commit(DevState *st, const BeginArgs &B, uint32_t h, bool tie) {
-    const uint32_t key = st->top_key, top_count = st->top_count, tie_count = st->tie_count;  // loaded before the stores
-    const long long live_tokens = st->live_tokens;
+// the state words read, loaded together
+__device__ inline FinishOut finish_state(const DevState *st) {
+    FinishOut f;
+    f.live = st->live;
+    f.hot_len = st->hot_len;
+    f.top_count = st->top_count;
+    f.tie_count = st->tie_count;
+    f.arena_top = st->arena_top;
+    f.arena_rep = st->arena_rep;
+    f.lastpair = st->lastpair_count;
+    f.key = st->top_key;
+    f.live_tokens = st->live_tokens;
+    return f;
+}
+__device__ inline uint32_t merge_begin_eval(const Tables &T, const DevState *st, const BeginArgs &B, bool *tie) {
+    return merge_begin_eval_v(T, finish_state(st), B, tie);
+}
+__device__ inline void merge_begin_commit_v(DevState *st, const BeginArgs &B, uint32_t h, bool tie, const FinishOut &f) {
+    const uint32_t key = f.key, top_count = f.top_count, tie_count = f.tie_count;
+    const long long live_tokens = f.live_tokens;
     st->cur_x = B.X;
     st->tie_on = tie ? 1u : 0u;
     if (h) {
@@ -2513,6 +2634,9 @@ __device__ inline void merge_begin_commit(DevState *st, const BeginArgs &B, uint
         st->cur_key = key;
         B.log[B.X - 256] = MergeLog{key, top_count, (uint32_t)live_tokens, tie_count};
     }
+}
+__device__ inline void merge_begin_commit(DevState *st, const BeginArgs &B, uint32_t h, bool tie) {
+    merge_begin_commit_v(st, B, h, tie, finish_state(st));
 }
 __global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, uint32_t top, uint32_t cap_mask,
                                                         uint64_t *__restrict__ tie_list, uint32_t tie_cap, int dyn,
@@ -2589,31 +2713,33 @@ __device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslo
     Summ old{0, 0};
     if (wave == 0 && sb * SUPER_BLOCKS + lane < nb && !((bits >> lane) & 1)) old = summ[sb * SUPER_BLOCKS + lane];
     const int ndirty = __popcll(bits);
-    for (int k = wave; k < ndirty; k += nwaves) {
-        uint64_t m = bits;  // k-th set bit
+    // two dirty blocks per wave per round, both blocks' slots loaded before either is folded (one
+    // memory latency per round, not two)
+    auto kth = [&](int k) -> uint32_t {  // index of the k-th set bit of `bits`
+        uint64_t m = bits;
         for (int j = 0; j < k; j++) m &= m - 1;
-        const uint32_t bi = (uint32_t)__builtin_ctzll(m), blk = sb * SUPER_BLOCKS + bi;
+        return (uint32_t)__builtin_ctzll(m);
+    };
+    auto load = [&](uint32_t blk, uint32_t (&w)[16]) {
         const uint32_t s0 = blk * SUMM_SLOTS + 64 * lane;
-        Summ x{0, 0};
-        if (s0 + 64 <= nslots) {
+        if (s0 < nslots) {
             const uint4 *p = reinterpret_cast<const uint4 *>(T.home_cnt + s0 / 4);
-            uint32_t w[16];
 #pragma unroll
             for (int v = 0; v < 4; v++) {
                 const uint4 q = p[v];
                 w[4 * v] = q.x; w[4 * v + 1] = q.y; w[4 * v + 2] = q.z; w[4 * v + 3] = q.w;
             }
+        }
+    };
+    auto fold = [&](uint32_t blk, const uint32_t (&w)[16]) -> Summ {
+        const uint32_t s0 = blk * SUMM_SLOTS + 64 * lane;
+        Summ x{0, 0};
+        if (s0 + 64 <= nslots) {
             x = fold64(w);
         } else if (s0 < nslots) {
-            const uint4 *p = reinterpret_cast<const uint4 *>(T.home_cnt + s0 / 4);
 #pragma unroll
-            for (int v = 0; v < 4; v++) {
-                const uint4 q = p[v];
-                const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int kk = 0; kk < 16; kk++)
-                    if (s0 + 16 * v + kk < nslots) x = slot_fold(x, ((w[kk >> 2] >> (8 * (kk & 3))) & 0xffu));
-            }
+            for (int kk = 0; kk < 64; kk++)
+                if (s0 + kk < nslots) x = slot_fold(x, ((w[kk >> 2] >> (8 * (kk & 3))) & 0xffu));
         }
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -2622,14 +2748,29 @@ __device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslo
             y.m = __shfl_down(x.m, off);
             if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
         }
-        if (lane == 0) {
-            if (wt) {
-                __hip_atomic_store(&summ[blk].q, x.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&summ[blk].m, x.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                summ[blk] = x;
-            }
-            s_new[bi] = x;
+        return x;
+    };
+    auto put = [&](uint32_t bi, Summ x) {
+        const uint32_t blk = sb * SUPER_BLOCKS + bi;
+        if (wt) {
+            __hip_atomic_store(&summ[blk].q, x.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&summ[blk].m, x.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            summ[blk] = x;
+        }
+        s_new[bi] = x;
+    };
+    for (int k = wave; k < ndirty; k += 2 * nwaves) {
+        const bool two = k + nwaves < ndirty;
+        const uint32_t bi0 = kth(k), bi1 = two ? kth(k + nwaves) : bi0;
+        uint32_t w0[16], w1[16];
+        load(sb * SUPER_BLOCKS + bi0, w0);
+        if (two) load(sb * SUPER_BLOCKS + bi1, w1);
+        const Summ x0 = fold(sb * SUPER_BLOCKS + bi0, w0);
+        if (lane == 0) put(bi0, x0);
+        if (two) {
+            const Summ x1 = fold(sb * SUPER_BLOCKS + bi1, w1);
+            if (lane == 0) put(bi1, x1);
         }
     }
     __syncthreads();
@@ -2769,11 +2910,11 @@ __device__ inline Summ wave_reduce_summ(Summ x) {
 // slots after s in its block, the blocks after it in its super-block, the other super-blocks, the
 // blocks before it in its super-block, the slots before s. Every load is issued before the first
 // reduction (one memory latency, not five).
-__device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const HomeView &V, uint32_t s) {
+// w: on return, this lane's 64 slots of s's block (zeros past the map), for the caller's own use
+__device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const HomeView &V, uint32_t s, uint32_t (&w)[16]) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t b = s / SUMM_SLOTS, sb = b / SUPER_BLOCKS, bbase = b * SUMM_SLOTS;
     const uint32_t s0 = bbase + 64 * lane, bend = min(V.C, bbase + SUMM_SLOTS);
-    uint32_t w[16];
     if (s0 < bend) {
         const uint4 *p = reinterpret_cast<const uint4 *>(V.hc + s0 / 4);
 #pragma unroll
@@ -2820,6 +2961,10 @@ __device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const H
     x = summ_cat(x, wave_reduce_summ(x5));
     return x.m;
 }
+__device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const HomeView &V, uint32_t s) {
+    uint32_t w[16];
+    return wave_carry_into(V, s, w);
+}
 // first free slot at or after h given the carry into h, by one wave, 64 slots per step; -1 when
 // the run reaches slot C-1 (wraps) or is absurdly long
 __device__ __attribute__((always_inline)) inline int64_t wave_first_free(const HomeView &V, uint32_t h, int64_t carry_in) {
@@ -2851,7 +2996,11 @@ __device__ __attribute__((always_inline)) inline int64_t wave_first_free(const H
     }
     return -1;
 }
-// last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none)
+// first free slot at or after h (-1 as wave_first_free), by one wave: wave_first_free re-reads the
+// slots wave_carry_into has just read (L1 hits, not a second memory round trip)
+__device__ __attribute__((always_inline)) inline int64_t wave_free_from(const HomeView &V, uint32_t h) {
+    return wave_first_free(V, h, wave_carry_into(V, h));
+}
 // last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none); lo is a multiple
 // of 64 and hi - lo <= 4096: lane L owns slots lo + 64L .. +63, read once as four 16-B vectors
 __device__ __attribute__((always_inline)) inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int64_t carry_in) {
@@ -2917,52 +3066,56 @@ __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uin
 template <int NT = DECIDE_THREADS>
 __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
                                    MergeLog *log, int dyn) {
-    static_assert(NT >= 192 && NT % 64 == 0, "three carry waves");
-    __shared__ uint64_t s1[NT / 64], s2[NT / 64];
-    __shared__ uint32_t sh[NT / 64];
-    __shared__ long long s_c1, s_c0, s_cw, s_last, s_free;
-    uint64_t m1 = ~0ull, m2 = ~0ull;
-    uint32_t hmax = 0;
-    for (uint32_t i = threadIdx.x; i < len; i += NT) {
-        const uint64_t e = list[i];
-        if (e < m1) { m2 = m1; m1 = e; } else if (e < m2) m2 = e;
-        hmax = max(hmax, (uint32_t)(e >> 32));
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint64_t b1 = __shfl_xor(m1, off), b2 = __shfl_xor(m2, off);
-        min2_combine(m1, m2, b1, b2);
-        hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
-    }
-    if ((threadIdx.x & 63) == 0) { s1[threadIdx.x >> 6] = m1; s2[threadIdx.x >> 6] = m2; sh[threadIdx.x >> 6] = hmax; }
-    __syncthreads();
-    m1 = s1[0]; m2 = s2[0]; hmax = sh[0];
-    for (int k = 1; k < NT / 64; k++) { min2_combine(m1, m2, s1[k], s2[k]); hmax = max(hmax, sh[k]); }
-    const uint32_t h1 = (uint32_t)(m1 >> 32);
-    const uint32_t ws = V.C > 4096 ? V.C - 4096 : 0;
-    // three carries in parallel, one per wave
+    static_assert(NT >= 192 && NT % 64 == 0, "three waves");
+    // three waves at once, one barrier: wave 0 reduces the tied keys (the two smallest home << 32 |
+    // key, the largest home) and finds the end of the smallest home's run; wave 1 the carry into
+    // slot 0; wave 2 the last free slot of the map's last 4096 slots (where a run wrapping past
+    // slot C-1 would start)
+    __shared__ long long s_c0, s_last, s_free;
+    __shared__ uint64_t s_m1, s_m2;
+    __shared__ uint32_t s_hmax;
     const int w = threadIdx.x >> 6;
-    if (w == 0) { const int64_t c = wave_carry_into(V, h1); if ((threadIdx.x & 63) == 0) s_c1 = c; }
-    if (w == 1) { const int64_t c = wave_carry_into(V, 0); if ((threadIdx.x & 63) == 0) s_c0 = c; }
-    if (w == 2) { const int64_t c = ws ? wave_carry_into(V, ws) : 0; if ((threadIdx.x & 63) == 0) s_cw = c; }
-    __syncthreads();
-    // wave 0: end of h1's run; wave 2: the run wrapping past slot C-1 (if any) starts after the
-    // last free slot of [ws, C)
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ws = V.C > 4096 ? V.C - 4096 : 0;
     if (w == 0) {
-        const int64_t f = wave_first_free(V, h1, s_c1);
-        if ((threadIdx.x & 63) == 0) s_free = f;
-    }
-    if (w == 2) {
-        const int64_t lf = s_c0 > 0 ? wave_last_free(V, ws, V.C, ws ? s_cw : s_c0) : -2;
-        if ((threadIdx.x & 63) == 0) s_last = lf;
+        uint64_t m1 = ~0ull, m2 = ~0ull;
+        uint32_t hmax = 0;
+        for (uint32_t i = lane; i < len; i += 64) {
+            const uint64_t e = list[i];
+            if (e < m1) { m2 = m1; m1 = e; } else if (e < m2) m2 = e;
+            hmax = max(hmax, (uint32_t)(e >> 32));
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint64_t b1 = __shfl_xor(m1, off), b2 = __shfl_xor(m2, off);
+            min2_combine(m1, m2, b1, b2);
+            hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
+        }
+        const int64_t f = len ? wave_free_from(V, (uint32_t)(m1 >> 32)) : -1;
+        if (lane == 0) { s_free = f; s_m1 = m1; s_m2 = m2; s_hmax = hmax; }
+    } else if (w == 1) {
+        const int64_t c = wave_carry_into(V, 0);
+        if (lane == 0) s_c0 = c;
+    } else if (w == 2 && ws) {
+        const int64_t lf = wave_last_free(V, ws, V.C, wave_carry_into(V, ws));
+        if (lane == 0) s_last = lf;
     }
     __syncthreads();
+    if (!ws) {  // a map of at most 4096 slots: the last free slot needs the carry into slot 0
+        if (w == 2) {
+            const int64_t lf = s_c0 > 0 ? wave_last_free(V, 0, V.C, s_c0) : -2;
+            if (lane == 0) s_last = lf;
+        }
+        __syncthreads();
+    }
+    const uint64_t m1 = s_m1, m2 = s_m2;
+    const uint32_t hmax = s_hmax;
     if (threadIdx.x) return;
     uint32_t verdict = total > len ? 1u : 0u;
     const int64_t s = s_free;  // first free slot at or after h1
     if (s < 0) verdict = 1;     // the run of h1 wraps (or is absurdly long)
     if (m2 != ~0ull && s > (int64_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
-    const long long lf = s_last;
+    const long long lf = s_c0 > 0 ? s_last : -2;  // -2: no run wraps past slot C-1
     if (lf != -2 && (lf < 0 || (long long)hmax >= lf + 1)) verdict = 1;  // a tied pair may have wrapped
     st->tie_verdict = verdict;
     st->tie_winner = (uint32_t)m1;
@@ -3000,6 +3153,7 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
 constexpr int NEXT_THREADS = 512;  // launch bounds: 4 waves per SIMD (two workgroups per CU; the decision spills a little)
 constexpr int NEXT_CAND = 64;          // keys kept per argmax block at the block's max
 constexpr int NEXT_MAX_SEL = 1024;     // argmax blocks (the reducer keeps one LDS entry per block)
+constexpr int NEXT_TIE_LDS = 512;      // tied keys the decision reads from LDS (more: from N.tie_list)
 struct NextArgs {
     BeginArgs B;          // merge X + 1 (B.X < x_end)
     uint32_t x_end;       // vocab size: no merge starts at x_end
@@ -3057,8 +3211,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     __shared__ MaxRec sm[NEXT_THREADS / WAVE];
     __shared__ uint32_t s_flag, s_nc, s_h, s_tie, s_len, s_ntb, s_ovf;
     __shared__ uint32_t s_key[NEXT_CAND];
-    __shared__ uint32_t s_pc[NEXT_MAX_SEL], s_pt[NEXT_MAX_SEL];
+    __shared__ uint32_t s_pc[NEXT_MAX_SEL], s_pt[NEXT_MAX_SEL], s_pk[NEXT_MAX_SEL];
     const uint32_t tid = threadIdx.x;
+    __shared__ uint32_t s_pre[64];
+    roll_preload(st, delta, X, s_pre);
     if (N.prof && blockIdx.x == 0 && tid == 0) {
         const unsigned long long now = wall_clock64();
         st->sel_t0 = now;
@@ -3163,29 +3319,33 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         atomicAdd(&st->sel_prof[7], 1ull);
     }
     // ---- the last block: argmax, roll of merge X -------------------------------------------------
+    // the stream's last pair count (block 0 stored it write-through): in flight with the partials
+    const uint32_t lastpair_wt = tid == 0 && N.world == 1 ? ld_wt(N.lastpair) : NO_ID;
     MaxRec q{0, 0, NO_ID};
     for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
         const MaxRec p{ld_wt(&partial[b].cnt), ld_wt(&partial[b].ties), ld_wt(&partial[b].id)};
         s_pc[b] = p.cnt;
         s_pt[b] = p.ties;
+        s_pk[b] = ld_wt(N.pkey + b);  // (with the partial: no second round trip once the max is known)
         q = max_combine(q, p);
     }
     const MaxRec Q = block_max(q, sm);  // (its barriers also publish s_pc / s_pt)
     if (Q.ties == 1 && Q.cnt) {  // the unique max: its block kept its key
         for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS)
-            if (s_pc[b] == Q.cnt) s_key[0] = ld_wt(N.pkey + b);
+            if (s_pc[b] == Q.cnt) s_key[0] = s_pk[b];
     }
     __syncthreads();
     if (N.prof && tid == 0) sel_tick(st, 1, &pt);
     if (tid == 0) {
+        FinishOut fo;
         select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, Q.ties == 1 && Q.cnt ? s_key[0] : NO_ID,
-                      N.world == 1 ? ld_wt(N.lastpair) : NO_ID);
+                      lastpair_wt, &fo, s_pre, Q.ties > 1);
         s_h = HALT_DONE;
         s_tie = 0;
         if (N.B.X < N.x_end) {
             bool tie;
-            const uint32_t h = merge_begin_eval(T, st, N.B, &tie);
-            merge_begin_commit(st, N.B, h, tie);
+            const uint32_t h = merge_begin_eval_v(T, fo, N.B, &tie);
+            merge_begin_commit_v(st, N.B, h, tie, fo);
             s_h = h;
             s_tie = tie ? 1u : 0u;
         }
@@ -3194,8 +3354,13 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     }
     __syncthreads();
     if (N.prof && tid == 0) sel_tick(st, 2, &pt);
+    // the tied top pair's key, deferred by select_finish (stored on every way out below)
+    auto put_key = [&]() {
+        if (tid == 0 && Q.cnt && Q.ties > 1) st->top_key = T.id_key[Q.id];
+    };
     if (s_h || !s_tie) {
         if (N.prof && tid == 0) st->pp_t[7] = wall_clock64();
+        put_key();
         return;
     }
     // ---- merge X+1 ties: gather the keys of the blocks whose max is the top count ----------------
@@ -3209,9 +3374,14 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     __syncthreads();
     if (total > N.tie_cap) {  // the host path decides (replicated state: every rank takes it)
         if (tid == 0) { st->halt = HALT_TIE; st->halt_at = N.B.X; }
+        put_key();
         return;
     }
     const uint32_t cap_mask = N.V.C - 1;
+    // the tied keys go to LDS when they fit (the decision reads them there: no global store and
+    // reload between the gather and the decision), else to N.tie_list
+    __shared__ uint64_t s_tl[NEXT_TIE_LDS];
+    const uint64_t *tie_list = N.tie_list;
     if (s_ovf || s_len != total) {
         // a block held more tied keys than it kept (how the hot list spreads them depends on the
         // rank's id numbering): collect them from the whole hot list here, so every rank agrees
@@ -3261,16 +3431,20 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
             if (s_to[mid] <= e) lo = mid; else hi = mid;
         }
         const uint32_t key = ld_wt(N.cand + s_tb[lo] * NEXT_CAND + (e - s_to[lo]));
-        N.tie_list[e] = ((uint64_t)(zig_pair_hash(key) & cap_mask) << 32) | key;
+        const uint64_t ent = ((uint64_t)(zig_pair_hash(key) & cap_mask) << 32) | key;
+        if (total <= NEXT_TIE_LDS) s_tl[e] = ent;
+        else N.tie_list[e] = ent;
     }
+    if (total <= NEXT_TIE_LDS) tie_list = s_tl;
     if (tid == 0) st->tie_len = total;
     }
     // ---- merge X+1 ties: the Zig-order decision, by this block (the list and the refreshed home
     // summaries are this block's writes or were published before its ticket) -------------------------
     __syncthreads();
     if (N.prof && tid == 0) sel_tick(st, 3, &pt);
-    decide_body<NEXT_THREADS>(st, N.tie_list, total, total, N.V, N.B.log, 1);
+    decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); st->pp_t[7] = wall_clock64(); }
+    put_key();
 }
 
 // rebuild the home histogram for a new Zig capacity
