@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 AB=zig-bpe_amd/zbpe/ab
-timeout -k 10 900 python -u -m pytest tests/test_gpu.py tests/test_dist.py -x -q --timeout 200 --timeout-method thread -k "neighbour or arena or c1 or synth_goldens or random_corpora or encode or sharded or bench" > gpurun_out/gt.log 2>&1 || { tail -40 gpurun_out/gt.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu.py tests/test_dist.py -x -q --timeout 200 --timeout-method thread -k "tie or edge or neighbour or arena or c1 or synth_goldens or random_corpora or encode or sharded or bench" > gpurun_out/gt.log 2>&1 || { tail -40 gpurun_out/gt.log; exit 1; }
 tail -2 gpurun_out/gt.log
 ZBPE_LIB=$PWD/$AB/libzbpe_head.so timeout -k 10 150 python -u tools/ab_run.py --reps 2 --cfg "" > gpurun_out/ab_prev.jsonl 2> gpurun_out/ab_prev.err || exit 2
 timeout -k 10 150 python -u tools/ab_run.py --reps 2 --cfg "" > gpurun_out/ab_head.jsonl 2> gpurun_out/ab_head.err || exit 3

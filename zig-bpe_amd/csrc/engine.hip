@@ -935,6 +935,9 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                         "tie gather %.2f, decide %.2f; argmax blocks done %.2f, refresh blocks done %.2f\n",
                 P[7], P[0] * us / calls, P[1] * us / calls, P[2] * us / calls, P[3] * us / calls, P[4] * us / calls,
                 P[5] * us / calls, P[6] * us / calls);
+        const double nd = std::max(1.0, (double)P[8]);
+        fprintf(stderr, "sel_prof: %llu tie decisions; avg us per decision: gather %.2f, refresh wait %.2f, carries %.2f, "
+                        "decision total %.2f\n", P[8], P[3] * us / nd, P[10] * us / nd, P[9] * us / nd, P[4] * us / nd);
         static const char *bucket[3] = {"merges < 7936", "merges 7936-19743", "merges >= 19744"};
         for (int k = 0; k < 3; k++) {
             const unsigned long long *Q = h_st->pipe_prof[k];
@@ -994,6 +997,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         arena_used() + (uint64_t)K * top0 > arena_limit())
         CHECK(compact_train(X0));
     CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
+    // the refresh counts of zbpe_select_next: each launch zeroes the next one's, unless this batch
+    // does not continue the last one's launches
+    if (fused_select && !begun) HIP_OK(hipMemsetAsync(d_st->ref_ticket, 0, sizeof(d_st->ref_ticket), stream));
     if (dist()) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
     const uint64_t C = home_slots;
     const uint32_t nb = (uint32_t)((C + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;

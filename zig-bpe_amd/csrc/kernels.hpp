@@ -2911,7 +2911,42 @@ __device__ inline Summ wave_reduce_summ(Summ x) {
 // blocks before it in its super-block, the slots before s. Every load is issued before the first
 // reduction (one memory latency, not five).
 // w: on return, this lane's 64 slots of s's block (zeros past the map), for the caller's own use
-__device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const HomeView &V, uint32_t s, uint32_t (&w)[16]) {
+// this lane's 64 slots (16 words of 4 one-byte home counts) folded in two parts around relative
+// slot r: slots [0, r) into lo, slots (r, 64) into hi (r < 0: all in hi; r >= 64: all in lo).
+// 32-bit and branch-free: q from byte sums of masked words (v_sad_u8), m by one slot_fold chain in
+// slot order that hands its value to lo and restarts at r (no array of extracted bytes, which the
+// compiler would spill)
+__device__ __attribute__((always_inline)) inline void fold64_split(const uint32_t (&w)[16], int r, Summ &lo, Summ &hi) {
+    uint32_t klo = 0, khi = 0;
+    int32_t m = 0, mlo = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int nlo = min(max(r - 4 * j, 0), 4);          // bytes of word j before r
+        const int nhi = min(max(4 * j + 3 - r, 0), 4);      // bytes of word j after r
+        const uint32_t mask_lo = (uint32_t)((1ull << (8 * nlo)) - 1ull);
+        const uint32_t mask_hi = (uint32_t)(0xFFFFFFFF00000000ull >> (8 * nhi));
+        klo = __builtin_amdgcn_sad_u8(w[j] & mask_lo, 0u, klo);
+        khi = __builtin_amdgcn_sad_u8(w[j] & mask_hi, 0u, khi);
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int k = 4 * j + bb;
+            const int32_t t = max(0, m + (int32_t)((w[j] >> (8 * bb)) & 0xffu) - 1);
+            const bool at = k == r;
+            mlo = at ? m : mlo;
+            m = at ? 0 : t;
+        }
+    }
+    const int32_t clo = min(max(r, 0), 64), chi = min(max(63 - r, 0), 64);
+    if (r >= 64) mlo = m;
+    lo = Summ{(int32_t)klo - clo, mlo};
+    hi = Summ{(int32_t)khi - chi, r >= 64 ? 0 : m};
+}
+// carry into slot s = m of the composition over slots s+1 .. s-1 (circular), by one wave: the
+// slots after s in its block, the blocks after it in its super-block, the other super-blocks, the
+// blocks before it in its super-block, the slots before s. Every load is issued before the first
+// reduction (one memory latency, not five).
+// w: on return, this lane's 64 slots of s's block (zeros past the map), for the caller's own use
+__device__ __attribute__((always_inline)) inline int32_t wave_carry_into(const HomeView &V, uint32_t s, uint32_t (&w)[16]) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t b = s / SUMM_SLOTS, sb = b / SUPER_BLOCKS, bbase = b * SUMM_SLOTS;
     const uint32_t s0 = bbase + 64 * lane, bend = min(V.C, bbase + SUMM_SLOTS);
@@ -2945,12 +2980,16 @@ __device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const H
         for (uint32_t i = i0; i < i1; i++) x3 = summ_cat(x3, ld_wt(V.sup + (sb + 1 + i) % V.nsb));
     }
     Summ x1{0, 0}, x5{0, 0};
+    if (bend - bbase == SUMM_SLOTS) {  // a whole block (every map of >= 4096 slots)
+        fold64_split(w, (int)s - (int)s0, x5, x1);
+    } else {  // a map of fewer than 4096 slots: slots past it are not folded
 #pragma unroll
-    for (int k = 0; k < 64; k++) {
-        const uint32_t t = s0 + k;
-        const uint32_t e = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        if (t > s && t < bend) x1 = slot_fold(x1, e);
-        if (t < s) x5 = slot_fold(x5, e);
+        for (int k = 0; k < 64; k++) {
+            const uint32_t t = s0 + k;
+            const uint32_t e = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+            if (t > s && t < bend) x1 = slot_fold(x1, e);
+            if (t < s) x5 = slot_fold(x5, e);
+        }
     }
     const Summ x2 = (bi > b && bi < V.nb) ? bs : Summ{0, 0};
     const Summ x4 = bi < b ? bs : Summ{0, 0};
@@ -2961,21 +3000,21 @@ __device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const H
     x = summ_cat(x, wave_reduce_summ(x5));
     return x.m;
 }
-__device__ __attribute__((always_inline)) inline int64_t wave_carry_into(const HomeView &V, uint32_t s) {
+__device__ __attribute__((always_inline)) inline int32_t wave_carry_into(const HomeView &V, uint32_t s) {
     uint32_t w[16];
     return wave_carry_into(V, s, w);
 }
 // first free slot at or after h given the carry into h, by one wave, 64 slots per step; -1 when
 // the run reaches slot C-1 (wraps) or is absurdly long
-__device__ __attribute__((always_inline)) inline int64_t wave_first_free(const HomeView &V, uint32_t h, int64_t carry_in) {
+__device__ __attribute__((always_inline)) inline int64_t wave_first_free(const HomeView &V, uint32_t h, int32_t carry_in) {
     const uint32_t lane = threadIdx.x & 63;
-    int64_t c = carry_in;
+    int32_t c = carry_in;
     for (uint32_t base = h; base < V.C && base - h <= (1u << 20); base += 64) {
         const uint32_t s = base + lane;
         const bool valid = s < V.C;
-        const int64_t k = valid ? (int64_t)home_at(V.hc, s) : 0;
+        const uint32_t k = valid ? home_at(V.hc, s) : 0u;
         // carry into slot s: composition of the slots [base, s) applied to c (exclusive scan)
-        Summ inc = summ_slot((uint32_t)k);
+        Summ inc = summ_slot(k);
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             Summ y;
@@ -2987,11 +3026,11 @@ __device__ __attribute__((always_inline)) inline int64_t wave_first_free(const H
         ex.q = __shfl_up(inc.q, 1);
         ex.m = __shfl_up(inc.m, 1);
         if (lane == 0) ex = Summ{0, 0};
-        const int64_t cin = max((int64_t)ex.m, c + ex.q);
-        const uint64_t fr = __ballot(valid && cin + k == 0);
+        const int32_t cin = max(ex.m, c + ex.q);
+        const uint64_t fr = __ballot(valid && cin + (int32_t)k == 0);
         if (fr) return (int64_t)base + __builtin_ctzll(fr);
         if (base + 64 >= V.C) return -1;
-        const int64_t tq = __shfl(inc.q, 63), tm = __shfl(inc.m, 63);
+        const int32_t tq = __shfl(inc.q, 63), tm = __shfl(inc.m, 63);
         c = max(tm, c + tq);
     }
     return -1;
@@ -3003,7 +3042,7 @@ __device__ __attribute__((always_inline)) inline int64_t wave_free_from(const Ho
 }
 // last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none); lo is a multiple
 // of 64 and hi - lo <= 4096: lane L owns slots lo + 64L .. +63, read once as four 16-B vectors
-__device__ __attribute__((always_inline)) inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int64_t carry_in) {
+__device__ __attribute__((always_inline)) inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int32_t carry_in) {
     const uint32_t lane = threadIdx.x & 63, s0 = lo + 64 * lane;
     uint32_t w[16];
     const bool mine = s0 < hi;
@@ -3018,14 +3057,11 @@ __device__ __attribute__((always_inline)) inline int64_t wave_last_free(const Ho
 #pragma unroll
         for (int k = 0; k < 16; k++) w[k] = 0;
     }
-    Summ x{0, 0};
-    if (s0 + 64 <= hi) {
-        x = fold64(w);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 64; k++)
-            if (s0 + k < hi) x = slot_fold(x, ((w[k >> 2] >> (8 * (k & 3))) & 0xffu));
-    }
+    // slots of this lane inside [lo, hi): all 64, none, or (a map of < 64 slots) a prefix
+    const int nin = (int)min(64u, hi > s0 ? hi - s0 : 0u);
+    Summ x{0, 0}, unused;
+    if (nin == 64) x = fold64(w);
+    else if (nin > 0) fold64_split(w, nin, x, unused);
     // exclusive ordered scan over lanes
     Summ inc = x;
 #pragma unroll
@@ -3039,19 +3075,28 @@ __device__ __attribute__((always_inline)) inline int64_t wave_last_free(const Ho
     ex.q = __shfl_up(inc.q, 1);
     ex.m = __shfl_up(inc.m, 1);
     if (lane == 0) ex = Summ{0, 0};
-    int64_t c = max((int64_t)ex.m, carry_in + ex.q);
-    long long last = -1;
+    int32_t c = max(ex.m, carry_in + ex.q);
+    int32_t last = -1;
 #pragma unroll
-    for (int k = 0; k < 64; k++) {
-        if (s0 + k < hi) {
-            const int64_t kk = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-            if (c + kk == 0) last = s0 + k;
-            else c = c + kk - 1;
+    for (int j = 0; j < 16; j++) {
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int k = 4 * j + bb;
+            const int32_t t = c + (int32_t)((w[j] >> (8 * bb)) & 0xffu);
+            const bool ok = k < nin;
+            last = ok && t == 0 ? (int32_t)(s0 + k) : last;
+            c = ok ? max(0, t - 1) : c;
         }
     }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) last = max(last, (long long)__shfl_xor(last, off));
+    for (int off = 32; off >= 1; off >>= 1) last = max(last, __shfl_xor(last, off));
     return last;
+}
+// sel_prof: add the ticks since *t to st->sel_prof[k] (one thread; fire-and-forget atomic)
+__device__ inline void sel_tick(DevState *st, int k, unsigned long long *t) {
+    const unsigned long long now = wall_clock64();
+    atomicAdd(&st->sel_prof[k], now - *t);
+    *t = now;
 }
 constexpr int DECIDE_THREADS = 256;
 // two smallest of two (smallest, second smallest) pairs
@@ -3065,7 +3110,7 @@ __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uin
 // (halt / commit).
 template <int NT = DECIDE_THREADS>
 __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
-                                   MergeLog *log, int dyn) {
+                                   MergeLog *log, int dyn, unsigned long long *prof_t = nullptr) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
     // three waves at once, one barrier: wave 0 reduces the tied keys (the two smallest home << 32 |
     // key, the largest home) and finds the end of the smallest home's run; wave 1 the carry into
@@ -3111,6 +3156,7 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
     const uint64_t m1 = s_m1, m2 = s_m2;
     const uint32_t hmax = s_hmax;
     if (threadIdx.x) return;
+    if (prof_t) sel_tick(st, 9, prof_t);  // the three waves' carries
     uint32_t verdict = total > len ? 1u : 0u;
     const int64_t s = s_free;  // first free slot at or after h1
     if (s < 0) verdict = 1;     // the run of h1 wraps (or is absurdly long)
@@ -3168,12 +3214,6 @@ struct NextArgs {
     int world;
     int prof;             // option sel_prof: accumulate phase times into st->sel_prof
 };
-// sel_prof: add the ticks since *t to st->sel_prof[k] (one thread; fire-and-forget atomic)
-__device__ inline void sel_tick(DevState *st, int k, unsigned long long *t) {
-    const unsigned long long now = wall_clock64();
-    atomicAdd(&st->sel_prof[k], now - *t);
-    *t = now;
-}
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
 // relaxed atomic stores) and is drained here, so no release fence (an L2 writeback, 1.7-6.5 us on
@@ -3206,16 +3246,28 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     // blocks [0, nref) refresh the home super-blocks (the longest role: dispatched first, one
     // workgroup per CU at this kernel's VGPR count), blocks [nref, nref + sel_blocks) run the argmax
     const uint32_t nref = N.V.C ? N.V.nsb : 0u;
-    const uint64_t rbits = blockIdx.x < nref ? home_dirty_bits(T, blockIdx.x) : 0ull;  // in flight with the halt load
+    const uint32_t tid = threadIdx.x;
+    if (blockIdx.x < nref) {
+        // refresh role, off the argmax's ticket: the last argmax block reduces, rolls and starts
+        // merge X+1 while these blocks work, and waits for their count (ref_ticket) only before a
+        // tie decision. They run even after a halt (a halted batch dirties no blocks; a refresh is
+        // always valid), so that every launch's count reaches nref.
+        refresh_super(T, blockIdx.x, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), true,
+                      home_dirty_bits(T, blockIdx.x));
+        if (N.prof && tid == 0) atomicMax(&st->sel_tr, (unsigned long long)wall_clock64());
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through summaries drained
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(&st->ref_ticket[X & 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (st->halt) return;
     __shared__ MaxRec sm[NEXT_THREADS / WAVE];
     __shared__ uint32_t s_flag, s_nc, s_h, s_tie, s_len, s_ntb, s_ovf;
     __shared__ uint32_t s_key[NEXT_CAND];
     __shared__ uint32_t s_pc[NEXT_MAX_SEL], s_pt[NEXT_MAX_SEL], s_pk[NEXT_MAX_SEL];
-    const uint32_t tid = threadIdx.x;
     __shared__ uint32_t s_pre[64];
     roll_preload(st, delta, X, s_pre);
-    if (N.prof && blockIdx.x == 0 && tid == 0) {
+    if (N.prof && blockIdx.x == nref && tid == 0) {  // the first argmax block
         const unsigned long long now = wall_clock64();
         st->sel_t0 = now;
         if (st->pp_t[5]) {  // the replace launch: its work span, its start -> this select's start, its phases
@@ -3232,7 +3284,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         }
     }
     const uint32_t bx = blockIdx.x - nref;  // argmax block index
-    if (blockIdx.x >= nref) {
+    {
         const uint32_t G = N.sel_blocks * NEXT_THREADS;
         for (uint32_t t = bx * NEXT_THREADS + tid; t < 2 * X; t += G) delta[t] = 0;
         const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
@@ -3302,19 +3354,20 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
             // the key of a block's unique max
             __hip_atomic_store(&N.pkey[bx], s_nc == 1 ? s_key[0] : NO_ID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-    } else if (N.V.C) {
-        refresh_super(T, blockIdx.x, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), true, rbits);
     }
-    if (N.prof && tid == 0) atomicMax(blockIdx.x >= nref ? &st->sel_ta : &st->sel_tr, (unsigned long long)wall_clock64());
-    if (!block_ticket_last(&st->ticket, gridDim.x, &s_flag)) return;
+    if (N.prof && tid == 0) atomicMax(&st->sel_ta, (unsigned long long)wall_clock64());
+    if (!block_ticket_last(&st->ticket, N.sel_blocks, &s_flag)) return;
+    // the next launch's refresh count (the launch before this one used it and has ended)
+    if (tid == 0) __hip_atomic_store(&st->ref_ticket[(X + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long pt = 0;
     if (N.prof && tid == 0) {
         pt = st->sel_t0;
         const unsigned long long ta = __hip_atomic_load(&st->sel_ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long tr = __hip_atomic_load(&st->sel_tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         atomicAdd(&st->sel_prof[5], ta - pt);
-        if (tr) atomicAdd(&st->sel_prof[6], tr - pt);
-        st->sel_ta = st->sel_tr = 0;
+        // refresh blocks that finished before this point (the rest run on; stale stamps are < pt)
+        if (tr > pt) atomicAdd(&st->sel_prof[6], tr - pt);
+        st->sel_ta = 0;
         sel_tick(st, 0, &pt);
         atomicAdd(&st->sel_prof[7], 1ull);
     }
@@ -3438,12 +3491,19 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     if (total <= NEXT_TIE_LDS) tie_list = s_tl;
     if (tid == 0) st->tie_len = total;
     }
-    // ---- merge X+1 ties: the Zig-order decision, by this block (the list and the refreshed home
-    // summaries are this block's writes or were published before its ticket) -------------------------
-    __syncthreads();
+    // ---- merge X+1 ties: the Zig-order decision, by this block (the list is this block's writes;
+    // the refreshed home summaries were stored write-through and drained before each refresh
+    // block's count: wait for all nref, then read them with sc1 loads) --------------------------------
     if (N.prof && tid == 0) sel_tick(st, 3, &pt);
-    decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1);
-    if (N.prof && tid == 0) { sel_tick(st, 4, &pt); st->pp_t[7] = wall_clock64(); }
+    if (nref && tid == 0) {
+        // every refresh block is resident or done (they never wait), so this ends
+        while (__hip_atomic_load(&st->ref_ticket[X & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nref)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+    if (N.prof && tid == 0) sel_tick(st, 10, &pt);
+    decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr);
+    if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }
 

@@ -67,12 +67,15 @@ struct DevState {
     uint32_t lists_x;        // tokens < lists_x existed when the lists were built (their entries carry neighbours)
     // option sel_prof: zbpe_select_next phase times (wall_clock64 ticks, summed over merges)
     unsigned long long sel_t0, sel_ta, sel_tr;  // start; latest argmax / refresh block finish
-    unsigned long long sel_prof[8];
+    unsigned long long sel_prof[12];  // [8] tie decisions, [9] their carries, [10] refresh wait
     // option sel_prof, whole merge pipeline (batch mode): probe stamps of the current launches and the
     // sums they fold into (Engine::train prints them): scan (list form) LDS clear / walk / flush done and
     // the next kernel's start, replace work span and the select's start, select end -> scan start
     unsigned long long pp_t[16];  // [8..12]: replace phases (update blocks: deltas in, gathered, reserved, table done; apply done)
     unsigned long long pipe_prof[3][16];  // by merge: [256, 8192), [8192, 20000), [20000, ...)
+    // zbpe_select_next of merge X: home-refresh workgroups done, counted in [X & 1] (the select of
+    // X - 1 zeroes [X & 1]; the host zeroes both before a batch that does not continue one)
+    uint32_t ref_ticket[2];
 };
 // why a device-resident batch stopped (the host finishes that merge on the synchronous path)
 enum HaltReason : uint32_t {
