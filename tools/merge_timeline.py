@@ -1,0 +1,102 @@
+"""Per-merge kernel timeline of a production C4 train (no events, no probes) from a rocprofv3 kernel trace.
+
+  rocprofv3 --kernel-trace --output-format csv -d D -o run -- python3 tools/merge_timeline.py --run L.json
+  python3 tools/merge_timeline.py --analyse D L.json
+
+--run trains C4 twice (warm-up, then the measured train) and writes the measured train's scan log (one
+entry per pair-scan launch: 2 x merge index + form, -1 = no-op) and device merge log (ties per merge).
+--analyse matches the trace's last pair-scan launches to the scan log; each batch merge's scan is
+followed by its zbpe_replace and zbpe_select_next (which starts merge X+1: its duration depends on
+whether merge X+1 is a tie). Reports, per merge-index bucket: average scan / replace / select
+durations and the gaps between them, with the select split by whether the next merge is tied.
+"""
+import argparse
+import bisect
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(out, opts):
+    sys.path.insert(0, os.path.join(ROOT, "zig-bpe_amd"))
+    import zbpe
+
+    e = zbpe.Engine(0)
+    e.upload(zbpe.synth_corpus("words_utf8", 0x5EED0004, 1 << 30, threads=16))
+    for kv in opts:
+        k, v = kv.split("=")
+        e.set_option(k, int(v))
+    e.train_resident(32000)
+    m, c, st = e.train_resident(32000)
+    log = e.merge_log()
+    json.dump({"scan_log": e.scan_log().tolist(), "ties": log[:, 3].tolist(), "count": log[:, 1].tolist()},
+              open(out, "w"))
+    print(f"{len(m)} merges, {st.total_s:.3f} s")
+    e.close()
+
+
+def analyse(d, logp):
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        sys.exit(f"no kernel trace under {d}")
+    ks = []
+    for p in files:
+        with open(p) as f:
+            for r in csv.DictReader(f):
+                ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "")))
+    ks.sort()
+    L = json.load(open(logp))
+    slog, ties = L["scan_log"], L["ties"]
+    scans = [i for i, k in enumerate(ks) if "zbpe_scan_pairs_t" in k[2]]
+    if len(scans) < len(slog):
+        sys.exit(f"{len(scans)} scans in the trace, {len(slog)} in the log")
+    scans = scans[len(scans) - len(slog):]
+    buckets = [(0, 2000), (2000, 8000), (8000, 20000), (20000, 1 << 30)]
+    acc = {b: {} for b in buckets}
+
+    def add(b, k, v):
+        a = acc[b].setdefault(k, [0.0, 0])
+        a[0] += v
+        a[1] += 1
+
+    for j, x in enumerate(slog):
+        if x < 0:
+            continue
+        mi, form = x >> 1, x & 1
+        i = scans[j]
+        if i + 3 >= len(ks):
+            continue
+        s, r, sel, nxt = ks[i], ks[i + 1], ks[i + 2], ks[i + 3]
+        if "zbpe_replace" not in r[2] or "zbpe_select_next" not in sel[2]:
+            continue
+        b = next(bb for bb in buckets if bb[0] <= mi < bb[1])
+        add(b, "scan_" + ("list" if form else "stream"), (s[1] - s[0]) / 1e3)
+        add(b, "gap_scan_replace", (r[0] - s[1]) / 1e3)
+        add(b, "replace", (r[1] - r[0]) / 1e3)
+        add(b, "gap_replace_select", (sel[0] - r[1]) / 1e3)
+        nt = mi + 1 < len(ties) and ties[mi + 1] > 1
+        add(b, "select_next_tied" if nt else "select_next_untied", (sel[1] - sel[0]) / 1e3)
+        if "zbpe_scan_pairs_t" in nxt[2]:
+            add(b, "gap_select_scan", (nxt[0] - sel[1]) / 1e3)
+            add(b, "merge_total", (nxt[0] - s[0]) / 1e3)
+    out = {}
+    for b in buckets:
+        out[f"merges [{b[0]}, {b[1] if b[1] < 1 << 30 else 'end'})"] = {
+            k: {"avg_us": round(v[0] / v[1], 2), "n": v[1]} for k, v in sorted(acc[b].items())}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--run", default="")
+    p.add_argument("--analyse", nargs=2, default=None)
+    p.add_argument("--opt", action="append", default=[], help="engine option k=v")
+    a = p.parse_args()
+    if a.run:
+        run(a.run, a.opt)
+    if a.analyse:
+        analyse(*a.analyse)

@@ -56,7 +56,7 @@ void Engine::release() {
     f(T.ht); f(T.id_key); f(T.id_cnt);
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
-    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_sizes);
+    f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_cs); f(d_rtk); f(d_sizes);
     f(d_enc_cnt); f(d_enc_ctr); f(d_nb);
     d_nb = nullptr; nb_cap = 0;
     d_enc_cnt = nullptr; d_enc_ctr = nullptr; enc_cnt_cap = enc_ctr_cap = 0;
@@ -72,7 +72,7 @@ void Engine::release() {
     if (h_bnd) (void)hipHostFree(h_bnd);
     h_bnd = nullptr;
     comm.reset();
-    d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr; d_cand = nullptr; d_sizes = nullptr; sizes_cap = 0;
+    d_tile_cnt = nullptr; d_tile_off = nullptr; d_tile_fn = d_carry = nullptr; d_bitmap = nullptr; d_cand = nullptr; d_cs = nullptr; d_rtk = nullptr; cs_cap = 0; d_sizes = nullptr; sizes_cap = 0;
     d_tie_list = nullptr; d_first = nullptr; d_gather = nullptr; d_recount = nullptr; h_st = nullptr; stream = nullptr;
     d_summ = nullptr; d_count_hist = nullptr; h_count_hist = nullptr; hot_cap_alloc = home_words_cap = 0; home_slots = 0;
     dirty_bits_cap = 0; d_sup = nullptr; sup_cap = 0; d_pres = nullptr; pres_cap = 0;
@@ -104,6 +104,7 @@ zbpe_status Engine::init(int dev) {
     for (auto &e : bev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no L2 writeback
     HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
     HIP_OK(hipMalloc(&d_cand, ((size_t)NEXT_MAX_SEL * (NEXT_CAND + 1) + 64) * sizeof(uint32_t)));  // keys | pkey | lastpair
+    HIP_OK(hipMalloc(&d_rtk, RTK_WORDS * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_count_hist, COUNT_BINS * sizeof(uint32_t)));
     HIP_OK(hipHostMalloc((void **)&h_count_hist, COUNT_BINS * sizeof(uint32_t), hipHostMallocDefault));
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
@@ -937,7 +938,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                 P[5] * us / calls, P[6] * us / calls);
         const double nd = std::max(1.0, (double)P[8]);
         fprintf(stderr, "sel_prof: %llu tie decisions; avg us per decision: gather %.2f, refresh wait %.2f, carries %.2f, "
-                        "decision total %.2f\n", P[8], P[3] * us / nd, P[10] * us / nd, P[9] * us / nd, P[4] * us / nd);
+                        "decision total %.2f; refresh prefix start %.2f, end %.2f (from the first argmax block's start)\n", P[8],
+                P[3] * us / nd, P[10] * us / nd, P[9] * us / nd, P[4] * us / nd, P[6] * us / nd, P[11] * us / nd);
         static const char *bucket[3] = {"merges < 7936", "merges 7936-19743", "merges >= 19744"};
         for (int k = 0; k < 3; k++) {
             const unsigned long long *Q = h_st->pipe_prof[k];
@@ -999,11 +1001,17 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
     // the refresh counts of zbpe_select_next: each launch zeroes the next one's, unless this batch
     // does not continue the last one's launches
-    if (fused_select && !begun) HIP_OK(hipMemsetAsync(d_st->ref_ticket, 0, sizeof(d_st->ref_ticket), stream));
+    if (fused_select && !begun) HIP_OK(hipMemsetAsync(d_rtk, 0, RTK_WORDS * sizeof(uint32_t), stream));
     if (dist()) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
     const uint64_t C = home_slots;
     const uint32_t nb = (uint32_t)((C + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
     const HomeView V{T.home_cnt, d_summ, d_sup, (uint32_t)C, nb, nsb};
+    // the tie decision's carries, precomputed by the select's last refresh workgroup (one thread per super-block)
+    uint32_t *cs = nullptr;
+    if (C && fused_select && refresh_prefix && nsb <= (uint32_t)NEXT_THREADS) {
+        CHECK(ensure(&d_cs, cs_cap, nsb + 1, "home carries"));
+        cs = d_cs;
+    }
     const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top0 / 256 + 1);
     const int64_t slots = n_slots;
     const double t0 = now_s();
@@ -1066,7 +1074,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
-                       dist() ? world : 1, (int)sel_prof};
+                       dist() ? world : 1, (int)sel_prof, cs, d_rtk};
             zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, left, X, N);
             LAUNCH_OK();
         } else {

@@ -147,8 +147,12 @@ struct Engine {
     double merge_weight() const { return timing_full && !lists_at_batch ? 1.0 : (double)merge_timing; }
     bool replace_split = false;     // profiling: apply and count update as separate launches
     bool fused_select = true;       // zbpe_select_next: the select of merge X also starts merge X+1 (ties included)
+    bool refresh_prefix = true;     // zbpe_select_next: the last refresh workgroup precomputes the tie decision's carries
     bool begun = false;             // the next batch's first merge was started by the last batch's final select
     uint32_t *d_cand = nullptr;     // zbpe_select_next: keys at each argmax block's max
+    uint32_t *d_cs = nullptr;       // zbpe_select_next: carries into the home super-blocks (refresh_prefix)
+    size_t cs_cap = 0;
+    uint32_t *d_rtk = nullptr;      // zbpe_select_next: refresh arrival counters (RTK_WORDS)
     MergeLog *d_log = nullptr;
     std::vector<MergeLog> h_log;
     Halo *d_halo = nullptr;

@@ -3042,11 +3042,10 @@ __device__ __attribute__((always_inline)) inline int64_t wave_free_from(const Ho
 }
 // last free slot in [lo, hi) given the carry into lo, by one wave (-1 if none); lo is a multiple
 // of 64 and hi - lo <= 4096: lane L owns slots lo + 64L .. +63, read once as four 16-B vectors
-__device__ __attribute__((always_inline)) inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int32_t carry_in) {
+// this lane's 64 slots lo + 64L .. +63 of [lo, hi) as 16 words (zeros past hi's lane)
+__device__ __attribute__((always_inline)) inline void wave_load_slots(const HomeView &V, uint32_t lo, uint32_t hi, uint32_t (&w)[16]) {
     const uint32_t lane = threadIdx.x & 63, s0 = lo + 64 * lane;
-    uint32_t w[16];
-    const bool mine = s0 < hi;
-    if (mine) {
+    if (s0 < hi) {
         const uint4 *p = reinterpret_cast<const uint4 *>(V.hc + s0 / 4);
 #pragma unroll
         for (int v = 0; v < 4; v++) {
@@ -3057,6 +3056,16 @@ __device__ __attribute__((always_inline)) inline int64_t wave_last_free(const Ho
 #pragma unroll
         for (int k = 0; k < 16; k++) w[k] = 0;
     }
+}
+__device__ __attribute__((always_inline)) inline int64_t wave_last_free_w(const uint32_t (&w)[16], uint32_t lo, uint32_t hi, int32_t carry_in);
+__device__ __attribute__((always_inline)) inline int64_t wave_last_free(const HomeView &V, uint32_t lo, uint32_t hi, int32_t carry_in) {
+    uint32_t w[16];
+    wave_load_slots(V, lo, hi, w);
+    return wave_last_free_w(w, lo, hi, carry_in);
+}
+// wave_last_free on slots already loaded (wave_load_slots)
+__device__ __attribute__((always_inline)) inline int64_t wave_last_free_w(const uint32_t (&w)[16], uint32_t lo, uint32_t hi, int32_t carry_in) {
+    const uint32_t lane = threadIdx.x & 63, s0 = lo + 64 * lane;
     // slots of this lane inside [lo, hi): all 64, none, or (a map of < 64 slots) a prefix
     const int nin = (int)min(64u, hi > s0 ? hi - s0 : 0u);
     Summ x{0, 0}, unused;
@@ -3098,6 +3107,88 @@ __device__ inline void sel_tick(DevState *st, int k, unsigned long long *t) {
     atomicAdd(&st->sel_prof[k], now - *t);
     *t = now;
 }
+// carry into slot s from the carry into its super-block, cs[s / 2^18] (refresh_prefix): the
+// blocks before s's block in its super-block, then the slots before s in its block; one load round
+// trip, two wave reductions. The lanes also load the 64 slots after s (wave_first_free re-reads
+// them from L1).
+__device__ __attribute__((always_inline)) inline int32_t wave_carry_from_super(const HomeView &V, const uint32_t *cs, uint32_t s) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t b = s / SUMM_SLOTS, sb = b / SUPER_BLOCKS, s0 = b * SUMM_SLOTS + 64 * lane;
+    uint32_t w[16];
+    if (s0 < s + 64) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(V.hc + s0 / 4);
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const uint4 q = p[v];
+            w[4 * v] = q.x; w[4 * v + 1] = q.y; w[4 * v + 2] = q.z; w[4 * v + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = 0;
+    }
+    const uint32_t bi = sb * SUPER_BLOCKS + lane;
+    const Summ bs = bi < b ? ld_wt(V.summ + bi) : Summ{0, 0};
+    const int32_t c_in = (int32_t)ld_wt(cs + sb);
+    // slots [s0, s) of this lane: all 64 below s, a prefix in s's lane, none above (identity)
+    const int r = (int)min((int64_t)s - (int64_t)s0, (int64_t)64);
+    Summ xs, unused;
+    fold64_split(w, r, xs, unused);
+    const Summ x = summ_cat(wave_reduce_summ(bs), wave_reduce_summ(xs));
+    return max(x.m, c_in + x.q);
+}
+__device__ inline void st_wt(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// by the last home-refresh workgroup of a zbpe_select_next launch (every summary fresh), for the
+// launch's tie decision: cs[k] = the carry into super-block k's first slot (cs[0] = the carry into
+// slot 0), cs[nsb] = the last free slot of the map's last 4096 slots given the carry into them, or
+// -2 when no run wraps past slot C-1 (cs[0] == 0). Needs nsb <= blockDim.x. Write-through stores.
+__device__ inline void refresh_prefix(const HomeView &V, uint32_t *cs) {
+    constexpr int MAXW = 16;
+    __shared__ Summ s_tot[MAXW];
+    __shared__ int32_t s_c0, s_clast;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // every load up front: the super summaries (all threads); the carry into slot 0 (wave 0); the
+    // wrap test's last block and the block summaries before it in the last super-block (wave 1)
+    const Summ S = tid < V.nsb ? ld_wt(V.sup + tid) : Summ{0, 0};
+    const uint32_t kl = V.nsb - 1, ws = V.nb > 1 ? V.C - SUMM_SLOTS : 0u;
+    uint32_t hw[16];
+    Summ xl{0, 0};
+    if (w == 1) {
+        const uint32_t bi = kl * SUPER_BLOCKS + lane;
+        const Summ bl = V.nb > 1 && bi < V.nb - 1 ? ld_wt(V.summ + bi) : Summ{0, 0};
+        wave_load_slots(V, ws, V.C, hw);
+        xl = wave_reduce_summ(bl);
+    } else if (w == 0) {
+        const int32_t c = wave_carry_into(V, 0u);
+        if (lane == 0) s_c0 = c;
+    }
+    Summ inc = S;  // inclusive ordered scan over the wave's super-blocks
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        Summ y;
+        y.q = __shfl_up(inc.q, off);
+        y.m = __shfl_up(inc.m, off);
+        if ((int)lane >= off) inc = summ_cat(y, inc);
+    }
+    if (lane == 63) s_tot[w] = inc;
+    __syncthreads();
+    Summ pre{0, 0};
+    for (uint32_t k = 0; k < w; k++) pre = summ_cat(pre, s_tot[k]);
+    Summ ex;
+    ex.q = __shfl_up(inc.q, 1);
+    ex.m = __shfl_up(inc.m, 1);
+    if (lane == 0) ex = Summ{0, 0};
+    const Summ E = summ_cat(pre, ex);  // super-blocks [0, tid)
+    const int32_t c0 = s_c0;
+    const int32_t cin = max(E.m, c0 + E.q);
+    if (tid < V.nsb) st_wt(cs + tid, (uint32_t)cin);
+    if (tid == kl) s_clast = cin;
+    __syncthreads();
+    if (w == 1) {  // the carry into ws = C - 4096 (the last block), then the last free slot of [ws, C)
+        const int32_t cw = V.nb > 1 ? max(xl.m, s_clast + xl.q) : c0;
+        const int32_t lf = c0 > 0 ? (int32_t)wave_last_free_w(hw, ws, V.C, cw) : -2;
+        if (lane == 0) st_wt(cs + V.nsb, (uint32_t)lf);
+    }
+}
 constexpr int DECIDE_THREADS = 256;
 // two smallest of two (smallest, second smallest) pairs
 __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uint64_t b2) {
@@ -3110,7 +3201,8 @@ __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uin
 // (halt / commit).
 template <int NT = DECIDE_THREADS>
 __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
-                                   MergeLog *log, int dyn, unsigned long long *prof_t = nullptr) {
+                                   MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
+                                   const uint32_t *cs = nullptr) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
     // three waves at once, one barrier: wave 0 reduces the tied keys (the two smallest home << 32 |
     // key, the largest home) and finds the end of the smallest home's run; wave 1 the carry into
@@ -3136,8 +3228,14 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
             min2_combine(m1, m2, b1, b2);
             hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
         }
-        const int64_t f = len ? wave_free_from(V, (uint32_t)(m1 >> 32)) : -1;
+        const uint32_t h1 = (uint32_t)(m1 >> 32);
+        const int64_t f = !len ? -1 : cs ? wave_first_free(V, h1, wave_carry_from_super(V, cs, h1)) : wave_free_from(V, h1);
         if (lane == 0) { s_free = f; s_m1 = m1; s_m2 = m2; s_hmax = hmax; }
+    } else if (cs) {  // carry into slot 0 and the wrap test's last free slot: precomputed (refresh_prefix)
+        if (w == 1 && lane == 0) {
+            s_c0 = (int32_t)ld_wt(cs);
+            s_last = (int32_t)ld_wt(cs + V.nsb);
+        }
     } else if (w == 1) {
         const int64_t c = wave_carry_into(V, 0);
         if (lane == 0) s_c0 = c;
@@ -3146,7 +3244,7 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
         if (lane == 0) s_last = lf;
     }
     __syncthreads();
-    if (!ws) {  // a map of at most 4096 slots: the last free slot needs the carry into slot 0
+    if (!ws && !cs) {  // a map of at most 4096 slots: the last free slot needs the carry into slot 0
         if (w == 2) {
             const int64_t lf = s_c0 > 0 ? wave_last_free(V, 0, V.C, s_c0) : -2;
             if (lane == 0) s_last = lf;
@@ -3213,6 +3311,8 @@ struct NextArgs {
     const Boundary *bnd;  // multi-GPU: boundary records (the stream's last pair on ties)
     int world;
     int prof;             // option sel_prof: accumulate phase times into st->sel_prof
+    uint32_t *cs;         // [nsb + 1] refresh_prefix's carries (nullptr: the decision computes them; nsb > NEXT_THREADS)
+    uint32_t *rtk;        // [RTK_WORDS] refresh arrival counters
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -3227,6 +3327,22 @@ __device__ inline bool block_ticket_last(uint32_t *ticket, uint32_t nblocks, uin
     if (threadIdx.x == 0) {
         const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *s_flag = t == nblocks - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+// block_ticket_last for many arrivals: workgroups [0, nblocks) count on eight per-XCD counters
+// (workgroup i in i % 8: the dispatcher's XCD round robin), the last of each group on the top one
+// (ctr: RTK_SET words; a single counter saturates at ~11-13 ns per arrival, MI355X_MICROARCH.md fanin)
+__device__ inline bool block_ticket_last_x(uint32_t *ctr, uint32_t nblocks, uint32_t *s_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t g = blockIdx.x & 7, gsize = (nblocks - g + 7) / 8, ngroups = min(nblocks, 8u);
+        uint32_t last = 0;
+        if (__hip_atomic_fetch_add(ctr + g * RTK_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1)
+            last = __hip_atomic_fetch_add(ctr + 8 * RTK_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
+        *s_flag = last;
     }
     __syncthreads();
     return *s_flag != 0;
@@ -3249,15 +3365,36 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     const uint32_t tid = threadIdx.x;
     if (blockIdx.x < nref) {
         // refresh role, off the argmax's ticket: the last argmax block reduces, rolls and starts
-        // merge X+1 while these blocks work, and waits for their count (ref_ticket) only before a
-        // tie decision. They run even after a halt (a halted batch dirties no blocks; a refresh is
-        // always valid), so that every launch's count reaches nref.
+        // merge X+1 while these blocks work, and waits for their arrivals only before a tie
+        // decision. They run even after a halt (a halted batch dirties no blocks; a refresh is
+        // always valid), so that every launch's arrivals reach nref.
+        // pfx: the decision's carries are precomputed when merge X was tied (ties come in streaks: the
+        // last quarter of C4 is 94 % tied), a predicate the decision reads alike (merge X's log entry,
+        // written by the launch before); then the last workgroup to arrive is elected (returning
+        // atomics, per-XCD counters, then the top one) and arrives once more when done. Else a
+        // workgroup's arrival is one non-returning add to its XCD's counter.
+        const bool pfx = N.cs && N.B.log[X - 256].ties > 1;
         refresh_super(T, blockIdx.x, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), true,
                       home_dirty_bits(T, blockIdx.x));
         if (N.prof && tid == 0) atomicMax(&st->sel_tr, (unsigned long long)wall_clock64());
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through summaries drained
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(&st->ref_ticket[X & 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __shared__ uint32_t s_rlast;
+        uint32_t *rtk = N.rtk + (X & 1) * RTK_SET;
+        if (!pfx) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through summaries drained
+            __syncthreads();
+            if (tid == 0) __hip_atomic_fetch_add(rtk + (blockIdx.x & 7) * RTK_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        if (block_ticket_last_x(rtk, nref, &s_rlast) && ld_wt(&st->ref_noprefix) != X) {
+            if (N.prof && tid == 0)
+                __hip_atomic_store(&st->sel_prof_pq, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            refresh_prefix(N.V, N.cs);
+            if (N.prof && tid == 0)
+                __hip_atomic_store(&st->sel_prof_pp, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_fetch_add(rtk + 8 * RTK_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         return;
     }
     if (st->halt) return;
@@ -3357,8 +3494,9 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     }
     if (N.prof && tid == 0) atomicMax(&st->sel_ta, (unsigned long long)wall_clock64());
     if (!block_ticket_last(&st->ticket, N.sel_blocks, &s_flag)) return;
+    const bool pfx = nref && N.cs && N.B.log[X - 256].ties > 1;  // the refresh precomputes the carries (its predicate)
     // the next launch's refresh count (the launch before this one used it and has ended)
-    if (tid == 0) __hip_atomic_store(&st->ref_ticket[(X + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 9) st_wt(N.rtk + ((X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
     unsigned long long pt = 0;
     if (N.prof && tid == 0) {
         pt = st->sel_t0;
@@ -3366,7 +3504,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         const unsigned long long tr = __hip_atomic_load(&st->sel_tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         atomicAdd(&st->sel_prof[5], ta - pt);
         // refresh blocks that finished before this point (the rest run on; stale stamps are < pt)
-        if (tr > pt) atomicAdd(&st->sel_prof[6], tr - pt);
+        (void)tr;
         st->sel_ta = 0;
         sel_tick(st, 0, &pt);
         atomicAdd(&st->sel_prof[7], 1ull);
@@ -3406,6 +3544,8 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         s_ovf = 0;
     }
     __syncthreads();
+    // merge X+1 needs no tie decision: the last refresh workgroup may skip its carries
+    if (tid == 0 && (s_h || !s_tie)) st_wt(&st->ref_noprefix, X);
     if (N.prof && tid == 0) sel_tick(st, 2, &pt);
     // the tied top pair's key, deferred by select_finish (stored on every way out below)
     auto put_key = [&]() {
@@ -3495,14 +3635,32 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     // the refreshed home summaries were stored write-through and drained before each refresh
     // block's count: wait for all nref, then read them with sc1 loads) --------------------------------
     if (N.prof && tid == 0) sel_tick(st, 3, &pt);
-    if (nref && tid == 0) {
-        // every refresh block is resident or done (they never wait), so this ends
-        while (__hip_atomic_load(&st->ref_ticket[X & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nref)
-            __builtin_amdgcn_s_sleep(1);
+    if (nref && tid < 64) {
+        // every refresh block is resident or done (they never wait), so this ends. pfx: the top
+        // counter reaches the groups + the prefix's arrival; else the XCD counters sum to nref
+        const uint32_t *rtk = N.rtk + (X & 1) * RTK_SET;
+        if (pfx) {
+            while (ld_wt(rtk + 8 * RTK_STRIDE) < min(nref, 8u) + 1u) __builtin_amdgcn_s_sleep(1);
+        } else {
+            for (;;) {
+                uint32_t c = tid < 8 ? ld_wt(rtk + tid * RTK_STRIDE) : 0u;
+#pragma unroll
+                for (int off = 4; off >= 1; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off);
+                if ((uint32_t)__shfl((int)c, 0) >= nref) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
     }
     __syncthreads();
-    if (N.prof && tid == 0) sel_tick(st, 10, &pt);
-    decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr);
+    if (N.prof && tid == 0) {
+        sel_tick(st, 10, &pt);
+        if (N.cs) {  // the last refresh workgroup's prefix: start, end (from this launch's t0)
+            const unsigned long long t0 = st->sel_t0;
+            atomicAdd(&st->sel_prof[6], __hip_atomic_load(&st->sel_prof_pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t0);
+            atomicAdd(&st->sel_prof[11], __hip_atomic_load(&st->sel_prof_pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t0);
+        }
+    }
+    decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }

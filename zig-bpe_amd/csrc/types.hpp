@@ -67,16 +67,23 @@ struct DevState {
     uint32_t lists_x;        // tokens < lists_x existed when the lists were built (their entries carry neighbours)
     // option sel_prof: zbpe_select_next phase times (wall_clock64 ticks, summed over merges)
     unsigned long long sel_t0, sel_ta, sel_tr;  // start; latest argmax / refresh block finish
-    unsigned long long sel_prof[12];  // [8] tie decisions, [9] their carries, [10] refresh wait
+    unsigned long long sel_prof[12];  // [8] tie decisions, [9] their carries, [10] refresh wait, [6]/[11] prefix start/end
+    unsigned long long sel_prof_pq, sel_prof_pp;  // refresh_prefix start / end stamps of the current launch
     // option sel_prof, whole merge pipeline (batch mode): probe stamps of the current launches and the
     // sums they fold into (Engine::train prints them): scan (list form) LDS clear / walk / flush done and
     // the next kernel's start, replace work span and the select's start, select end -> scan start
     unsigned long long pp_t[16];  // [8..12]: replace phases (update blocks: deltas in, gathered, reserved, table done; apply done)
     unsigned long long pipe_prof[3][16];  // by merge: [256, 8192), [8192, 20000), [20000, ...)
-    // zbpe_select_next of merge X: home-refresh workgroups done, counted in [X & 1] (the select of
-    // X - 1 zeroes [X & 1]; the host zeroes both before a batch that does not continue one)
-    uint32_t ref_ticket[2];
+    // zbpe_select_next of merge X whose merge X+1 is not tied (its last argmax block stores X): the
+    // last refresh workgroup skips the decision's carries (zeroed with the state at each train)
+    uint32_t ref_noprefix;
 };
+// zbpe_select_next's refresh arrival counters (a device buffer): per launch parity X & 1, eight
+// per-XCD counters (workgroup i counts in i % 8) and a top counter, each on its own 128-B line. The
+// select of X - 1 zeroes parity X & 1; the host zeroes both before a batch that does not continue one.
+constexpr int RTK_STRIDE = 32;                     // words between counters
+constexpr int RTK_SET = 9 * RTK_STRIDE;            // words per parity
+constexpr int RTK_WORDS = 2 * RTK_SET;
 // why a device-resident batch stopped (the host finishes that merge on the synchronous path)
 enum HaltReason : uint32_t {
     HALT_NONE = 0,
