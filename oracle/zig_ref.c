@@ -484,7 +484,7 @@ int zref_encode(const uint16_t *triples, size_t n_merges, const uint8_t *text, s
             size_t i = 0, j = 0;
             while (i < len) {
                 if (i + 1 < len && out[i] == a && out[i + 1] == b) {
-                    if (x == a && j > 0) { /* rare: new token equals first; defer to literal */
+                    if (x == a) { /* rare: new token equals first (it chains); defer to literal */
                         return zref_encode(triples, n_merges, text, n, 1, out, out_len);
                     }
                     out[j++] = x;

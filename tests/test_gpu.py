@@ -214,6 +214,30 @@ def test_self_pairs_from_lists_vs_oracle(kind, seed, n, vocab):
     e.close()
 
 
+@pytest.mark.parametrize("encode_batch", [1, 32])
+def test_encode_new_token_equals_first_vs_oracle(encode_batch):
+    """A merge table (e.g. from deserializeMerges) may hold (a, b) -> a. The reference's encode re-tests
+    position i after merging there (basic_tokenizer.zig:71-88 does not advance i), so a absorbs the whole
+    run of b's after it, and (a, a) -> a collapses a run of a's: the device repeats such a merge until a
+    pass finds no occurrence. Compared with the oracle's literal orderedRemove loop."""
+    e = zbpe.Engine(0)
+    e.set_option("encode_batch", encode_batch)
+    text = zbpe.synth_corpus("runs", 54, 50000) + b"abbbbbab aaaaaaa bbbb abab" * 50
+    m, _, _ = e.train(text, 400)
+    a, b = ord("a"), ord("b")
+    x = int(m[0][2])
+    tables = [
+        np.array([[a, b, a]], dtype=np.uint16),                       # a absorbs runs of b
+        np.array([[a, a, a]], dtype=np.uint16),                       # runs of a collapse
+        np.array([[b, b, b], [a, b, a]], dtype=np.uint16),
+        np.concatenate([m[:20], np.array([[x, a, x], [a, b, a]], dtype=np.uint16), m[20:40]]),
+    ]
+    for mm in tables:
+        for t in (text, b"ab", b"abb", b"aab", b"bbbb", b"", text[:997]):
+            assert np.array_equal(e.encode(mm, t), O.encode(mm, t, literal=True)), (mm[:3].tolist(), t[:20])
+    e.close()
+
+
 def test_encode_runs_vs_oracle(engine):
     text = zbpe.synth_corpus("runs", 43, 100000)
     m, _, _ = _train(engine, text, 600)

@@ -33,7 +33,8 @@ def run(out, opts):
     e.train_resident(32000)
     m, c, st = e.train_resident(32000)
     log = e.merge_log()
-    json.dump({"scan_log": e.scan_log().tolist(), "ties": log[:, 3].tolist(), "count": log[:, 1].tolist()},
+    json.dump({"scan_log": e.scan_log().tolist(), "ties": log[:, 3].tolist(), "count": log[:, 1].tolist(),
+               "live": log[:, 2].tolist()},
               open(out, "w"))
     print(f"{len(m)} merges, {st.total_s:.3f} s")
     e.close()
@@ -56,6 +57,7 @@ def analyse(d, logp):
         sys.exit(f"{len(scans)} scans in the trace, {len(slog)} in the log")
     scans = scans[len(scans) - len(slog):]
     buckets = [(0, 2000), (2000, 8000), (8000, 20000), (20000, 1 << 30)]
+    dens_acc = {}
     acc = {b: {} for b in buckets}
 
     def add(b, k, v):
@@ -75,6 +77,13 @@ def analyse(d, logp):
             continue
         b = next(bb for bb in buckets if bb[0] <= mi < bb[1])
         add(b, "scan_" + ("list" if form else "stream"), (s[1] - s[0]) / 1e3)
+        if not form and "live" in L:  # stream form: by occurrence density (count / live tokens)
+            dens = L["count"][mi] / max(1, L["live"][mi])
+            db = next(x for x in (0.0005, 0.002, 0.005, 0.01, 0.02, 1.0) if dens <= x)
+            a = dens_acc.setdefault(db, [0.0, 0.0, 0])
+            a[0] += (s[1] - s[0])
+            a[1] += 2.0 * L["live"][mi]
+            a[2] += 1
         add(b, "gap_scan_replace", (r[0] - s[1]) / 1e3)
         add(b, "replace", (r[1] - r[0]) / 1e3)
         add(b, "gap_replace_select", (sel[0] - r[1]) / 1e3)
@@ -87,6 +96,9 @@ def analyse(d, logp):
     for b in buckets:
         out[f"merges [{b[0]}, {b[1] if b[1] < 1 << 30 else 'end'})"] = {
             k: {"avg_us": round(v[0] / v[1], 2), "n": v[1]} for k, v in sorted(acc[b].items())}
+    out["stream_scans_by_density"] = {
+        f"count/live <= {k}": {"launches": v[2], "avg_us": round(v[0] / v[2] / 1e3, 2), "alg_GBps": round(v[1] / v[0], 1)}
+        for k, v in sorted(dens_acc.items())}
     print(json.dumps(out, indent=1))
 
 

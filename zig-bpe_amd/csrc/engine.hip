@@ -1382,9 +1382,6 @@ zbpe_status Engine::recount_check(uint64_t *mismatches, uint32_t *first_bad_key)
 zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n, uint16_t *out,
                            size_t *out_len) {
     for (size_t k = 0; k < n_merges; k++) {
-        if (triples[3 * k + 2] == triples[3 * k])
-            return fail(ZBPE_INVALID_ARGUMENT, "merge %zu: new_token == first (%u) is not supported by the device encoder", k,
-                        triples[3 * k]);
         if (triples[3 * k + 2] == HOLE || triples[3 * k] == HOLE || triples[3 * k + 1] == HOLE)
             return fail(ZBPE_INVALID_ARGUMENT, "merge %zu uses token 65535", k);
     }
@@ -1402,7 +1399,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
         for (size_t k = 0; k < n_merges; k++) {
             const uint32_t X = triples[3 * k + 2];
             max_tok = std::max<uint32_t>(max_tok, std::max<uint32_t>(X, std::max(triples[3 * k], triples[3 * k + 1])));
-            if (X < 256 || seen[X]) distinct = false;
+            if (X < 256 || seen[X] || X == triples[3 * k]) distinct = false;  // (X == first would overwrite first's list)
             seen[X] = 1;
         }
     }
@@ -1467,6 +1464,16 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
         }
         const uint32_t a = triples[3 * k], b = triples[3 * k + 1], X = triples[3 * k + 2];
         k++;
+        // X == a: the reference re-tests position i after a merge there (it does not advance), so an a
+        // absorbs the whole run of b's after it (a == b: a run of a's collapses to one a). Each pass
+        // of the merge below absorbs one b per a (halves an a-run): repeat until a pass finds none.
+        const bool chain = X == a;
+        uint64_t occ_seen = 0;
+        if (chain) {
+            CHECK(sync_state());
+            occ_seen = h_st->total_occ;
+        }
+        for (;;) {
         ScanArgs A{d_tok[cur], n_slots, a, b, d_delta, d_delta + 65536, d_st, recbuf, reccap, 0, tail, tail + 1, Halo{},
                    nullptr, vp, X, nullptr, 0, nullptr, use_lists ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio,
                    use_lists ? 1 : 0, nullptr};
@@ -1491,6 +1498,11 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
                                                    batched ? d_enc_cnt : nullptr, a, b);
         LAUNCH_OK();
         enc_batches++;
+        if (!chain) break;
+        CHECK(sync_state());
+        if (h_st->total_occ == occ_seen) break;
+        occ_seen = h_st->total_occ;
+        }
         if (!use_lists && (k & 255) == 0) {  // without lists: squeeze the holes now and then
             CHECK(sync_state());
             holes += h_st->total_occ;
