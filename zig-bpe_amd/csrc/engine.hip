@@ -409,7 +409,7 @@ zbpe_status Engine::rebuild_hot() {
     if (!T.hot || hot_cap_alloc < need) {
         if (T.hot) (void)hipFree(T.hot);
         T.hot = nullptr;
-        if (hipMalloc(&T.hot, need * 4) != hipSuccess) {
+        if (hipMalloc(&T.hot, need * 8) != hipSuccess) {
             (void)hipGetLastError();
             hot_cap_alloc = 0;
             return fail(ZBPE_OUT_OF_MEMORY, "hot list allocation (%zu ids) failed", need);

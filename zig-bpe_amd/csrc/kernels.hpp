@@ -127,6 +127,7 @@ __device__ inline uint32_t wave_append(uint32_t *counter, bool flag) {
     const uint64_t below = m & ((1ull << lane) - 1ull);
     return flag ? base + (uint32_t)__popcll(below) : ~0u;
 }
+__device__ inline unsigned long long hot_entry(uint32_t key, uint32_t id) { return ((unsigned long long)key << 32) | id; }
 __device__ inline void pair_new(const Tables &T, DevState *st, uint32_t key, uint32_t count) {
     uint32_t id = atomicAdd(&st->num_ids, 1u);
     if (id >= T.id_cap) { atomicOr(&st->error, 1u); return; }
@@ -137,7 +138,7 @@ __device__ inline void pair_new(const Tables &T, DevState *st, uint32_t key, uin
     home_add(T, st, key, true);
     if (count >= st->theta) {
         uint32_t j = atomicAdd(&st->hot_len, 1u);
-        if (j < T.hot_cap) T.hot[j] = id;
+        if (j < T.hot_cap) T.hot[j] = hot_entry(key, id);
     }
 }
 __device__ inline void pair_dec(const Tables &T, DevState *st, uint32_t key, uint32_t d) {
@@ -1773,7 +1774,10 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
         stamp(10);
         const uint32_t base = s_base, hbase = s_hbase;
         for (uint32_t j = tid; j < s_nhot; j += UPD_THREADS)
-            if (hbase + j < T.hot_cap && base + s_hot[j] < T.id_cap) T.hot[hbase + j] = base + s_hot[j];
+            if (hbase + j < T.hot_cap && base + s_hot[j] < T.id_cap) {
+                const uint32_t i = s_hot[j];
+                T.hot[hbase + j] = hot_entry(g == 1 ? pair_key(s_t[i], X) : pair_key(X, s_t[i]), base + i);
+            }
     }
     int live_delta = 0;
     for (uint32_t i = tid; i < n; i += UPD_THREADS) {
@@ -2378,7 +2382,7 @@ __global__ void __launch_bounds__(256) zbpe_hot_build(Tables T, DevState *st) {
         const uint32_t i = i0 + (threadIdx.x & 63);
         const bool take = i < n && T.id_cnt[i] >= theta;
         const uint32_t j = wave_append(&st->hot_len, take);
-        if (take && j < T.hot_cap) T.hot[j] = i;
+        if (take && j < T.hot_cap) T.hot[j] = hot_entry(T.id_key[i], i);
     }
 }
 // Fused select: argmax over the hot list, the final reduction by the last block to finish
@@ -2422,7 +2426,7 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
     const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
     MaxRec r{0, 0, NO_ID};
     for (uint32_t i = blockIdx.x * ARGMAX_THREADS + threadIdx.x; i < nh; i += gridDim.x * ARGMAX_THREADS) {
-        const uint32_t id = T.hot[i], c = T.id_cnt[id];
+        const uint32_t id = (uint32_t)T.hot[i], c = T.id_cnt[id];
         if (c >= theta && c) r = max_combine(r, MaxRec{c, 1u, id});
     }
     r = wave_max(r);
@@ -2657,7 +2661,7 @@ __global__ void __launch_bounds__(256) zbpe_tie_collect(Tables T, DevState *st, 
         uint32_t id = NO_ID;
         bool tied = false;
         if (i < n) {
-            id = T.hot[i];
+            id = (uint32_t)T.hot[i];
             tied = T.id_cnt[id] == top;
         }
         const uint32_t j = wave_append(&st->tie_len, tied);
@@ -3446,12 +3450,16 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         }
         // four hot entries per thread per step, every load of a step issued together
         MaxRec r{0, 0, NO_ID};
-        uint32_t ids[4] = {NO_ID, NO_ID, NO_ID, NO_ID}, cs[4] = {0, 0, 0, 0};
+        uint32_t ids[4] = {NO_ID, NO_ID, NO_ID, NO_ID}, cs[4] = {0, 0, 0, 0}, ks[4] = {0, 0, 0, 0};
         bool one_step = true;
         for (uint32_t i0 = bx * NEXT_THREADS + tid; i0 < nh; i0 += 4 * G) {
             one_step = i0 == bx * NEXT_THREADS + tid;
 #pragma unroll
-            for (int u = 0; u < 4; u++) ids[u] = i0 + u * G < nh ? T.hot[i0 + u * G] : NO_ID;
+            for (int u = 0; u < 4; u++) {
+                const unsigned long long e = i0 + u * G < nh ? T.hot[i0 + u * G] : (unsigned long long)NO_ID;
+                ids[u] = (uint32_t)e;
+                ks[u] = (uint32_t)(e >> 32);  // the key rides along: the block's keys at its max come from registers
+            }
 #pragma unroll
             for (int u = 0; u < 4; u++) cs[u] = ids[u] != NO_ID ? T.id_cnt[ids[u]] : 0u;
 #pragma unroll
@@ -3467,15 +3475,16 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
                 for (int u = 0; u < 4; u++) {
                     if (ids[u] != NO_ID && cs[u] == R.cnt) {
                         const uint32_t j = atomicAdd(&s_nc, 1u);
-                        if (j < NEXT_CAND) s_key[j] = T.id_key[ids[u]];
+                        if (j < NEXT_CAND) s_key[j] = ks[u];
                     }
                 }
             } else {
                 for (uint32_t i = bx * NEXT_THREADS + tid; i < nh; i += G) {
-                    const uint32_t id = T.hot[i];
+                    const unsigned long long e = T.hot[i];
+                    const uint32_t id = (uint32_t)e;
                     if (T.id_cnt[id] == R.cnt) {
                         const uint32_t j = atomicAdd(&s_nc, 1u);
-                        if (j < NEXT_CAND) s_key[j] = T.id_key[id];
+                        if (j < NEXT_CAND) s_key[j] = (uint32_t)(e >> 32);
                     }
                 }
             }
@@ -3584,11 +3593,13 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         for (uint32_t i0 = tid & ~63u; i0 < nh; i0 += NEXT_THREADS) {  // wave-uniform trip count
             const uint32_t i = i0 + (tid & 63);
             uint32_t id = NO_ID;
-            if (i < nh) id = T.hot[i];
+            unsigned long long e = NO_ID;
+            if (i < nh) e = T.hot[i];
+            id = (uint32_t)e;
             const bool tied = id != NO_ID && T.id_cnt[id] == top;
             const uint32_t j = wave_append(&s_len, tied);
             if (tied && j < total) {
-                const uint32_t key = T.id_key[id];
+                const uint32_t key = (uint32_t)(e >> 32);
                 N.tie_list[j] = ((uint64_t)(zig_pair_hash(key) & cap_mask) << 32) | key;
             }
         }

@@ -109,7 +109,7 @@ struct Tables {
     uint32_t *id_key;   // [id_cap]
     uint32_t *id_cnt;   // [id_cap]
     uint32_t id_cap;
-    uint32_t *hot;      // candidate ids for the argmax (count >= theta when appended)
+    unsigned long long *hot;  // argmax candidates, key << 32 | id (count >= theta when appended; the key rides along)
     uint32_t hot_cap;
     uint32_t *home_cnt; // u8 x 4 per word: live keys per home slot of the Zig map (nullptr: not kept)
     uint32_t home_mask; // Zig map capacity - 1 the histogram is kept for
