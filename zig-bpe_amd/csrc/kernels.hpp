@@ -816,7 +816,7 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
 // PROF (option sel_prof): the pipeline probes; a separate instantiation, so the production kernel's
 // code and register allocation are untouched by them
 template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false, bool PROF = false>
-__global__ void __launch_bounds__(SCAN_THREADS, 4) zbpe_scan_pairs_t(ScanArgs A0) {
+__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
     if (PROF && blockIdx.x == 0 && threadIdx.x == 0) {  // the last select's end -> this scan's start
         DevState *st = A0.st;
         const unsigned long long now = wall_clock64();
@@ -949,34 +949,22 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     for (uint32_t b0 = vb * per_block; b0 < span; b0 += gstride) {
         const uint32_t e0 = ab + b0 + threadIdx.x * ept;  // this thread's first entry (absolute)
         uint32_t mk = 0;
-        // the entries' positions are loaded with their neighbour words (same round trip; the matches'
-        // positions then reach the resolving lanes by shuffles, not by a dependent gather). Entries
-        // below n + 64 (the neighbour array's size) are inside the arena too.
-        uint32_t pos[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) pos[k] = 0;
         if (e0 < off + len) {
             if (ept >= 8) {  // 16-B aligned words (ab and ept are multiples of 8)
                 const uint4 *q = reinterpret_cast<const uint4 *>(NB + e0);
-                const uint4 *ql = reinterpret_cast<const uint4 *>(A.lists + e0);
                 const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
                 const uint4 w[4] = {q[0], q[1], ept == 16 ? q[2] : none, ept == 16 ? q[3] : none};
-                const uint4 pl[4] = {ql[0], ql[1], ept == 16 ? ql[2] : none, ept == 16 ? ql[3] : none};
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
-                    const uint4 v = w[k >> 2], u = pl[k >> 2];
+                    const uint4 v = w[k >> 2];
                     const uint32_t word = (k & 3) == 0 ? v.x : (k & 3) == 1 ? v.y : (k & 3) == 2 ? v.z : v.w;
-                    pos[k] = (k & 3) == 0 ? u.x : (k & 3) == 1 ? u.y : (k & 3) == 2 ? u.z : u.w;
                     const uint32_t e = e0 + k;
                     mk |= (((word >> sh) & 0xFFFFu) == partner && e >= off && e < off + len && (uint32_t)k < ept) ? (1u << k) : 0u;
                 }
             } else {
                 uint32_t t[4];
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    t[k] = (uint32_t)k < ept ? NB[e0 + k] : ~0u;
-                    pos[k] = (uint32_t)k < ept ? A.lists[e0 + k] : 0u;
-                }
+                for (int k = 0; k < 4; k++) t[k] = (uint32_t)k < ept ? NB[e0 + k] : ~0u;
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const uint32_t e = e0 + k;
@@ -1005,21 +993,12 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
             }
             const uint32_t o_incl = (uint32_t)__shfl((int)incl, owner), o_c = (uint32_t)__shfl((int)c, owner);
             const uint32_t o_mk = (uint32_t)__shfl((int)mk, owner);
-            uint32_t bit = 0;
             if (j < M) {
                 uint32_t rank = j - (o_incl - o_c), m = o_mk;  // the rank-th set bit of the owner's mask
                 for (uint32_t q = 0; q < rank; q++) m &= m - 1;
-                bit = (uint32_t)__ffs(m) - 1;
+                const uint32_t e = ab + b0 + ((threadIdx.x & ~63u) + (uint32_t)owner) * ept + (uint32_t)__ffs(m) - 1;
+                p = (int64_t)A.lists[e];
             }
-            uint32_t pv = 0;  // the owner's pos[bit]
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                if ((uint32_t)k < ept) {
-                    const uint32_t v = (uint32_t)__shfl((int)pos[k], owner);
-                    pv = bit == (uint32_t)k ? v : pv;
-                }
-            }
-            if (j < M) p = (int64_t)pv;
             // the entry's stream window in one round trip (vector, the word before, the two after)
             const int64_t vi = p < 0 ? 0 : (p >> 3);
             const uint4 cv = tv[vi];
