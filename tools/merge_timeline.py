@@ -96,6 +96,14 @@ def analyse(d, logp):
     for b in buckets:
         out[f"merges [{b[0]}, {b[1] if b[1] < 1 << 30 else 'end'})"] = {
             k: {"avg_us": round(v[0] / v[1], 2), "n": v[1]} for k, v in sorted(acc[b].items())}
+    # kernel time of the measured train by kernel (from its first pair scan to the end of the trace)
+    t0 = ks[scans[0]][0]
+    tot = {}
+    for a0, a1, name in ks:
+        if a0 >= t0:
+            short = name.split("(")[0].replace("void ", "").replace("zbpe::", "")[:40]
+            tot[short] = tot.get(short, 0.0) + (a1 - a0) / 1e6
+    out["kernel_ms_measured_train"] = {k: round(v, 2) for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:14]}
     out["stream_scans_by_density"] = {
         f"count/live <= {k}": {"launches": v[2], "avg_us": round(v[0] / v[2] / 1e3, 2), "alg_GBps": round(v[1] / v[0], 1)}
         for k, v in sorted(dens_acc.items())}

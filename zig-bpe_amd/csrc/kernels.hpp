@@ -3676,11 +3676,15 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     put_key();
 }
 
-// rebuild the home histogram for a new Zig capacity
+// rebuild the home histogram for a new Zig capacity: counts only (the caller recomputes every summary;
+// home_add's dirty-bit OR would put ~5e7 atomics on the few hundred dirty-bitmap words)
 __global__ void __launch_bounds__(256) zbpe_home_build(Tables T, DevState *st) {
     const uint32_t n = min(st->num_ids, T.id_cap);
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-        if (T.id_cnt[i]) home_add(T, st, T.id_key[i], true);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        if (!T.id_cnt[i]) continue;
+        const uint32_t s = (uint32_t)(zig_pair_hash(T.id_key[i]) & T.home_mask);
+        atomicAdd(&T.home_cnt[s >> 2], 1u << (8 * (s & 3)));
+    }
 }
 
 // exact fallback: first occurrence position of every live pair in the current stream
