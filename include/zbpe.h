@@ -139,7 +139,7 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * token), "sel_prof" (in-kernel wall-clock
  * probes of the merge pipeline, printed to stderr after train), "replace_split" (profiling: apply and count update as separate launches), "list_mode"
  * (0: always stream the token stream; 1: token occurrence lists once counts are small), "list_ratio"
- * (list scan when list length * ratio < stream slots), "list_start" (build the lists at a compaction
+ * (train: list scan when list length * ratio < stream slots), "encode_list_ratio" (the same for encode), "list_start" (build the lists at a compaction
  * once top count * list_start < live tokens; 0: at the first compaction), "compact_den_lists" (compact_den
  * once lists are on). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);

@@ -270,7 +270,7 @@ zbpe_status Engine::compact_train(uint32_t X) {
     const bool want = list_mode && pres_vp <= PRES_MAX_VP && (uint64_t)n_slots < 0xF0000000ull &&
                       (lists_on || list_start == 0 || (uint64_t)h_st->top_count * list_start < (uint64_t)n_live);
     if (want && !(dist() && replicate_late)) {  // sharded: lists come with the replication (run_batch)
-        CHECK(build_lists(X));
+        CHECK(build_lists(X, list_ratio));
     } else {
         HIP_OK(hipMemsetAsync(&d_st->arena_top, 0, 4, stream));
         HIP_OK(hipMemsetAsync(&d_st->arena_rep, 0, 4, stream));
@@ -352,7 +352,7 @@ zbpe_status Engine::grow_arena(uint64_t need) {
     return ZBPE_OK;
 }
 
-zbpe_status Engine::build_lists(uint32_t lists_x) {
+zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio) {
     const int64_t n = n_slots;
     if ((uint64_t)n + (1u << 20) > lists_cap) CHECK(grow_arena((uint64_t)n + (16u << 20)));  // lists <= n entries
     const uint32_t nchunks = (uint32_t)std::max<int64_t>(1, (n + LIST_CHUNK - 1) / LIST_CHUNK);
@@ -361,7 +361,7 @@ zbpe_status Engine::build_lists(uint32_t lists_x) {
     LAUNCH_OK();
     zbpe_list_colscan<<<(pres_vp + 255) / 256, 256, 0, stream>>>(d_list_cnt, nchunks, pres_vp, d_list_total);
     LAUNCH_OK();
-    const uint32_t max_len = (uint32_t)std::min<uint64_t>(0xFFFFFFFEu, (uint64_t)n / list_ratio);
+    const uint32_t max_len = (uint32_t)std::min<uint64_t>(0xFFFFFFFEu, (uint64_t)n / ratio);
     zbpe_list_offsets<<<1, 1024, 0, stream>>>(d_list_total, pres_vp, max_len, T.lst_off, T.lst_len, d_st, lists_x);
     LAUNCH_OK();
     if (list_nb) {  // the build-time neighbours of every list entry (the filtered list walk)
@@ -982,7 +982,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         HIP_OK(hipEventRecord(ev[3], stream));
         CHECK(compact());  // this shard's live tokens, contiguous
         CHECK(replicate());
-        CHECK(build_lists(X0));
+        CHECK(build_lists(X0, list_ratio));
         HIP_OK(hipEventRecord(ev[4], stream));
         HIP_OK(hipEventSynchronize(ev[4]));
         float ms;
@@ -1409,7 +1409,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
     if (use_lists) {
         CHECK(ensure(&d_lists, lists_cap, 2 * n + 1024, "occurrence arena"));  // lists <= n, records <= n
         pres_vp = vp;
-        CHECK(build_lists(256));  // the byte tokens exist at the build; every merge makes a new token >= 256
+        CHECK(build_lists(256, enc_list_ratio));  // the byte tokens exist at the build; every merge makes a new token >= 256
     } else {
         lists_on = false;
         CHECK(ensure(&d_rec, rec_cap, std::max<size_t>(n / 2 + 1, 1), "occurrence records"));
@@ -1451,7 +1451,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
                 k++;
             }
             ScanArgs A{d_tok[cur], n_slots, 0, 0, d_delta, d_delta + 65536, d_st, d_rec, 0, 0, tail, tail + 1, Halo{},
-                       nullptr, vp, 0, nullptr, 0, nullptr, d_lists, T.lst_off, T.lst_len, list_ratio, 0, nullptr};
+                       nullptr, vp, 0, nullptr, 0, nullptr, d_lists, T.lst_off, T.lst_len, enc_list_ratio, 0, nullptr};
             set_list_nb(A);
             hipLaunchKernelGGL(zbpe_encode_scan_batch, dim3(scan_grid(n_slots), E.nb), dim3(SCAN_THREADS), 0, stream, A, E,
                                (const int32_t *)d_enc_cnt, d_enc_ctr, d_rec);
@@ -1475,7 +1475,7 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
         }
         for (;;) {
         ScanArgs A{d_tok[cur], n_slots, a, b, d_delta, d_delta + 65536, d_st, recbuf, reccap, 0, tail, tail + 1, Halo{},
-                   nullptr, vp, X, nullptr, 0, nullptr, use_lists ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio,
+                   nullptr, vp, X, nullptr, 0, nullptr, use_lists ? d_lists : nullptr, T.lst_off, T.lst_len, enc_list_ratio,
                    use_lists ? 1 : 0, nullptr};
         set_list_nb(A);
         if (a != b) {

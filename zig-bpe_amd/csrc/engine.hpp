@@ -117,7 +117,8 @@ struct Engine {
     bool list_streak = false;   // the last batch used list scans only
     int list_grid = 0;          // scan grid after such a batch (option "list_grid"; 0 = the full grid)
     int list_mode = 1;          // 0: never build lists, 1: once pair counts are small against the stream
-    uint32_t list_ratio = 256;  // list scan when list length * ratio < stream slots
+    uint32_t list_ratio = 96;   // training: list scan when list length * ratio < stream slots
+    uint32_t enc_list_ratio = 256;  // the same for encode (option "encode_list_ratio")
     uint32_t self_list_ratio = 8;  // self pair from a's list when length * ratio < stream slots (0: never)
     uint64_t list_start = 64;   // build lists at a compaction once top count * list_start < live tokens (0: always)
     // per-merge trace (option "trace"), ZBPE_TRACE_COLS floats per merge
@@ -168,7 +169,7 @@ struct Engine {
         double tm_count = 0, tm_select = 0, tm_replace = 0, tm_comm = 0;  // stage times of the timed batch merges
         double batch_s = 0;                                   // device span of the batches
     } run;
-    uint64_t hot_target = 1u << 16;  // ids the hot list aims to hold after a rebuild
+    uint64_t hot_target = 1u << 15;  // ids the hot list aims to hold after a rebuild
     uint64_t hot_rebuilds = 0, home_rebuilds = 0;
     hipEvent_t ev[6] = {};
 
@@ -211,7 +212,7 @@ struct Engine {
     zbpe_status compact();
     zbpe_status compact_train(uint32_t X);
     zbpe_status grow_arena(uint64_t need);
-    zbpe_status build_lists(uint32_t lists_x);
+    zbpe_status build_lists(uint32_t lists_x, uint32_t ratio);
     void set_list_nb(ScanArgs &A) const;
     zbpe_status replicate();
     zbpe_status launch_argmax(uint32_t X, int roll);
