@@ -27,11 +27,15 @@ def main():
     p.add_argument("--vocab", type=int, default=32000)
     p.add_argument("--check-bytes", type=int, default=200_000)
     p.add_argument("--reps", type=int, default=2)
+    p.add_argument("--opt", action="append", default=[], help="engine option k=v applied before encode (repeatable)")
     a = p.parse_args()
     e = zbpe.Engine(0)
     e.upload(zbpe.synth_corpus("words_utf8", 0x5EED0004, a.train_bytes, threads=16))
     merges, counts, st = e.train_resident(a.vocab)
     text = zbpe.synth_corpus("words_utf8", 0x5EED0005, a.n_bytes, threads=16)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        e.set_option(k, int(v))
     times = []
     out = None
     for _ in range(a.reps):
@@ -40,7 +44,8 @@ def main():
         times.append(time.perf_counter() - t)
     best = min(times)
     res = {"metric": "encode chars/s (C5: 100 M chars, C4 merges)", "value": a.n_bytes / best, "unit": "chars/s",
-           "seconds": best, "merges": int(len(merges)), "tokens_out": int(len(out)), "reps": a.reps}
+           "seconds": best, "merges": int(len(merges)), "tokens_out": int(len(out)), "reps": a.reps,
+           "opts": a.opt}
     if a.check_bytes:
         import oracle as O
         ref = O.encode(merges, text[: a.check_bytes])

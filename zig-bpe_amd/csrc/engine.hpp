@@ -118,7 +118,7 @@ struct Engine {
     int list_grid = 0;          // scan grid after such a batch (option "list_grid"; 0 = the full grid)
     int list_mode = 1;          // 0: never build lists, 1: once pair counts are small against the stream
     uint32_t list_ratio = 96;   // training: list scan when list length * ratio < stream slots
-    uint32_t enc_list_ratio = 256;  // the same for encode (option "encode_list_ratio")
+    uint32_t enc_list_ratio = 48;   // the same for encode (option "encode_list_ratio")
     uint32_t self_list_ratio = 8;  // self pair from a's list when length * ratio < stream slots (0: never)
     uint64_t list_start = 64;   // build lists at a compaction once top count * list_start < live tokens (0: always)
     // per-merge trace (option "trace"), ZBPE_TRACE_COLS floats per merge
