@@ -598,6 +598,7 @@ static const ScanFn kScanVariants[] = {zbpe_scan_pairs_t<4, true, true, true, tr
                                        zbpe_scan_pairs_t<2, true, true, true, true>, zbpe_scan_pairs_t<4, true, true, false, true>,
                                        zbpe_scan_pairs_t<4, false, true, true, true>};
 static const int kScanUnroll[] = {4, 8, 4, 4, 2, 4, 4};
+static constexpr int kScanBlocksPerCuMax = 4;
 
 zbpe_status Engine::set_scan_variant(int v) {
     if (v < 0 || v >= (int)(sizeof(kScanVariants) / sizeof(kScanVariants[0])))
@@ -605,7 +606,9 @@ zbpe_status Engine::set_scan_variant(int v) {
     int nb = 0;
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)kScanVariants[v], SCAN_THREADS, 0));
     scan_variant = v;
-    scan_blocks_per_cu = std::max(1, nb);
+    // at most four per CU: the occupancy query reports 8, but a grid past four workgroups per CU ran long list walks
+    // in two dispatch rounds (C4: 8 per CU 17.4k merges/s, 4 per CU 17.8k, profiles/r02_ab_knobs.jsonl)
+    scan_blocks_per_cu = std::max(1, std::min(nb, kScanBlocksPerCuMax));
     return ZBPE_OK;
 }
 

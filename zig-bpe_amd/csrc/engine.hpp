@@ -176,7 +176,7 @@ struct Engine {
     // policy knobs
     uint64_t compact_den = 8;     // compact when holes > slots / compact_den
     uint64_t compact_den_lists = 8;  // the same once occurrence lists are on (a compaction also rebuilds them)
-    int scan_blocks_per_cu = 8;
+    int scan_blocks_per_cu = 4;  // set by set_scan_variant: occupancy, at most four (one dispatch round)
     bool debug_checks = false;    // extra syncs + consistency checks
     bool force_exact_ties = false;  // resolve every tie by the exact emulation and cross-check the fast path
 
