@@ -70,7 +70,18 @@ typedef struct zbpe_stats {
      * all-reduce, from the HIP events of the timed merges, split like the stage buckets */
     double sharded_s, replicate_s, replicated_s, comm_s;
     uint64_t sharded_merges;
+    /* ties decided by both the device's cluster test and the exact emulation, with the same winner
+     * (options "exact_ties", "exact_ties_from" / "exact_ties_to"); a disagreement fails the train */
+    uint64_t tie_crosschecks;
 } zbpe_stats;
+
+/* Layout version of zbpe_stats. The struct is caller-allocated and has grown across versions: a
+ * consumer compares zbpe_stats_size() with the size of the zbpe_stats of the header it was built against
+ * before passing a zbpe_stats: the library writes zbpe_stats_size() bytes.
+ *   1: up to tie_fallbacks ... list_builds;  2: + replications, phase split, sharded_merges;
+ *   3: + tie_crosschecks. */
+#define ZBPE_STATS_VERSION 3
+size_t zbpe_stats_size(void);
 
 /* Create a single-GPU context on HIP device `device`. */
 zbpe_status zbpe_create(int device, zbpe_ctx **out);
@@ -126,7 +137,8 @@ zbpe_status zbpe_verify_counts(zbpe_ctx *ctx, uint64_t *mismatches);
 zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_tokens);
 
 /* Tuning / test options: "debug_checks" (0/1), "exact_ties" (resolve every tie by the exact
- * first-occurrence emulation and cross-check the GPU cluster test), "compact_den" (compact when
+ * first-occurrence emulation and cross-check the GPU cluster test), "exact_ties_from" / "exact_ties_to"
+ * (the same for merge indices k in [from, to) only; the other merges stay device-resident), "compact_den" (compact when
  * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..6: unroll, load kind, phase-2 form;
  * see engine.hip kScanVariants), "hot_target" (ids kept by the argmax hot list),
  * "block_skip" (0/1: stream only the 8192-slot blocks that hold the pair's rarer token),

@@ -237,9 +237,34 @@ static double now_s(void) {
  * out_ties: number of pairs sharing the top count per merge (may be NULL);
  * out_distinct: D_t per merge (may be NULL); max_merges caps the loop (0 = no cap) so that
  * a bounded CPU sample can be timed. */
+/* FNV-1a 64 over the u16 stream's bytes (the long-run goldens record it per merge window). */
+uint64_t zref_fnv64(const uint16_t *tok, size_t len) {
+    uint64_t h = 0xcbf29ce484222325ULL;
+    const uint8_t *p = (const uint8_t *)tok;
+    for (size_t i = 0; i < 2 * len; i++) h = (h ^ p[i]) * 0x100000001b3ULL;
+    return h;
+}
+
+/* zref_train with a progress log: when `progress` is non-NULL, one line per merge
+ * "k first second new_token count ties distinct len_after" is appended and flushed, and every
+ * `fnv_every` merges (0 = never) a line "fnv k len fnv64" of the stream after merge k, so a
+ * multi-hour golden run keeps what it has computed if it is stopped. */
+int zref_train_log(const uint8_t *text, size_t n, uint32_t vocab_size, int verbose, uint32_t max_merges,
+                   uint16_t *out_triples, uint64_t *out_counts, uint32_t *out_ties, uint32_t *out_distinct,
+                   size_t *out_n_merges, zref_stats *stats, uint16_t *out_tokens, size_t *out_n_tokens,
+                   const char *progress, uint32_t fnv_every);
+
 int zref_train(const uint8_t *text, size_t n, uint32_t vocab_size, int verbose, uint32_t max_merges,
                uint16_t *out_triples, uint64_t *out_counts, uint32_t *out_ties, uint32_t *out_distinct,
                size_t *out_n_merges, zref_stats *stats, uint16_t *out_tokens, size_t *out_n_tokens) {
+    return zref_train_log(text, n, vocab_size, verbose, max_merges, out_triples, out_counts, out_ties,
+                          out_distinct, out_n_merges, stats, out_tokens, out_n_tokens, NULL, 0);
+}
+
+int zref_train_log(const uint8_t *text, size_t n, uint32_t vocab_size, int verbose, uint32_t max_merges,
+                   uint16_t *out_triples, uint64_t *out_counts, uint32_t *out_ties, uint32_t *out_distinct,
+                   size_t *out_n_merges, zref_stats *stats, uint16_t *out_tokens, size_t *out_n_tokens,
+                   const char *progress, uint32_t fnv_every) {
     zref_stats st;
     memset(&st, 0, sizeof(st));
     double t_train = now_s();
@@ -252,6 +277,7 @@ int zref_train(const uint8_t *text, size_t n, uint32_t vocab_size, int verbose, 
     uint16_t *tok = (uint16_t *)malloc(sizeof(uint16_t) * (n ? n : 1));
     if (!tok) return 2;
     for (size_t i = 0; i < n; i++) tok[i] = text[i];
+    FILE *plog = progress ? fopen(progress, "w") : NULL;
     size_t len = n;
     size_t pairs_cap = 0;
     uint32_t *pairs = NULL;
@@ -339,6 +365,18 @@ int zref_train(const uint8_t *text, size_t n, uint32_t vocab_size, int verbose, 
         len = j;
         st.replace_pair_s += now_s() - t3;
         st.replace_pair_calls++;
+        if (plog) {
+            fprintf(plog, "%u %u %u %u %llu %u %zu %zu\n", merges_done - 1, first, second, cur,
+                    (unsigned long long)top.count, ties, d, len);
+            if (fnv_every && merges_done % fnv_every == 0)
+                fprintf(plog, "fnv %u %zu %016llx\n", merges_done, len,
+                        (unsigned long long)zref_fnv64(tok, len));
+            fflush(plog);
+        }
+    }
+    if (plog) {
+        fprintf(plog, "done %u %zu %016llx\n", merges_done, len, (unsigned long long)zref_fnv64(tok, len));
+        fclose(plog);
     }
     st.total_s = now_s() - t_train;
     *out_n_merges = merges_done;

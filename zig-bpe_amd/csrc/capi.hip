@@ -17,7 +17,9 @@ static const char *env_or(const char *k) { const char *v = getenv(k); return v &
 
 extern "C" {
 
-const char *zbpe_version(void) { return "zbpe-mi355x 0.1 (gfx950)"; }
+const char *zbpe_version(void) { return "zbpe-mi355x 0.3 (gfx950, zbpe_stats v3)"; }
+
+size_t zbpe_stats_size(void) { return sizeof(zbpe_stats); }
 
 zbpe_status zbpe_create(int device, zbpe_ctx **out) {
     if (!out) return ZBPE_INVALID_ARGUMENT;
@@ -119,6 +121,8 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     zbpe::Engine &e = ctx->eng;
     if (k == "debug_checks") e.debug_checks = value != 0;
     else if (k == "exact_ties") e.force_exact_ties = value != 0;
+    else if (k == "exact_ties_from" && value >= 0 && value < 65536) e.exact_lo = (uint32_t)value + 256;
+    else if (k == "exact_ties_to" && value >= 0 && value < 65536) e.exact_hi = (uint32_t)value + 256;
     else if (k == "compact_den" && value > 0) e.compact_den = (uint64_t)value;
     else if (k == "scan_blocks_per_cu" && value > 0) e.scan_blocks_per_cu = (int)value;
     else if (k == "scan_variant") return e.set_scan_variant((int)value);

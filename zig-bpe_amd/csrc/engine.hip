@@ -15,6 +15,8 @@
 #include <cstring>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "kernels.hpp"
 #include "zig_order.hpp"
 
@@ -57,7 +59,10 @@ void Engine::release() {
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_cs); f(d_rtk); f(d_sizes);
-    f(d_enc_cnt); f(d_enc_ctr); f(d_nb);
+    f(d_enc_cnt); f(d_enc_ctr); f(d_nb); f(d_ord_pos); f(d_ord_ent); f(d_sort_tmp);
+    d_ord_pos = nullptr; d_ord_ent = nullptr; d_sort_tmp = nullptr; ord_pos_cap = ord_ent_cap = sort_tmp_cap = 0;
+    if (h_ord) (void)hipHostFree(h_ord);
+    h_ord = nullptr; h_ord_cap = 0;
     d_nb = nullptr; nb_cap = 0;
     d_enc_cnt = nullptr; d_enc_ctr = nullptr; enc_cnt_cap = enc_ctr_cap = 0;
     for (auto &e : bev) if (e) (void)hipEventDestroy(e);
@@ -532,7 +537,7 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     CHECK(sync_state());
     if (h_st->tie_len != ties)
         return fail(ZBPE_INTERNAL, "tie collection found %u pairs at count %u, argmax said %u", h_st->tie_len, top, ties);
-    if (h_st->tie_verdict == 0 && !force_exact_ties) {
+    if (h_st->tie_verdict == 0 && !exact_now) {
         *winner = h_st->tie_winner;
         return ZBPE_OK;
     }
@@ -548,6 +553,37 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
         zbpe_first_occ<<<2048, 256, 0, stream>>>(A, T, d_first, d_st);  // shard-local positions
         LAUNCH_OK();
     }
+    if (!dist()) {
+        // one GPU: sort the live pairs by first occurrence on the device (positions are unique per pair),
+        // copy the ordered emulation entries to pinned host memory, replay the Zig map on the host
+        CHECK(ensure(&d_ord_pos, ord_pos_cap, 2 * (size_t)D + 2, "tie emulation positions"));
+        CHECK(ensure(&d_ord_ent, ord_ent_cap, 2 * (size_t)D + 2, "tie emulation entries"));
+        uint32_t *pos_in = d_ord_pos, *pos_out = d_ord_pos + D + 1;
+        unsigned long long *ent_in = d_ord_ent, *ent_out = d_ord_ent + D + 1;
+        zbpe_gather_order<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_first, d_st, top, pos_in, ent_in,
+                                                                                        (uint32_t)(D + 1));
+        LAUNCH_OK();
+        CHECK(sync_state());
+        const uint32_t g = h_st->gather_len;
+        if (g != D) return fail(ZBPE_INTERNAL, "gathered %u live pairs, expected %llu", g, (unsigned long long)D);
+        int end_bit = 1;
+        while (end_bit < 32 && ((uint64_t)n_slots >> end_bit)) end_bit++;
+        size_t tmp_bytes = 0;
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, pos_in, pos_out, ent_in, ent_out, (int)g, 0, end_bit, stream));
+        CHECK(ensure(&d_sort_tmp, sort_tmp_cap, tmp_bytes + 16, "tie emulation sort scratch"));
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(d_sort_tmp, tmp_bytes, pos_in, pos_out, ent_in, ent_out, (int)g, 0, end_bit, stream));
+        if (h_ord_cap < g) {
+            if (h_ord) (void)hipHostFree(h_ord);
+            h_ord = nullptr;
+            h_ord_cap = 0;
+            HIP_OK(hipHostMalloc((void **)&h_ord, (size_t)g * 8 + 8, hipHostMallocDefault));
+            h_ord_cap = g;
+        }
+        HIP_OK(hipMemcpyAsync(h_ord, ent_out, (size_t)g * 8, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        if (!zig_emulate_first_tied(h_ord, g, call_after, winner))
+            return fail(ZBPE_INTERNAL, "exact tie emulation found no pair with count %u", top);
+    } else {
     zbpe_gather_live<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_first, d_st, d_gather, (uint32_t)gather_cap);
     LAUNCH_OK();
     CHECK(sync_state());
@@ -583,8 +619,12 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     for (uint32_t i = 0; i < g; i++) in[i] = ZigOrderInput{order[i], recs[i].key, recs[i].count};
     if (!zig_order_winner(std::move(in), top, call_after, winner))
         return fail(ZBPE_INTERNAL, "exact tie emulation found no pair with count %u", top);
-    if (h_st->tie_verdict == 0 && *winner != h_st->tie_winner)
-        return fail(ZBPE_INTERNAL, "tie fast path chose 0x%08x, exact emulation 0x%08x", h_st->tie_winner, *winner);
+    }
+    if (h_st->tie_verdict == 0) {
+        if (*winner != h_st->tie_winner)
+            return fail(ZBPE_INTERNAL, "tie fast path chose 0x%08x, exact emulation 0x%08x", h_st->tie_winner, *winner);
+        stats.tie_crosschecks++;  // both paths decided this tie, alike
+    }
     return ZBPE_OK;
 }
 
@@ -866,7 +906,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             if (rank == 0) fprintf(stderr, "No more pairs to merge. Stopping early.\n");
             break;
         }
-        if (merge_batch > 1 && !debug_checks && !force_exact_ties && vocab_size - X > 1) {
+        if (merge_batch > 1 && !debug_checks && !exact_at(X) && vocab_size - X > 1) {
             uint32_t done = 0;
             bool halted = false;
             const bool was_sharded = dist();
@@ -972,7 +1012,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
 // merge the device cannot finish alone (self pair, undecided tie, capacity change, hot-list
 // rebuild), after which every remaining kernel of the batch returns at once. One sync per batch.
 zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
-    const uint32_t K = std::min<uint32_t>(merge_batch, run.vocab - X0);
+    uint32_t K = std::min<uint32_t>(merge_batch, run.vocab - X0);
+    if (X0 < exact_lo && exact_lo < exact_hi) K = std::min<uint32_t>(K, exact_lo - X0);  // stop at the exact-tie window
     *done = 0;
     *halted = false;
     // multi-GPU: once pair counts are small against the stream (the single-GPU criterion for
@@ -1140,7 +1181,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             }
             // the sampled merges give the shares of the stages; the batch's measured span is split by them
             run.tm_count += w * (ms_scan + ms_comm) * 1e-3;  // the exchange of the count deltas is counting
-            run.tm_comm += w * ms_comm * 1e-3;
+            if (dist()) run.tm_comm += w * ms_comm * 1e-3;  // world 1 or replicas: no collective, only an event gap
             run.tm_select += w * ms_sel * 1e-3;
             run.tm_replace += w * ms_rep * 1e-3;
         }
@@ -1171,6 +1212,8 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     const uint32_t top = h_st->top_count, ties = h_st->tie_count;
     uint32_t key = h_st->top_key;
     const double t_sel = now_s();
+    exact_now = exact_at(X);
+    begun = false;  // this merge's select (zbpe_select) does not start the next merge on the device
     if (ties > 1) CHECK(resolve_tie(top, ties, &key));
     stats.sort_pairs_calls++;
     if (ties > 1) run.ev_select += now_s() - t_sel;

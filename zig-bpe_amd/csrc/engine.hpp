@@ -83,6 +83,13 @@ struct Engine {
     size_t first_cap = 0;
     LiveRec *d_gather = nullptr;
     size_t gather_cap = 0;
+    // exact tie emulation on one GPU: live pairs sorted by first occurrence on the device
+    uint32_t *d_ord_pos = nullptr;
+    unsigned long long *d_ord_ent = nullptr;
+    uint8_t *d_sort_tmp = nullptr;
+    size_t ord_pos_cap = 0, ord_ent_cap = 0, sort_tmp_cap = 0;
+    uint64_t *h_ord = nullptr;  // pinned
+    size_t h_ord_cap = 0;
     uint32_t *d_recount = nullptr;
     size_t recount_cap = 0;
     uint32_t *d_count_hist = nullptr, *h_count_hist = nullptr;
@@ -179,6 +186,11 @@ struct Engine {
     int scan_blocks_per_cu = 4;  // set by set_scan_variant: occupancy, at most four (one dispatch round)
     bool debug_checks = false;    // extra syncs + consistency checks
     bool force_exact_ties = false;  // resolve every tie by the exact emulation and cross-check the fast path
+    // the same for the merges X in [exact_lo, exact_hi) only (options "exact_ties_from" / "exact_ties_to", merge
+    // indices X - 256): those run on the synchronous path, the others in device-resident batches
+    uint32_t exact_lo = 0xFFFFFFFFu, exact_hi = 0;
+    bool exact_at(uint32_t X) const { return force_exact_ties || (X >= exact_lo && X < exact_hi); }
+    bool exact_now = false;         // the merge being finished on the synchronous path is in the exact window
 
     zbpe_stats stats{};
     uint64_t stats_rebuilds = 0;

@@ -3711,6 +3711,26 @@ __global__ void __launch_bounds__(256) zbpe_gather_live(Tables T, const uint32_t
     }
 }
 
+// The exact tie emulation's input on one GPU: every live pair as a (first occurrence, entry) pair for a
+// device radix sort by position; entry = zig_emu_entry (zig_order.hpp): low 31 bits of the Zig hash,
+// the tied bit (count == top), the key. One wave-aggregated append per wave.
+__global__ void __launch_bounds__(256) zbpe_gather_order(Tables T, const uint32_t *__restrict__ first, DevState *st, uint32_t top,
+                                                         uint32_t *__restrict__ pos_out, unsigned long long *__restrict__ ent_out,
+                                                         uint32_t out_cap) {
+    const uint32_t n = min(st->num_ids, T.id_cap);
+    const uint32_t n_round = (n + 63) & ~63u;  // whole waves reach the ballot
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_round; i += gridDim.x * 256) {
+        const uint32_t c = i < n ? T.id_cnt[i] : 0;
+        const uint32_t j = wave_append(&st->gather_len, c != 0);
+        if (c && j < out_cap) {
+            const uint32_t key = T.id_key[i];
+            const uint32_t h = ((uint32_t)zig_pair_hash(key) & 0x7FFFFFFFu) | (c == top ? 0x80000000u : 0u);
+            pos_out[j] = first[i];
+            ent_out[j] = ((unsigned long long)h << 32) | key;
+        }
+    }
+}
+
 // verification: recount every live pair of the stream and compare with the maintained counts
 // recount every pair this shard owns (the pair leaving the shard included, through the halo)
 __global__ void __launch_bounds__(256) zbpe_recount(ScanArgs A, Tables T, uint32_t *recount, DevState *st) {

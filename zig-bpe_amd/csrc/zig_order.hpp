@@ -44,38 +44,63 @@ struct ZigOrderInput {
     uint32_t key, count;
 };
 
+// One live pair for the emulation: the low 31 bits of its Zig hash (homes of every capacity up to
+// 2^31), whether it is tied at the top count, and its key.
+inline uint64_t zig_emu_entry(uint32_t key, bool tied) {
+    return ((uint64_t)(((uint32_t)host_zig_pair_hash(key) & 0x7FFFFFFFu) | (tied ? 0x80000000u : 0u)) << 32) | key;
+}
+
+// Emulates the Zig map's life -- insertions in first-occurrence order, a grow to twice the capacity
+// whenever a getOrPut finds the table full (re-inserting in old-slot order), the trailing grow when
+// a getOrPut follows the last insertion -- and returns the key of the first slot (ascending) whose
+// pair is tied (bit 63 of zig_emu_entry). `ins` lists the live pairs in insertion order.
+// The table holds the entries themselves, so a grow re-inserts from the old table in slot order: the
+// new homes of consecutive old slots are two sequential streams (h, h + cap), and only the new
+// insertions hit random slots, which are prefetched a few keys ahead. Key 0xFFFFFFFF (two hole
+// tokens) never occurs, so ~0 marks an empty slot.
+inline bool zig_emulate_first_tied(const uint64_t *ins, size_t n, bool call_after_last_insert, uint32_t *winner) {
+    constexpr uint64_t EMPTY = ~0ull;
+    constexpr size_t PF = 16;
+    std::vector<uint64_t> tab, old;
+    uint64_t cap = 0, avail = 0, size = 0;
+    auto place = [&](uint64_t e) {
+        const uint64_t m = cap - 1;
+        uint64_t s = (e >> 32) & 0x7FFFFFFFu & m;
+        while (tab[s] != EMPTY) s = (s + 1) & m;
+        tab[s] = e;
+    };
+    auto grow = [&](uint64_t nc) {
+        old.swap(tab);
+        tab.assign(nc, EMPTY);
+        cap = nc;
+        for (uint64_t e : old)
+            if (e != EMPTY) place(e);
+        avail = zig_max_load(cap) - size;
+    };
+    for (size_t i = 0; i < n; i++) {
+        if (avail == 0) grow(cap ? cap * 2 : 8);
+        if (i + PF < n) __builtin_prefetch(&tab[(ins[i + PF] >> 32) & 0x7FFFFFFFu & (cap - 1)], 1);
+        place(ins[i]);
+        avail--;
+        size++;
+    }
+    if (avail == 0 && call_after_last_insert) grow(cap * 2);
+    for (uint64_t e : tab)
+        if (e != EMPTY && (e >> 63)) {
+            *winner = (uint32_t)e;
+            return true;
+        }
+    return false;
+}
+
 // Returns the key of the first slot (ascending) holding a pair with count == top.
 inline bool zig_order_winner(std::vector<ZigOrderInput> live, uint32_t top, bool call_after_last_insert,
                              uint32_t *winner) {
     std::sort(live.begin(), live.end(),
               [](const ZigOrderInput &x, const ZigOrderInput &y) { return x.first_pos < y.first_pos; });
-    uint64_t cap = 0, avail = 0;
-    std::vector<uint32_t> key, idx;  // idx: index into live, or UINT32_MAX when empty
-    auto place = [&](uint32_t i) {
-        uint64_t m = cap - 1, s = host_zig_pair_hash(live[i].key) & m;
-        while (idx[s] != UINT32_MAX) s = (s + 1) & m;
-        idx[s] = i;
-        avail--;
-    };
-    auto grow = [&](uint64_t nc) {
-        std::vector<uint32_t> old = std::move(idx);
-        cap = nc;
-        idx.assign(cap, UINT32_MAX);
-        avail = zig_max_load(cap);
-        for (uint32_t i : old)
-            if (i != UINT32_MAX) place(i);
-    };
-    for (uint32_t i = 0; i < live.size(); i++) {
-        if (avail == 0) grow(cap ? cap * 2 : 8);
-        place(i);
-    }
-    if (avail == 0 && call_after_last_insert) grow(cap * 2);
-    for (uint64_t s = 0; s < cap; s++)
-        if (idx[s] != UINT32_MAX && live[idx[s]].count == top) {
-            *winner = live[idx[s]].key;
-            return true;
-        }
-    return false;
+    std::vector<uint64_t> ins(live.size());
+    for (size_t i = 0; i < live.size(); i++) ins[i] = zig_emu_entry(live[i].key, live[i].count == top);
+    return zig_emulate_first_tied(ins.data(), ins.size(), call_after_last_insert, winner);
 }
 
 }  // namespace zbpe

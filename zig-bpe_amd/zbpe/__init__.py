@@ -137,6 +137,7 @@ class Stats(ctypes.Structure):
         ("replicated_s", ctypes.c_double),
         ("comm_s", ctypes.c_double),
         ("sharded_merges", ctypes.c_uint64),
+        ("tie_crosschecks", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -147,6 +148,7 @@ EXPORTS = (
     "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_create_dist_host", "zbpe_destroy", "zbpe_last_error",
     "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts", "zbpe_tokens",
     "zbpe_set_option", "zbpe_format_time_stats", "zbpe_bench_scan", "zbpe_bench_train_scan", "zbpe_merge_log", "zbpe_trace", "zbpe_scan_log", "zbpe_zig_order_winner", "zbpe_version",
+    "zbpe_stats_size",
 )
 MERGE_LOG_COLUMNS = ("key", "count", "live", "ties", "list_scan", "list_len", "key_live", "zero")
 TRACE_COLUMNS = ("merge", "count", "live", "slots", "streamed", "scan_ms", "replace_ms", "select_ms", "wall_ms",
@@ -224,8 +226,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_zig_order_winner.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
     L.zbpe_version.restype = ctypes.c_char_p
     for name in EXPORTS:
-        if name not in ("zbpe_destroy", "zbpe_last_error", "zbpe_version") and hasattr(L, name):
+        if name not in ("zbpe_destroy", "zbpe_last_error", "zbpe_version", "zbpe_stats_size") and hasattr(L, name):
             getattr(L, name).restype = ctypes.c_int
+    if hasattr(L, "zbpe_stats_size"):  # the caller-allocated zbpe_stats must match the library's layout
+        L.zbpe_stats_size.restype = ctypes.c_size_t
+        if L.zbpe_stats_size() != ctypes.sizeof(Stats):
+            raise ImportError(f"{path}: zbpe_stats is {L.zbpe_stats_size()} B, this binding's is {ctypes.sizeof(Stats)} B")
     _lib = L
     return L
 
