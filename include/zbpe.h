@@ -90,7 +90,9 @@ zbpe_status zbpe_create(int device, zbpe_ctx **out);
  * (e.g. with torch.distributed); every rank then calls zbpe_create_dist. The token stream is split
  * into `world` contiguous shards; pair-count deltas are summed with an RCCL all-reduce each merge
  * while scans stream the shards. When the occurrence lists take over, the ranks all-gather the
- * whole stream once and finish as replicas (no per-merge collective; option "replicate_late"). */
+ * whole stream once and finish as replicas (no per-merge collective; option "replicate_late").
+ * world == 1 with a unique id: a one-rank RCCL communicator, and the sharded code path with every
+ * collective (all-reduce of the count deltas, boundary all-gathers) runs over that one rank. */
 zbpe_status zbpe_comm_unique_id(void *out128);
 zbpe_status zbpe_create_dist(int device, int rank, int world, const void *unique_id128, zbpe_ctx **out);
 

@@ -59,6 +59,8 @@ def lib() -> ctypes.CDLL:
         L.zref_encode.restype = ctypes.c_int
         L.zref_decode.restype = ctypes.c_int
         L.zref_step.restype = ctypes.c_int
+        L.zref_train_log.restype = ctypes.c_int
+        L.zref_fnv64.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -177,6 +179,13 @@ def decode(merges: np.ndarray, tokens) -> bytes:
 def serialize(merges: np.ndarray) -> bytes:
     """serializeMerges (basic_tokenizer.zig:319-330): "{first},{second},{new_token}\\n" per merge."""
     return "".join(f"{int(a)},{int(b)},{int(c)}\n" for a, b, c in np.asarray(merges).reshape(-1, 3)).encode()
+
+
+def fnv64(tokens) -> int:
+    """FNV-1a 64 of a u16 token stream's little-endian bytes (the long-run goldens' stream checksum)."""
+    t = np.ascontiguousarray(np.asarray(tokens, dtype=np.uint16))
+    tt = t if len(t) else np.zeros(1, dtype=np.uint16)
+    return int(lib().zref_fnv64(_p(tt), ctypes.c_size_t(len(t))))
 
 
 def wyhash(seed: int, data: bytes) -> int:

@@ -42,7 +42,12 @@ def train_worker(rank, world, port, q, case):
         import zbpe
 
         dist = _init(rank, world, port)
-        text = case["text"] if "text" in case else zbpe.synth_corpus(case["kind"], case["seed"], case["n"])
+        if "text" in case:
+            text = case["text"]
+        elif "parts" in case:
+            text = b"".join(zbpe.synth_corpus(k, s, n) for k, s, n in case["parts"])
+        else:
+            text = zbpe.synth_corpus(case["kind"], case["seed"], case["n"])
         e = zbpe.Engine(0, rank=rank, world=world, collective=zbpe.torch_collective(rank, world))
         for k, v in case.get("options", {}).items():
             e.set_option(k, v)

@@ -38,15 +38,6 @@ RUNS = {
 FNV_EVERY = 64
 
 
-def fnv64(tokens: np.ndarray) -> int:
-    """FNV-1a 64 of the u16 stream's little-endian bytes (oracle zref_fnv64)."""
-    import oracle as O
-    L = O.lib()
-    L.zref_fnv64.restype = ctypes.c_uint64
-    t = np.ascontiguousarray(tokens, dtype=np.uint16)
-    return int(L.zref_fnv64(t.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(len(t))))
-
-
 def run(name: str, log: str, max_merges: int = 0) -> None:
     import oracle as O
     import zbpe
@@ -90,13 +81,15 @@ def convert(name: str, log: str) -> str:
                 ties.append(int(p[5]))
                 distinct.append(int(p[6]))
                 lens.append(int(p[7]))
+    import zbpe
+    corpus_sha = hashlib.sha256(zbpe.synth_corpus(kind, seed, n, threads=8)).hexdigest()
     complete = done is not None and done[0] == vocab - 256
     if done is not None and done[0] == len(merges):
         fnv = [x for x in fnv if x[0] != done[0]] + [done]
     out = {
         "source": "oracle/zig_ref.c zref_train_log (literal restatement of basic_tokenizer.zig:140-306), "
                   "tests/golden/make_golden_large.py",
-        "kind": kind, "seed": seed, "n": n, "vocab_size": vocab,
+        "kind": kind, "seed": seed, "n": n, "vocab_size": vocab, "corpus_sha256": corpus_sha,
         "complete": complete, "n_merges": len(merges),
         "merges": merges, "counts": counts, "ties": ties, "distinct": distinct, "len_after": lens,
         "fnv64_after": fnv,

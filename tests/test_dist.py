@@ -52,15 +52,32 @@ CASES = [
     # alike), and a global top count above the arena grows it on every rank (run-heavy: skewed counts)
     dict(kind="runs", seed=67, n=60000, vocab=450, options={"arena_cap": 3000, "replicate_late": 0}),
     dict(text=b"ab" * 20000 + b"xy" * 3000, vocab=320, options={"arena_cap": 12000, "replicate_late": 0}),
+    # skewed shards (rank 0 words, the rest random bytes): one shard's holes pile up while another's do not;
+    # compactions are decided on replicated totals, so the ranks' arena fills stay equal
+    dict(parts=[("words_utf8", 68, 150000), ("uniform", 69, 150000)], vocab=700, options={"arena_cap": 40000}),
+    dict(parts=[("words_utf8", 68, 150000), ("uniform", 69, 150000)], vocab=700,
+         options={"arena_cap": 40000, "replicate_late": 0, "list_start": 0}),
 ]
+
+
+def case_text(case) -> bytes:
+    if "text" in case:
+        return case["text"]
+    if "parts" in case:
+        return b"".join(zbpe.synth_corpus(k, s, n) for k, s, n in case["parts"])
+    return zbpe.synth_corpus(case["kind"], case["seed"], case["n"])
+
+
+def case_id(c) -> str:
+    name = c.get("kind", "parts" if "parts" in c else "text") + str(c.get("n", len(c.get("text", b""))))
+    return name + "".join(f"-{k}{v}" for k, v in c.get("options", {}).items())
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("case", CASES, ids=lambda c: c.get("kind", "text") + str(c.get("n", len(c.get("text", b""))))
-                         + "".join(f"-{k}{v}" for k, v in c.get("options", {}).items()))
+@pytest.mark.parametrize("case", CASES, ids=case_id)
 def test_sharded_training_matches_oracle(world, case):
-    text = case["text"] if "text" in case else zbpe.synth_corpus(case["kind"], case["seed"], case["n"])
+    text = case_text(case)
     ref = O.train(text, case["vocab"])
     out = run(train_worker, world, case)
     for r in range(world):
@@ -73,6 +90,42 @@ def test_sharded_training_matches_oracle(world, case):
     if case.get("replicated"):
         assert all(out[r][3]["replications"] == 1 for r in range(world))
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[9], CASES[-1]], ids=case_id)
+def test_one_rank_host_collective_runs_sharded_path(case):
+    """world 1 with a host collective: the sharded code path (every collective, over one rank)"""
+    text = case_text(case)
+    ref = O.train(text, case["vocab"])
+    out = run(train_worker, 1, case)
+    assert out[0][1] == ref.merges.tolist() and out[0][2] == ref.counts.tolist()
+    assert out[0][3]["sharded_merges"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("options", [{}, {"replicate_late": 0, "list_start": 0}, {"exact_ties": 1}],
+                         ids=["replicate_late", "sharded_to_the_end", "exact_ties"])
+def test_rccl_one_rank_communicator(options):
+    """A one-rank RCCL communicator (zbpe_create_dist, world 1): ncclAllReduce / ncclAllGather run on the
+    engine stream every merge (count deltas, boundaries, first occurrences, stream gather), merges equal
+    the oracle's; the full recount all-reduces through RCCL too"""
+    text = zbpe.synth_corpus("words_utf8", 71, 300000)
+    ref = O.train(text, 700)
+    e = zbpe.Engine(0, rank=0, world=1, unique_id=zbpe.comm_unique_id())
+    try:
+        for k, v in options.items():
+            e.set_option(k, v)
+        m, c, st = e.train(text, 700)
+        assert m.tolist() == ref.merges.tolist() and c.tolist() == ref.counts.tolist()
+        assert st.sharded_merges > 0
+        if not options.get("exact_ties"):  # (batched merges: the all-reduce's device time, from the timed merges)
+            assert st.comm_s > 0
+        if options.get("replicate_late", 1) and not options.get("exact_ties"):
+            assert st.replications == 1
+        assert e.verify_counts() == 0
+    finally:
+        e.close()
 
 
 @pytest.mark.gpu

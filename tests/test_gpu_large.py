@@ -1,24 +1,33 @@
 """Parity at the BASELINE.json sizes (C3, C4, C5) on the MI355X.
 
-A full oracle run of C3/C4 is out of reach on the CPU (the reference recounts every pair of the
-stream per merge: hours to days), so each check is one reference loop iteration on the device's own
-state: train to 256 + k merges, download the device's token stream (zbpe_tokens) and ask the oracle
-what expandVocabulary would merge next on it (oracle.step = basic_tokenizer.zig:183-204 once:
-count in the Zig map, slot order, stable sort, [0]). That must be the full run's merge k + 1 with
-its count. Together with "the first k merges of a run to 256 + k equal the full run's" this checks
-merge k + 1 against the reference at the sampled k, on the real C4 stream, ties included.
+Unconditional, full-sequence goldens (tests/golden/large_*.json, made by make_golden_large.py: the
+literal oracle run from the raw bytes in the build container):
+  - C3 (64 MiB, V=4096): all 3,840 merges, their counts and the final stream's FNV-64;
+  - C4 (1 GiB, V=32000): the first K merges (the oracle's prefix, ~3-9 s per literal iteration on the
+    1 GiB stream), and the stream's FNV-64 after a checkpoint merge.
+Exact tie cross-checks: every C3 tie, and a window of >= 50 consecutive late C4 merges, decided by
+both the device's cluster test and the exact Zig-map emulation (options exact_ties /
+exact_ties_from / exact_ties_to); a disagreement fails the train.
+
+Conditional samples at any merge of C4: train to 256 + k merges, download the device's token
+stream (zbpe_tokens) and ask the oracle what expandVocabulary would merge next on it (oracle.step =
+basic_tokenizer.zig:183-204 once: count in the Zig map, slot order, stable sort, [0]). That must be
+the full run's merge k + 1 with its count.
 
 Size-independent properties at full size: the incremental counts equal a full recount of the final
 stream (zbpe_verify_counts), encode(corpus) reproduces the training stream, decode(encode(x)) == x.
 C5: encode with all 31,744 C4 merges against the oracle's encode on a 1 MiB slice of the C5 text.
 """
 import hashlib
+import json
+import os
 
 import numpy as np
 import pytest
 
 import oracle as O
 import zbpe
+from helpers import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
@@ -36,6 +45,8 @@ class Run:
         fin = self.e.tokens()
         self.final_len = len(fin)
         self.final_sha = hashlib.sha256(fin.tobytes()).hexdigest()
+        self.final_fnv = O.fnv64(fin)
+        self.text_sha = hashlib.sha256(self.text).hexdigest()
         del fin
 
     def check_step(self, k):
@@ -54,6 +65,18 @@ class Run:
 
     def close(self):
         self.e.close()
+
+
+def large_golden(name: str) -> dict:
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def check_vs_golden(run: Run, g: dict, k: int):
+    """the run's first k merges and counts == the oracle's (unconditional: both from the raw bytes)"""
+    assert run.text_sha == g["corpus_sha256"], "corpus generator changed"
+    assert run.merges[:k].astype(int).tolist() == g["merges"][:k]
+    assert run.counts[:k].astype(int).tolist() == g["counts"][:k]
 
 
 def decode_np(merges: np.ndarray, tokens: np.ndarray) -> bytes:
@@ -107,6 +130,38 @@ def test_c4_full_run_properties(c4):
     assert c4.stats.final_tokens == c4.final_len
 
 
+C4_GOLDEN = "large_c4_words_utf8_1GiB_v32000_prefix.json"
+C3_GOLDEN = "large_c3_words_utf8_64MiB_v4096.json"
+
+
+def test_c4_prefix_vs_oracle_golden(c4):
+    """the first K merges of C4 (the oracle's literal run from the 1 GiB of bytes) bit-exact, ties
+    included, and the device stream after the last checkpoint equal to the oracle's (FNV-64)"""
+    g = large_golden(C4_GOLDEN)
+    K = g["n_merges"]
+    assert K >= 500
+    check_vs_golden(c4, g, K)
+    k, ln, fnv = [x for x in g["fnv64_after"] if x[0] <= K][-1]
+    m, c, st = c4.e.train_resident(256 + k)
+    tok = c4.e.tokens()
+    assert len(tok) == ln and O.fnv64(tok) == int(fnv, 16)
+
+
+def test_c4_late_ties_exact_window(c4):
+    """>= 50 consecutive late C4 tie decisions (merges 25,000-25,069) taken by both the device's
+    cluster test and the exact Zig-map emulation (first occurrences of all ~4e7 live pairs); a
+    disagreement fails the train; the merges equal the production run's"""
+    e = c4.e
+    e.set_option("exact_ties_from", 25000)
+    e.set_option("exact_ties_to", 25070)
+    try:
+        m, c, st = e.train_resident(32000)
+    finally:
+        e.set_option("exact_ties_to", 0)
+    assert np.array_equal(m, c4.merges) and np.array_equal(c, c4.counts)
+    assert st.tie_crosschecks == st.tie_fallbacks >= 50
+
+
 @pytest.mark.parametrize("k", [0, 1, 2, 100, 1000, 1400, 2500, 5000, 10000, 15000, 20000, 25000, 31000, 31743])
 def test_c4_oracle_step(c4, k):
     c4.check_step(k)
@@ -143,6 +198,30 @@ def test_c3_full_run_properties(c3):
     # the first merge against the oracle's count of the whole 64 MiB byte stream
     r = O.step(np.frombuffer(c3.text, np.uint8).astype(np.uint16))
     assert (r.pair, r.count) == ((int(c3.merges[0, 0]), int(c3.merges[0, 1])), int(c3.counts[0]))
+
+
+def test_c3_full_sequence_vs_oracle_golden(c3):
+    """all 3,840 C3 merges and counts equal the oracle's literal run from the 64 MiB of bytes, and the
+    final stream equals the oracle's (FNV-64 and length)"""
+    g = large_golden(C3_GOLDEN)
+    assert g["complete"] and g["n_merges"] == 3840
+    check_vs_golden(c3, g, 3840)
+    k, ln, fnv = g["fnv64_after"][-1]
+    assert k == 3840 and c3.final_len == ln and c3.final_fnv == int(fnv, 16)
+
+
+def test_c3_every_tie_exact(c3):
+    """every C3 tie (1,221) decided by both the cluster test and the exact Zig-map emulation"""
+    g = large_golden(C3_GOLDEN)
+    e = c3.e
+    e.set_option("exact_ties", 1)
+    try:
+        m, c, st = e.train_resident(4096)
+    finally:
+        e.set_option("exact_ties", 0)
+    assert np.array_equal(m, c3.merges) and np.array_equal(c, c3.counts)
+    tied = sum(t > 1 for t in g["ties"])
+    assert st.tie_iterations == st.tie_fallbacks == st.tie_crosschecks == tied > 1000
 
 
 @pytest.mark.parametrize("k", [1, 37, 500, 2000, 3839])

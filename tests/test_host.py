@@ -56,6 +56,41 @@ def test_zig_order_emulator_matches_oracle():
             _zig_check(r.tokens)
 
 
+@pytest.mark.parametrize("threads", [2, 4, 8, 16])
+def test_zig_order_parallel_levels_match(monkeypatch, threads):
+    """The parallel level builder (segments cut at slots empty in the final table, zig_order.hpp) gives the
+    same Zig order as the one-thread replay: real streams against the oracle's map (every level parallel),
+    and random live sets with many ties, each winner checked against the sequential build."""
+    monkeypatch.setenv("ZBPE_EMU_THREADS", str(threads))
+    monkeypatch.setenv("ZBPE_EMU_PAR_MIN", "0")
+    _zig_check(list(c1_text()))
+    g = [x for x in synth_goldens() if x["kind"] == "words_utf8"][0]
+    _zig_check(O.train(synth_text(g), 300).tokens)
+    rng = np.random.default_rng(threads)
+    for n, call_after in ((5000, False), (200000, True), (419430, False), (419430, True)):  # 419430 = max load of 2^19
+        keys = rng.choice(1 << 31, size=n, replace=False).astype(np.uint32)
+        first = rng.permutation(n).astype(np.uint32)
+        counts = rng.integers(1, 40, size=n).astype(np.uint32)
+        top = 39
+        monkeypatch.setenv("ZBPE_EMU_PAR_MIN", "0")
+        par = zbpe.zig_order_winner(first, keys, counts, top, call_after)
+        monkeypatch.setenv("ZBPE_EMU_PAR_MIN", str(1 << 40))
+        seq = zbpe.zig_order_winner(first, keys, counts, top, call_after)
+        assert par == seq
+
+
+def test_zig_order_parallel_level_tables_equal(tmp_path):
+    """tests/model/zig_emu_check.cpp: the parallel level builder's table equals the one-thread replay's,
+    slot for slot (random sequences, loads 30-80 %, 2-16 threads)"""
+    import subprocess
+
+    exe = tmp_path / "zig_emu_check"
+    src = os.path.join(ROOT, "tests", "model", "zig_emu_check.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-o", str(exe), src], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_synth_corpus_deterministic():
     a = zbpe.synth_corpus("words_utf8", 5, 3 << 20, threads=1)
     b = zbpe.synth_corpus("words_utf8", 5, 3 << 20, threads=7)

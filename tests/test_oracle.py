@@ -212,3 +212,29 @@ def test_list_neighbour_filter_invariant(corpus):
 
     _apply_merges_with_holes(text, merges, on_merge)
     assert checked[0] > 1000
+
+
+def test_large_goldens_are_the_oracles_runs():
+    """tests/golden/large_*.json (full-sequence C3 and the C4 prefix, made by make_golden_large.py) are
+    the oracle's literal runs: their first merges recomputed here, and their internal invariants."""
+    import json
+    import os
+
+    import zbpe
+    from helpers import GOLDEN
+
+    for name, first in (("large_c3_words_utf8_64MiB_v4096.json", 6), ("large_c4_words_utf8_1GiB_v32000_prefix.json", 0)):
+        with open(os.path.join(GOLDEN, name)) as f:
+            g = json.load(f)
+        m, c, ln = g["merges"], g["counts"], g["len_after"]
+        assert len(m) == len(c) == len(ln) == len(g["ties"]) == g["n_merges"] > 0
+        assert [x for _, _, x in m] == list(range(256, 256 + len(m)))
+        assert all(c[i] >= c[i + 1] for i in range(len(c) - 1))
+        prev = g["n"]
+        for (a, b, _), cnt, after in zip(m, c, ln):  # a merge removes one token per occurrence
+            assert after == prev - cnt if a != b else prev - cnt <= after < prev  # (a, a): overlapping counts
+            prev = after
+        if first:
+            text = zbpe.synth_corpus(g["kind"], g["seed"], g["n"])
+            r = O.train(text, 256 + first)
+            assert r.merges.astype(int).tolist() == m[:first] and r.counts.astype(int).tolist() == c[:first]

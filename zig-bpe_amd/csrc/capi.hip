@@ -33,6 +33,7 @@ zbpe_status zbpe_create(int device, zbpe_ctx **out) {
     }
     if (env_or("ZBPE_DEBUG")) c->eng.debug_checks = true;
     if (env_or("ZBPE_EXACT_TIES")) c->eng.force_exact_ties = true;
+    if (env_or("ZBPE_TIE_PROF")) c->eng.tie_prof = true;
     if (const char *v = env_or("ZBPE_COMPACT_DEN")) c->eng.compact_den = strtoull(v, nullptr, 10);
     if (const char *v = env_or("ZBPE_SCAN_BLOCKS_PER_CU")) c->eng.scan_blocks_per_cu = atoi(v);
     *out = c;
@@ -56,9 +57,10 @@ static zbpe_status finish_dist(zbpe_ctx *c, int rank, int world, std::unique_ptr
 zbpe_status zbpe_create_dist(int device, int rank, int world, const void *unique_id128, zbpe_ctx **out) {
     if (!out || world < 1 || rank < 0 || rank >= world || (world > 1 && !unique_id128)) return ZBPE_INVALID_ARGUMENT;
     zbpe_status s = zbpe_create(device, out);
-    if (s != ZBPE_OK || world == 1) return s;
+    if (s != ZBPE_OK || (world == 1 && !unique_id128)) return s;
     auto comm = std::make_unique<zbpe::RcclComm>();
     if (!comm->init(rank, world, unique_id128)) return (*out)->eng.fail(ZBPE_COMM_ERROR, "ncclCommInitRank failed (rank %d of %d)", rank, world);
+    (*out)->eng.force_shard = world == 1;  // a one-rank communicator: the sharded path, over one rank
     return finish_dist(*out, rank, world, std::move(comm), out);
 }
 
@@ -71,6 +73,7 @@ zbpe_status zbpe_create_dist_host(int device, int rank, int world, zbpe_collecti
     comm->user = user;
     comm->rank = rank;
     comm->world = world;
+    (*out)->eng.force_shard = world == 1;
     return finish_dist(*out, rank, world, std::move(comm), out);
 }
 
@@ -80,7 +83,7 @@ const char *zbpe_last_error(const zbpe_ctx *ctx) { return ctx ? ctx->eng.err.c_s
 
 zbpe_status zbpe_upload(zbpe_ctx *ctx, const uint8_t *text, size_t n) {
     if (!ctx || (!text && n)) return ZBPE_INVALID_ARGUMENT;
-    return ctx->eng.upload(text, n, ctx->eng.world > 1);
+    return ctx->eng.upload(text, n, ctx->eng.multi());
 }
 
 zbpe_status zbpe_train_resident(zbpe_ctx *ctx, uint16_t vocab_size, int verbose, uint16_t *out_triples,
@@ -94,7 +97,7 @@ zbpe_status zbpe_train(zbpe_ctx *ctx, const uint8_t *text, size_t n, uint16_t vo
     if (!ctx || !out_n_merges || (!text && n)) return ZBPE_INVALID_ARGUMENT;
     *out_n_merges = 0;
     if (vocab_size < 256) return ctx->eng.fail(ZBPE_INVALID_VOCAB_SIZE, "vocabSize %u < 256", vocab_size);
-    zbpe_status s = ctx->eng.upload(text, n, ctx->eng.world > 1);
+    zbpe_status s = ctx->eng.upload(text, n, ctx->eng.multi());
     if (s != ZBPE_OK) return s;
     return zbpe_train_resident(ctx, vocab_size, verbose, out_triples, out_counts, out_n_merges, stats);
 }

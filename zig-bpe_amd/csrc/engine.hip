@@ -255,6 +255,7 @@ zbpe_status Engine::compact() {
     LAUNCH_OK();
     cur ^= 1;
     n_slots = n_live;
+    if (dist()) global_slots = global_live;  // every rank compacts together (holes_over)
     stats.compactions++;
     CHECK(build_presence());
     if (debug_checks) {
@@ -269,11 +270,23 @@ zbpe_status Engine::compact() {
 
 // Compaction during training: positions move, so the occurrence lists are rebuilt (once they are
 // on, or once pair counts have become small against the stream), else the arena is emptied.
+// Hole-ratio compaction trigger. One GPU (and replicas): this stream's holes. Sharded: the holes of all
+// shards from replicated totals, so every rank compacts at the same merge -- a compaction resets the
+// arena fill (arena_rep) and may rebuild the lists, both of which gate halts and collectives
+// (a rank-local trigger let one rank's arena_rep drift from the others').
+bool Engine::holes_over() const {
+    const uint64_t den = lists_on ? compact_den_lists : compact_den;
+    if (!dist()) return (uint64_t)(n_slots - n_live) * den > (uint64_t)n_slots;
+    return (global_slots - global_live) * den > global_slots;
+}
+
 zbpe_status Engine::compact_train(uint32_t X) {
     HIP_OK(hipEventRecord(ev[3], stream));
     CHECK(compact());
+    // sharded: on replicated quantities (every rank compacts here, at the same merge)
+    const uint64_t live_ref = dist() ? global_live : (uint64_t)n_live, ranks = dist() ? (uint64_t)world : 1;
     const bool want = list_mode && pres_vp <= PRES_MAX_VP && (uint64_t)n_slots < 0xF0000000ull &&
-                      (lists_on || list_start == 0 || (uint64_t)h_st->top_count * list_start < (uint64_t)n_live);
+                      (lists_on || list_start == 0 || (uint64_t)h_st->top_count * list_start * ranks < live_ref);
     if (want && !(dist() && replicate_late)) {  // sharded: lists come with the replication (run_batch)
         CHECK(build_lists(X, list_ratio));
     } else {
@@ -357,9 +370,30 @@ zbpe_status Engine::grow_arena(uint64_t need) {
     return ZBPE_OK;
 }
 
+// max over the ranks of a u32 (an all-reduce(min) of its complement); the value itself on one GPU
+zbpe_status Engine::max_over_ranks(uint32_t v, uint32_t *out) {
+    if (!dist()) { *out = v; return ZBPE_OK; }
+    uint32_t *d_w = d_delta + DELTA_WORDS - 8;  // scratch words past the delta layout
+    const uint32_t c = ~v;
+    HIP_OK(hipMemcpyAsync(d_w, &c, 4, hipMemcpyHostToDevice, stream));
+    if (!comm->allreduce_u32(d_w, 1, COMM_MIN_U32, stream)) return fail(ZBPE_COMM_ERROR, "all-reduce(min) failed");
+    uint32_t r = 0;
+    HIP_OK(hipMemcpyAsync(&r, d_w, 4, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    HIP_OK(hipMemsetAsync(d_w, 0, 4, stream));
+    *out = ~r;
+    return ZBPE_OK;
+}
+
 zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio) {
     const int64_t n = n_slots;
-    if ((uint64_t)n + (1u << 20) > lists_cap) CHECK(grow_arena((uint64_t)n + (16u << 20)));  // lists <= n entries
+    if (dist()) {  // (sharded, replicate_late off) the arena limit stays replicated: grown from the largest shard
+        uint32_t nmax = 0;
+        CHECK(max_over_ranks((uint32_t)n, &nmax));
+        if ((uint64_t)nmax + (1u << 20) > arena_cap_rep) CHECK(grow_arena((uint64_t)nmax + (16u << 20)));
+    } else if ((uint64_t)n + (1u << 20) > lists_cap) {
+        CHECK(grow_arena((uint64_t)n + (16u << 20)));  // lists <= n entries
+    }
     const uint32_t nchunks = (uint32_t)std::max<int64_t>(1, (n + LIST_CHUNK - 1) / LIST_CHUNK);
     CHECK(ensure(&d_list_cnt, list_cnt_cap, (size_t)nchunks * pres_vp, "list chunk histograms"));
     zbpe_list_hist<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt);
@@ -375,6 +409,13 @@ zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio) {
     zbpe_list_scatter<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt, T.lst_off,
                                                                        T.lst_len, d_lists, list_nb ? d_nb : nullptr);
     LAUNCH_OK();
+    if (dist()) {  // arena_rep (the replicated fill that halts are decided on) >= every rank's arena_top
+        CHECK(sync_state());
+        uint32_t top_max = 0;
+        CHECK(max_over_ranks(h_st->arena_top, &top_max));
+        const uint32_t rep = std::max(top_max, h_st->arena_rep);
+        HIP_OK(hipMemcpyAsync(&d_st->arena_rep, &rep, 4, hipMemcpyHostToDevice, stream));
+    }
     lists_on = true;
     nb_built = list_nb;
     pres_on = false;  // block skipping is not maintained once scans can bypass the stream
@@ -545,8 +586,8 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     // exact emulation from first-occurrence order
     stats.tie_fallbacks++;
     CHECK(ensure(&d_first, first_cap, nid, "first occurrences"));
-    CHECK(ensure(&d_gather, gather_cap, (size_t)D, "live pairs"));
     HIP_OK(hipMemsetAsync(d_first, 0xFF, (size_t)nid * 4, stream));
+    const double tp0 = now_s();
     HIP_OK(hipMemsetAsync(&d_st->gather_len, 0, 4, stream));
     {
         ScanArgs A{d_tok[cur], n_slots, 0, 0, nullptr, nullptr, d_st, nullptr, 0, 0, nullptr, nullptr, halo};
@@ -564,6 +605,7 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
                                                                                         (uint32_t)(D + 1));
         LAUNCH_OK();
         CHECK(sync_state());
+        const double tp1 = now_s();
         const uint32_t g = h_st->gather_len;
         if (g != D) return fail(ZBPE_INTERNAL, "gathered %u live pairs, expected %llu", g, (unsigned long long)D);
         int end_bit = 1;
@@ -581,9 +623,14 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
         }
         HIP_OK(hipMemcpyAsync(h_ord, ent_out, (size_t)g * 8, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
-        if (!zig_emulate_first_tied(h_ord, g, call_after, winner))
+        const double tp2 = now_s();
+        if (!zig_emulate_first_tied(h_ord, g, call_after, winner, emu_work))
             return fail(ZBPE_INTERNAL, "exact tie emulation found no pair with count %u", top);
+        if (tie_prof)
+            fprintf(stderr, "tie_prof: %u live pairs, %u tied: first occurrences + gather %.1f ms, sort + copy %.1f ms, "
+                            "host emulation %.1f ms\n", g, ties, (tp1 - tp0) * 1e3, (tp2 - tp1) * 1e3, (now_s() - tp2) * 1e3);
     } else {
+    CHECK(ensure(&d_gather, gather_cap, (size_t)D, "live pairs"));
     zbpe_gather_live<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_first, d_st, d_gather, (uint32_t)gather_cap);
     LAUNCH_OK();
     CHECK(sync_state());
@@ -696,7 +743,7 @@ zbpe_status Engine::bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms,
 // form when its list is short), with the per-merge counters and deltas reset between launches. The
 // stream, the lists and the counts are left as they were (records land past the arena top).
 zbpe_status Engine::bench_train_scan(int reps, int grid, double *avg_us, uint32_t *pair, uint32_t *list_len, int *mode) {
-    if (!trained || world > 1) return fail(ZBPE_INVALID_ARGUMENT, "bench_train_scan needs a trained single-GPU context");
+    if (!trained || multi()) return fail(ZBPE_INVALID_ARGUMENT, "bench_train_scan needs a trained single-GPU context");
     HIP_OK(hipSetDevice(device));
     CHECK(sync_state());
     const uint32_t key = h_st->top_key, a = key & 0xFFFF, b = key >> 16, X = 256 + (uint32_t)run.merges;
@@ -808,7 +855,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     *out_n_merges = 0;
     if (vocab_size < 256) return fail(ZBPE_INVALID_VOCAB_SIZE, "vocabSize %u < 256", vocab_size);
     if (!uploaded) return fail(ZBPE_INVALID_ARGUMENT, "no corpus uploaded");
-    if (!sharded && world > 1) return fail(ZBPE_INVALID_ARGUMENT, "distributed context: upload the corpus with zbpe_upload");
+    if (!sharded && multi()) return fail(ZBPE_INVALID_ARGUMENT, "distributed context: upload the corpus with zbpe_upload");
     HIP_OK(hipSetDevice(device));
     const size_t n = n_text;
     double ev_count = 0, ev_select = 0, ev_replace = 0;
@@ -847,6 +894,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     replicated = false;
     sum_tokens_rep = 0;
     global_live = sharded ? n_total : n;
+    global_slots = global_live;
     if (T.home_cnt) { (void)hipFree(T.home_cnt); T.home_cnt = nullptr; home_words_cap = 0; }
     if (T.home_dirty) { (void)hipFree(T.home_dirty); T.home_dirty = nullptr; dirty_bits_cap = 0; }
     hot_stale = true;
@@ -870,7 +918,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         LAUNCH_OK();
         HIP_OK(hipMemsetAsync(d_delta, 0, 2 * 65536 * 4, stream));
     }
-    if (world > 1) {  // boundary tokens of every shard (the first select needs the stream's last pair)
+    if (multi()) {  // boundary tokens of every shard (the first select needs the stream's last pair)
         zbpe_boundary<<<1, 1, 0, stream>>>(d_tok[cur], n_slots, n_live, d_bnd_mine, nullptr);
         LAUNCH_OK();
         if (!comm->allgather(d_bnd_mine, d_bnd_all, sizeof(Boundary), stream))
@@ -949,7 +997,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     stats.sort_pairs_s = ev_select;
     stats.replace_pair_s = ev_replace;
     stats.final_tokens = (uint64_t)n_live;
-    if (world > 1) {  // stream lengths are per shard: sum them (scan bytes stay per rank, like scan time)
+    if (multi()) {  // stream lengths are per shard: sum them (scan bytes stay per rank, like scan time)
         // the replicated phase counted the whole stream on every rank: rank 0 contributes it once
         uint64_t v[2] = {replicated ? (rank == 0 ? stats.final_tokens : 0) : stats.final_tokens,
                          stats.sum_tokens - sum_tokens_rep + (rank == 0 ? sum_tokens_rep : 0)};
@@ -1039,9 +1087,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     CHECK(maybe_grow_tables(X0, K));
     if (hot_stale) CHECK(rebuild_hot());  // a table rebuild renumbered the ids the tie kernels read
     const uint32_t top0 = h_st->top_count;
-    if ((uint64_t)(n_slots - n_live) * (lists_on ? compact_den_lists : compact_den) > (uint64_t)n_slots ||
-        arena_used() + (uint64_t)K * top0 > arena_limit())
-        CHECK(compact_train(X0));
+    if (holes_over() || arena_used() + (uint64_t)K * top0 > arena_limit()) CHECK(compact_train(X0));
     CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
     // the refresh counts of zbpe_select_next: each launch zeroes the next one's, unless this batch
     // does not continue the last one's launches
@@ -1336,7 +1382,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     const uint64_t gone = h_st->last_holes;  // slots of this shard that became holes
     n_live -= gone;
     (void)gone;
-    if ((uint64_t)(n_slots - n_live) * (lists_on ? compact_den_lists : compact_den) > (uint64_t)n_slots) CHECK(compact_train(X + 1));
+    if (holes_over()) CHECK(compact_train(X + 1));
     return ZBPE_OK;
 }
 

@@ -10,6 +10,7 @@
 #include "../../include/zbpe.h"
 #include "comm.hpp"
 #include "types.hpp"
+#include "zig_order.hpp"
 
 namespace zbpe { struct ScanArgs; }
 
@@ -56,9 +57,14 @@ struct Engine {
     uint64_t sum_tokens_rep = 0;     // stats.sum_tokens accumulated while replicated (counted once)
     uint64_t n_total = 0;            // corpus bytes over all ranks
     uint64_t global_live = 0;        // live tokens over all ranks (host-tracked from the merged counts)
+    uint64_t global_slots = 0;       // stream slots over all ranks (changes at compactions, which are global)
     uint32_t *d_sizes = nullptr;     // [2 * world + 2] live-token counts of the shards
     size_t sizes_cap = 0;
-    bool dist() const { return world > 1 && !replicated; }
+    // a one-rank communicator (zbpe_create_dist with world 1 and a unique id, or a host callback) runs the
+    // sharded code path too: every collective of a multi-GPU run executes, over one rank
+    bool force_shard = false;
+    bool multi() const { return world > 1 || force_shard; }
+    bool dist() const { return multi() && !replicated; }
     uint64_t shard_offset = 0;  // global position of the shard's first byte
     int next_byte = -1;         // first byte of the next shard (-1: none)
     Halo halo0{}, halo{};
@@ -90,6 +96,8 @@ struct Engine {
     size_t ord_pos_cap = 0, ord_ent_cap = 0, sort_tmp_cap = 0;
     uint64_t *h_ord = nullptr;  // pinned
     size_t h_ord_cap = 0;
+    ZigEmuWork emu_work;        // the host emulation's tables, kept between ties
+    bool tie_prof = false;      // env ZBPE_TIE_PROF: phase times of every exact tie emulation on stderr
     uint32_t *d_recount = nullptr;
     size_t recount_cap = 0;
     uint32_t *d_count_hist = nullptr, *h_count_hist = nullptr;
@@ -223,6 +231,8 @@ struct Engine {
     zbpe_status build_presence();
     zbpe_status compact();
     zbpe_status compact_train(uint32_t X);
+    bool holes_over() const;
+    zbpe_status max_over_ranks(uint32_t v, uint32_t *out);
     zbpe_status grow_arena(uint64_t need);
     zbpe_status build_lists(uint32_t lists_x, uint32_t ratio);
     void set_list_nb(ScanArgs &A) const;

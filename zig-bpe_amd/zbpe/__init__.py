@@ -246,11 +246,12 @@ class Engine:
     def __init__(self, device: int = 0, rank: int = 0, world: int = 1, unique_id: Optional[bytes] = None,
                  collective=None):
         """world > 1: RCCL with `unique_id` (from comm_unique_id() on rank 0), or a host `collective`
-        (torch_collective(rank, world)) so several ranks can share one GPU."""
+        (torch_collective(rank, world)) so several ranks can share one GPU. world == 1 with a unique_id or a
+        collective: a one-rank communicator that runs the sharded code path (tests)."""
         self._L = load_library()
         self._ctx = ctypes.c_void_p()
         self._collective = collective  # keep the callback alive
-        if world == 1 and collective is None:
+        if world == 1 and collective is None and unique_id is None:
             st = self._L.zbpe_create(device, ctypes.byref(self._ctx))
         elif collective is not None:
             st = self._L.zbpe_create_dist_host(device, rank, world, collective, None, ctypes.byref(self._ctx))
