@@ -51,6 +51,10 @@ def parse():
                    help="write the probe train's per-launch scan log + per-merge live tokens (tools/pmc_traffic.py, tools/scan_forms.py)")
     p.add_argument("--share-gpu", action="store_true",
                    help="all ranks on cuda:0 with host (gloo) collectives -- rehearses N>1 on one GPU")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the other BASELINE configs (C1/C2 CPU+GPU, C3 train, C5 encode) and the incremental CPU model")
+    p.add_argument("--inc-merges", type=int, default=4,
+                   help="cpu_incremental: merges of C4 timed with tests/model/inc_model.cpp")
     return p.parse_args()
 
 
@@ -113,6 +117,112 @@ def cpu_baseline(eng, text: bytes, vocab: int, live, late_k: int):
         "extrapolated_full_job_s": full_s,
         "_pairs": (r0.pair, r1.pair),
     }
+
+
+def cpu_incremental(text: bytes, gpu_merges, k: int):
+    """Algorithm-matched CPU figure: tests/model/inc_model.cpp (the device's incremental counting, one
+    core, g++ -O3; a pass over the stream per merge finds the occurrences) on the C4 corpus for the
+    first k merges, next to the literal port's per-merge cost (cpu_baseline)."""
+    import subprocess
+    import tempfile
+
+    src = os.path.join(ROOT, "tests", "model", "inc_model.cpp")
+    with tempfile.TemporaryDirectory() as d:
+        exe, corpus = os.path.join(d, "inc_model"), os.path.join(d, "corpus.bin")
+        subprocess.run(["g++", "-O3", "-std=c++17", "-o", exe, src], check=True)
+        with open(corpus, "wb") as f:
+            f.write(text)
+        t = time.perf_counter()
+        r = subprocess.run([exe, corpus, "32000", "0", str(k)], capture_output=True, text=True, check=True)
+        wall = time.perf_counter() - t
+    timing = dict(kv.split("=") for kv in r.stderr.split("timing:")[1].split("\n")[0].split())
+    merges = [tuple(int(v) for v in line.split(",")) for line in r.stdout.split()]
+    agrees = [list(x) for x in merges] == [list(map(int, row)) for row in gpu_merges[: len(merges)]]
+    init_s, merges_s = float(timing["init_s"]), float(timing["merges_s"])
+    return {"value": len(merges) / merges_s if merges_s > 0 else None, "unit": "merges/s", "cores": 1,
+            "kind": "incremental model (tests/model/inc_model.cpp, g++ -O3)", "merges": len(merges),
+            "init_s": init_s, "merges_s": merges_s, "wall_s": wall, "agrees_with_gpu": bool(agrees),
+            "sample": f"the first {len(merges)} merges of C4 ({len(text)} B): incremental counts, one stream pass per merge"}
+
+
+def histogram_roofline(eng, late: int, reps: int = 5):
+    """The north-star's full pair-histogram kernel (zbpe_pair_hist: every adjacent pair of the stream,
+    LDS-staged per workgroup; the recount behind verify_counts), timed with HIP events at t = 0 (the
+    widened 1 GiB stream, ~3.6e3 distinct pairs) and after `late` merges (~5e7 distinct pairs: most pairs
+    miss the LDS tables and pay a global lookup). Algorithmic bytes: 2 B per token."""
+    out = {}
+    for name, v in (("t0", 256), (f"after_{late}", 256 + late)):
+        eng.train_resident(v)
+        r = eng.bench_recount(reps)
+        out[name] = {"kernel": "zbpe_pair_hist", "bound": "hbm", "achieved": r["GBps"], "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": r["GBps"] / HBM_PEAK_GBPS, "avg_launch_us": r["us"], "tokens": r["tokens"],
+                     "alg_bytes_per_launch": 2 * r["tokens"], "counts_match_incremental": r["mismatches"] == 0}
+    return out
+
+
+def extra_configs(zbpe, eng, c4_merges, args):
+    """The other BASELINE.json configs, under the same clock (rank 0, one GPU):
+      c1: taylorswift.txt, V=300 -- the oracle (CPU, full run) and the GPU, merges compared
+      c2: 1 MiB synthetic ASCII, V=512 -- the same
+      c3: 64 MiB UTF-8 synthetic, V=4096 -- GPU merges/s and the stream-form scan GB/s (its 128 MiB u16
+          stream fits the 256 MiB Infinity Cache: L3-resident, not an HBM figure)
+      c5: encode 100 M chars with the C4 merges -- chars/s (host buffers in and out, PCIe included), and
+          a 200 kB prefix against the oracle's encode"""
+    import gzip
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    out = {}
+    with gzip.open(os.path.join(ROOT, "tests", "golden", "c1_taylorswift.txt.gz"), "rb") as f:
+        c1 = f.read()
+    c2 = zbpe.synth_corpus("words", 0x5EED0002, 1 << 20)
+    for name, text, vocab in (("c1", c1, 300), ("c2", c2, 512)):
+        t = time.perf_counter()
+        ref = oracle.train(text, vocab)
+        cpu_s = time.perf_counter() - t
+        eng.train(text, vocab)  # warm
+        t = time.perf_counter()
+        m, c, st = eng.train(text, vocab)
+        gpu_s = time.perf_counter() - t
+        out[name] = {"bytes": len(text), "vocab_size": vocab, "merges": int(len(m)),
+                     "cpu_oracle_s": cpu_s, "gpu_train_s": gpu_s,
+                     "bit_exact": bool(np.array_equal(m, ref.merges) and np.array_equal(c, ref.counts)),
+                     "note": "gpu_train_s: zbpe_train with the host buffer (upload included); cpu: the oracle, 1 thread"}
+    c3 = zbpe.synth_corpus("words_utf8", 0x5EED0003, 64 << 20, threads=16)
+    eng.upload(c3)
+    eng.train_resident(4096)
+    times = []
+    for _ in range(3):
+        t = time.perf_counter()
+        m3, c3c, st3 = eng.train_resident(4096)
+        times.append(time.perf_counter() - t)
+    eng.set_option("timing_full", 1)
+    _, _, sp = eng.train_resident(4096)
+    eng.set_option("timing_full", 0)
+    gbps = sp.scan_timed_alg_bytes / sp.scan_kernel_s / 1e9 if sp.scan_kernel_s > 0 else 0.0
+    out["c3"] = {"bytes": len(c3), "vocab_size": 4096, "merges": int(len(m3)), "value": len(m3) / min(times),
+                 "unit": "merges/s", "best_s": min(times),
+                 "stream_scan_GBps": gbps, "stream_scan_launches_timed": int(sp.scan_timed_launches),
+                 "stream_scan_note": "L3-resident: the 128 MiB u16 stream fits the 256 MiB Infinity Cache",
+                 "ties": int(st3.tie_iterations)}
+    del c3
+    c5 = zbpe.synth_corpus("words_utf8", 0x5EED0005, 100_000_000, threads=16)
+    eng.encode(c4_merges, c5[: 1 << 20])  # warm
+    times = []
+    enc = None
+    for _ in range(2):
+        t = time.perf_counter()
+        enc = eng.encode(c4_merges, c5)
+        times.append(time.perf_counter() - t)
+    pre = c5[:200_000]
+    out["c5"] = {"chars": len(c5), "merges": int(len(c4_merges)), "value": len(c5) / min(times), "unit": "chars/s",
+                 "best_s": min(times), "tokens_out": int(len(enc)),
+                 "prefix_equals_oracle": bool(np.array_equal(eng.encode(c4_merges, pre), oracle.encode(c4_merges, pre))),
+                 "prefix_bytes": len(pre), "note": "zbpe_encode with host buffers in and out (PCIe included)"}
+    return out
 
 
 def probe_roofline(eng, vocab: int, scan_log_out: str):
@@ -294,8 +404,14 @@ def main():
             cb["oracle_agrees_with_gpu"] = bool(p0 == tuple(int(v) for v in m[0, :2]) and
                                                 (k >= len(m) or p1 == tuple(int(v) for v in m[k, :2])))
             res["cpu_baseline"] = cb
+            if args.inc_merges > 0:
+                res["cpu_incremental"] = cpu_incremental(text, m, args.inc_merges)
+        if world == 1 and not args.no_extra:
+            res["roofline_pair_histogram"] = histogram_roofline(eng, min(args.cpu_late_merge, merges))
         else:
             res["cpu_baseline"] = None
+        if world == 1 and not args.no_extra and args.n_bytes == 1 << 30 and args.vocab == 32000:
+            res["configs"] = extra_configs(zbpe, eng, m, args)
         if args.stats_out:
             with open(args.stats_out, "w") as f:
                 json.dump({"merges": m.tolist(), "counts": c.tolist()}, f)

@@ -178,6 +178,15 @@ zbpe_status zbpe_bench_scan(zbpe_ctx *ctx, uint16_t a, uint16_t b, int reps, dou
 zbpe_status zbpe_bench_train_scan(zbpe_ctx *ctx, int reps, int grid, double *avg_us, uint32_t *pair, uint32_t *list_len,
                                   int *mode);
 
+/* Benchmark diagnostic, after zbpe_train* (one GPU): `reps` launches of the full pair-histogram kernel
+ * (the recount behind zbpe_verify_counts: every adjacent pair of the current stream, counted in LDS
+ * tables per workgroup, the rest by global lookups) over the stream compacted into the spare buffer;
+ * the first launch is not timed. *avg_us: average launch time (HIP events); *gbps = 2 B per token /
+ * *avg_us; *n_tokens: the stream's live tokens; *mismatches: pair counts of the last launch that differ
+ * from the incremental table (0 expected). */
+zbpe_status zbpe_bench_recount(zbpe_ctx *ctx, int reps, double *avg_us, double *gbps, uint64_t *n_tokens,
+                               uint64_t *mismatches);
+
 /* Profiling diagnostic: with option "trace" = 1, train records one row of ZBPE_TRACE_COLS floats per
  * merge: {merge index, count, live tokens, stream slots, slots streamed by the scan (a list scan in a
  * device-resident batch: entries of the walked list), scan ms,

@@ -2,7 +2,9 @@
 // algorithm used by the HIP engine, run on the CPU so its delta rules and the Zig-order tie
 // fast path can be checked against the oracle before they are written as kernels.
 //   build: g++ -O2 -std=c++17 -o inc_model inc_model.cpp
-//   run:   ./inc_model <corpus file> <vocab>  -> merges on stdout, stats on stderr
+//   run:   ./inc_model <corpus file> <vocab> [check_fast 0/1] [max_merges]  -> merges on stdout, stats on stderr
+// Also the algorithm-matched CPU baseline of bench.py (one core, -O3): the same incremental counting as
+// the device, with a pass over the stream per merge to find the occurrences, timed on C4's first merges.
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -10,6 +12,7 @@
 #include <unordered_map>
 #include <vector>
 #include <algorithm>
+#include <chrono>
 
 static const uint16_t HOLE = 0xFFFF;
 static inline void mum(uint64_t &a, uint64_t &b) { __uint128_t x = (__uint128_t)a * b; a = (uint64_t)x; b = (uint64_t)(x >> 64); }
@@ -111,10 +114,21 @@ struct Model {
 int main(int argc, char **argv) {
     if (argc < 3) return 1;
     FILE *f = fopen(argv[1], "rb"); if (!f) return 1;
-    std::vector<uint8_t> text; int c; while ((c = fgetc(f)) != EOF) text.push_back((uint8_t)c); fclose(f);
+    std::vector<uint8_t> text;
+    { uint8_t buf[1 << 16]; size_t k; while ((k = fread(buf, 1, sizeof buf, f)) > 0) text.insert(text.end(), buf, buf + k); }
+    fclose(f);
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_start = now();
     int V = atoi(argv[2]); int check_fast = argc > 3 ? atoi(argv[3]) : 1;
+    long max_merges = argc > 4 ? atol(argv[4]) : 0;
+    if (max_merges > 0 && 256 + max_merges < V) V = (int)(256 + max_merges);
     Model M; M.tok.assign(text.begin(), text.end());
-    for (size_t i = 0; i + 1 < M.tok.size(); i++) M.add(M.tok[i] | ((uint32_t)M.tok[i + 1] << 16), 1);
+    {  // initial counts: byte pairs in a dense histogram, then into the map
+        std::vector<int64_t> h(65536, 0);
+        for (size_t i = 0; i + 1 < text.size(); i++) h[text[i] | (text[i + 1] << 8)]++;
+        for (uint32_t p = 0; p < 65536; p++) if (h[p]) M.add((p & 0xFF) | ((p >> 8) << 16), h[p]);
+    }
+    const double t_init = now();
     std::vector<int64_t> left(65536), right(65536);
     for (int X = 256; X < V; X++) {
         if (M.D == 0) { fprintf(stderr, "No more pairs to merge. Stopping early.\n"); break; }
@@ -172,6 +186,7 @@ int main(int argc, char **argv) {
         if (M.holes * 8 > M.tok.size()) M.compact();
         if ((X & 1023) == 0) fprintf(stderr, "X=%d D=%lld ids=%zu top=%llu n=%zu\n", X, (long long)M.D, M.cnt.size(), (unsigned long long)top, M.tok.size() - M.holes);
     }
+    fprintf(stderr, "timing: init_s=%.3f merges_s=%.3f\n", t_init - t_start, now() - t_init);
     fprintf(stderr, "ties=%llu fallbacks=%llu D=%lld ids=%zu new_keys=%llu compactions=%llu\n", (unsigned long long)M.ties,
             (unsigned long long)M.fallbacks, (long long)M.D, M.cnt.size(), (unsigned long long)M.new_keys_total, (unsigned long long)M.compactions);
     return 0;

@@ -195,6 +195,12 @@ zbpe_status zbpe_bench_train_scan(zbpe_ctx *ctx, int reps, int grid, double *avg
     return ctx->eng.bench_train_scan(reps, grid, avg_us, pair, list_len, mode);
 }
 
+zbpe_status zbpe_bench_recount(zbpe_ctx *ctx, int reps, double *avg_us, double *gbps, uint64_t *n_tokens,
+                               uint64_t *mismatches) {
+    if (!ctx || !avg_us || !gbps || !n_tokens || !mismatches || reps < 0) return ZBPE_INVALID_ARGUMENT;
+    return ctx->eng.bench_recount(reps, avg_us, gbps, n_tokens, mismatches);
+}
+
 zbpe_status zbpe_merge_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_t *n_rows) {
     if (!ctx || !n_rows || (!rows && cap_rows)) return ZBPE_INVALID_ARGUMENT;
     const auto &L = ctx->eng.h_log;

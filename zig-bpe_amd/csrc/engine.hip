@@ -116,6 +116,7 @@ zbpe_status Engine::init(int dev) {
     // the initial byte-pair histogram keeps 128 KiB of bins in LDS
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_count_byte_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4));
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_pres_build, hipFuncAttributeMaxDynamicSharedMemorySize, PRES_MAX_VP * 4));
+    HIP_OK(hipFuncSetAttribute((const void *)zbpe_pair_hist, hipFuncAttributeMaxDynamicSharedMemorySize, PH_SLOTS * 8));
     CHECK(set_scan_variant(0));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dev));
@@ -1394,24 +1395,34 @@ zbpe_status Engine::verify_counts(uint64_t *mismatches) {
 // Diagnostic download of the live token stream (holes squeezed out) into the spare stream buffer,
 // leaving the current buffer, its holes and the occurrence lists as they are. out == nullptr or a
 // short cap: only *n_tokens.
+// the live tokens of the current stream, holes squeezed out, into the spare stream buffer (the current
+// buffer, its holes and the occurrence lists stay as they are); *total: their number
+zbpe_status Engine::compact_to_spare(uint64_t *total) {
+    *total = 0;
+    const int64_t ntiles = (n_slots + COMPACT_TILE - 1) / COMPACT_TILE;
+    if (ntiles <= 0) return ZBPE_OK;
+    CHECK(ensure(&d_tile_cnt, tile_cnt_cap, ntiles, "compaction tiles"));
+    CHECK(ensure(&d_tile_off, tile_off_cap, ntiles + 1, "compaction offsets"));
+    uint16_t *src = d_tok[cur], *dst = d_tok[cur ^ 1];
+    zbpe_compact_count<<<ntiles, 256, 0, stream>>>(src, n_slots, d_tile_cnt);
+    LAUNCH_OK();
+    zbpe_scan_u32<<<1, 1024, 0, stream>>>(d_tile_cnt, ntiles, d_tile_off, d_tile_off + ntiles);
+    LAUNCH_OK();
+    zbpe_compact_scatter<<<ntiles, 256, 0, stream>>>(src, n_slots, d_tile_off, dst);
+    LAUNCH_OK();
+    HIP_OK(hipMemcpyAsync(total, d_tile_off + ntiles, 8, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    return ZBPE_OK;
+}
+
+// Diagnostic download of the live token stream (holes squeezed out) into the spare stream buffer,
+// leaving the current buffer, its holes and the occurrence lists as they are. out == nullptr or a
+// short cap: only *n_tokens.
 zbpe_status Engine::tokens(uint16_t *out, size_t cap, size_t *n_tokens) {
     if (!stream_ready && !trained && n_slots == 0) { *n_tokens = 0; return ZBPE_OK; }
     HIP_OK(hipSetDevice(device));
-    const int64_t ntiles = (n_slots + COMPACT_TILE - 1) / COMPACT_TILE;
     uint64_t total = 0;
-    if (ntiles > 0) {
-        CHECK(ensure(&d_tile_cnt, tile_cnt_cap, ntiles, "compaction tiles"));
-        CHECK(ensure(&d_tile_off, tile_off_cap, ntiles + 1, "compaction offsets"));
-        uint16_t *src = d_tok[cur], *dst = d_tok[cur ^ 1];
-        zbpe_compact_count<<<ntiles, 256, 0, stream>>>(src, n_slots, d_tile_cnt);
-        LAUNCH_OK();
-        zbpe_scan_u32<<<1, 1024, 0, stream>>>(d_tile_cnt, ntiles, d_tile_off, d_tile_off + ntiles);
-        LAUNCH_OK();
-        zbpe_compact_scatter<<<ntiles, 256, 0, stream>>>(src, n_slots, d_tile_off, dst);
-        LAUNCH_OK();
-        HIP_OK(hipMemcpyAsync(&total, d_tile_off + ntiles, 8, hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipStreamSynchronize(stream));
-    }
+    CHECK(compact_to_spare(&total));
     *n_tokens = (size_t)total;
     if (out && cap >= total && total) {
         HIP_OK(hipMemcpyAsync(out, d_tok[cur ^ 1], (size_t)total * 2, hipMemcpyDeviceToHost, stream));
@@ -1430,9 +1441,9 @@ zbpe_status Engine::recount_check(uint64_t *mismatches, uint32_t *first_bad_key)
     CHECK(ensure(&d_recount, recount_cap, std::max<uint32_t>(nid, 1), "recount"));
     HIP_OK(hipMemsetAsync(d_recount, 0, (size_t)std::max<uint32_t>(nid, 1) * 4, stream));
     HIP_OK(hipMemsetAsync(&d_st->mismatches, 0, 4, stream));
-    ScanArgs A{d_tok[cur], n_slots, 0, 0, nullptr, nullptr, d_st, nullptr, 0, 0, nullptr, nullptr, halo};
-    zbpe_recount<<<2048, 256, 0, stream>>>(A, T, d_recount, d_st);
-    LAUNCH_OK();
+    uint64_t total = 0;
+    CHECK(compact_to_spare(&total));
+    CHECK(launch_pair_hist(total));
     if (!dist()) {
         zbpe_recount_compare<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_recount, d_st);
         LAUNCH_OK();
@@ -1467,6 +1478,49 @@ zbpe_status Engine::recount_check(uint64_t *mismatches, uint32_t *first_bad_key)
         }
     }
     *mismatches = bad;
+    return ZBPE_OK;
+}
+
+// the full pair histogram (zbpe_pair_hist) of the compacted stream in the spare buffer into d_recount
+zbpe_status Engine::launch_pair_hist(uint64_t total) {
+    const int32_t next_tok = dist() && halo.nright > 0 ? (int32_t)halo_right(halo, 0) : -1;  // the pair leaving the shard
+    zbpe_pair_hist<<<std::max(1, num_cus), PH_THREADS, PH_SLOTS * 8, stream>>>(d_tok[cur ^ 1], (int64_t)total, next_tok, T,
+                                                                                d_recount, d_st);
+    LAUNCH_OK();
+    return ZBPE_OK;
+}
+
+// Benchmark diagnostic: `reps` launches of the full pair histogram over the current stream (compacted
+// into the spare buffer first, untimed), HIP events around each launch; checks the last one against the
+// incremental counts.
+zbpe_status Engine::bench_recount(int reps, double *avg_us, double *gbps, uint64_t *n_tokens, uint64_t *mismatches) {
+    if (!trained) return fail(ZBPE_INVALID_ARGUMENT, "bench_recount needs a trained context");
+    if (dist()) return fail(ZBPE_INVALID_ARGUMENT, "bench_recount is a single-GPU diagnostic");
+    HIP_OK(hipSetDevice(device));
+    CHECK(sync_state());
+    const uint32_t nid = h_st->num_ids;
+    CHECK(ensure(&d_recount, recount_cap, std::max<uint32_t>(nid, 1), "recount"));
+    uint64_t total = 0;
+    CHECK(compact_to_spare(&total));
+    double sum = 0;
+    for (int r = 0; r <= reps; r++) {
+        HIP_OK(hipMemsetAsync(d_recount, 0, (size_t)std::max<uint32_t>(nid, 1) * 4, stream));
+        HIP_OK(hipMemsetAsync(&d_st->mismatches, 0, 4, stream));
+        HIP_OK(hipEventRecord(ev[0], stream));
+        CHECK(launch_pair_hist(total));
+        HIP_OK(hipEventRecord(ev[1], stream));
+        HIP_OK(hipEventSynchronize(ev[1]));
+        float ms;
+        HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        if (r) sum += ms;  // the first launch warms up
+    }
+    zbpe_recount_compare<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_recount, d_st);
+    LAUNCH_OK();
+    CHECK(sync_state());
+    *mismatches = h_st->mismatches;
+    *avg_us = reps ? sum * 1e3 / reps : 0;
+    *gbps = *avg_us > 0 ? 2.0 * (double)total / (*avg_us * 1e-6) / 1e9 : 0;
+    *n_tokens = total;
     return ZBPE_OK;
 }
 

@@ -220,6 +220,7 @@ struct Engine {
     zbpe_status set_scan_variant(int v);
     zbpe_status bench_scan(uint32_t a, uint32_t b, int reps, double *avg_ms, double *gbps);
     zbpe_status bench_train_scan(int reps, int grid, double *avg_us, uint32_t *pair, uint32_t *list_len, int *mode);
+    zbpe_status bench_recount(int reps, double *avg_us, double *gbps, uint64_t *n_tokens, uint64_t *mismatches);
 
    private:
     zbpe_status sync_state();
@@ -248,6 +249,8 @@ struct Engine {
     void halo_from_boundaries();
     zbpe_status comm_sum(uint32_t *d, size_t n);
     zbpe_status recount_check(uint64_t *mismatches, uint32_t *first_bad_key);
+    zbpe_status compact_to_spare(uint64_t *total);
+    zbpe_status launch_pair_hist(uint64_t total);
     zbpe_status resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner);
 };
 

@@ -3744,6 +3744,75 @@ __global__ void __launch_bounds__(256) zbpe_recount(ScanArgs A, Tables T, uint32
         atomicAdd(&recount[id], 1u);
     }
 }
+// Full pair histogram of a hole-free stream (countCodePointPairs over the whole stream,
+// basic_tokenizer.zig:257-278, against the table's ids): the verification recount and the north-star
+// histogram kernel. One 1024-thread workgroup per CU streams 16-B vectors (non-temporal, a lane's
+// successor token from its neighbour lane by a shuffle) and counts pairs in an LDS open-addressed table
+// of PH_SLOTS keys (128 KiB): hot pairs take one LDS atomic each, and only a pair that finds no slot
+// within PH_PROBES probes pays the global hash lookup + atomic. The LDS table is flushed once at the
+// end (one lookup + one atomic per distinct pair per workgroup). `next_tok` is the token after the
+// stream (the next shard's first, or -1).
+constexpr int PH_THREADS = 1024;
+constexpr uint32_t PH_SLOTS = 16384;
+constexpr int PH_PROBES = 8;
+constexpr uint32_t PH_EMPTY = 0xFFFFFFFFu;  // (65535, 65535): two holes, never a pair
+__device__ inline void ph_count(uint32_t *s_key, uint32_t *s_cnt, const Tables &T, uint32_t *recount, DevState *st,
+                                uint32_t key) {
+    uint32_t h = (key * 0x9E3779B1u) >> (32 - 14);
+#pragma unroll 1
+    for (int q = 0; q < PH_PROBES; q++) {
+        const uint32_t k = __hip_atomic_load(&s_key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (k == key) { atomicAdd(&s_cnt[h], 1u); return; }
+        if (k == PH_EMPTY) {
+            const uint32_t old = atomicCAS(&s_key[h], PH_EMPTY, key);
+            if (old == PH_EMPTY || old == key) { atomicAdd(&s_cnt[h], 1u); return; }
+        }
+        h = (h + 1) & (PH_SLOTS - 1);
+    }
+    const uint32_t id = ht_find(T, key);
+    if (id == NO_ID) { atomicAdd(&st->mismatches, 1u); return; }
+    atomicAdd(&recount[id], 1u);
+}
+__global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__restrict__ tok, int64_t n, int32_t next_tok,
+                                                              Tables T, uint32_t *__restrict__ recount, DevState *st) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t ph_lds[];
+    uint32_t *s_key = ph_lds, *s_cnt = ph_lds + PH_SLOTS;
+    for (uint32_t i = threadIdx.x; i < PH_SLOTS; i += PH_THREADS) { s_key[i] = PH_EMPTY; s_cnt[i] = 0; }
+    __syncthreads();
+    const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
+    const int64_t nvec = (n + 7) / 8;
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * PH_THREADS;
+    for (int64_t base = (int64_t)blockIdx.x * PH_THREADS + (threadIdx.x & ~63); base < nvec; base += stride) {
+        const int64_t vi = base + lane;
+        const bool valid = vi < nvec;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(tv + (valid ? vi : 0)));
+        const uint4 v = valid ? make_uint4(y.x, y.y, y.z, y.w) : make_uint4(0, 0, 0, 0);
+        uint32_t nx = (uint32_t)__shfl_down((int)(v.x & 0xFFFFu), 1);  // the next vector's first token
+        const int64_t p8 = vi * 8 + 8;                                  // its position
+        if (lane == 63 && valid && p8 < n) nx = tok[p8];
+        if (valid && p8 >= n) nx = p8 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY;
+        if (!valid) continue;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int64_t p = vi * 8 + k;
+            if (p >= n) break;
+            const uint32_t b = k < 7 ? (p + 1 < n ? tok_at(v, k + 1) : (next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY)) : nx;
+            if (b == PH_EMPTY) continue;
+            ph_count(s_key, s_cnt, T, recount, st, pair_key(tok_at(v, k), b));
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < PH_SLOTS; i += PH_THREADS) {
+        const uint32_t k = s_key[i];
+        if (k == PH_EMPTY) continue;
+        const uint32_t id = ht_find(T, k);
+        if (id == NO_ID) { atomicAdd(&st->mismatches, s_cnt[i]); continue; }
+        atomicAdd(&recount[id], s_cnt[i]);
+    }
+}
+
 // (key, table count, this shard's recount) of every id, for the cross-rank comparison
 __global__ void __launch_bounds__(256) zbpe_recount_dump(Tables T, const uint32_t *recount, const DevState *st, uint32_t *out) {
     const uint32_t n = min(st->num_ids, T.id_cap);

@@ -148,7 +148,7 @@ EXPORTS = (
     "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_create_dist_host", "zbpe_destroy", "zbpe_last_error",
     "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts", "zbpe_tokens",
     "zbpe_set_option", "zbpe_format_time_stats", "zbpe_bench_scan", "zbpe_bench_train_scan", "zbpe_merge_log", "zbpe_trace", "zbpe_scan_log", "zbpe_zig_order_winner", "zbpe_version",
-    "zbpe_stats_size",
+    "zbpe_stats_size", "zbpe_bench_recount",
 )
 MERGE_LOG_COLUMNS = ("key", "count", "live", "ties", "list_scan", "list_len", "key_live", "zero")
 TRACE_COLUMNS = ("merge", "count", "live", "slots", "streamed", "scan_ms", "replace_ms", "select_ms", "wall_ms",
@@ -218,6 +218,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         L.zbpe_bench_train_scan.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                             ctypes.POINTER(ctypes.c_int)]
+    if hasattr(L, "zbpe_bench_recount"):
+        L.zbpe_bench_recount.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     L.zbpe_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
     L.zbpe_bench_scan.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double)]
@@ -331,6 +334,13 @@ class Engine:
         self._check(self._L.zbpe_bench_train_scan(self._ctx, reps, grid, ctypes.byref(us), ctypes.byref(pair), ctypes.byref(ln),
                                                   ctypes.byref(mode)), "zbpe_bench_train_scan")
         return {"us": us.value, "pair": (pair.value & 0xFFFF, pair.value >> 16), "list_len": ln.value, "mode": mode.value}
+
+    def bench_recount(self, reps: int = 5) -> dict:
+        """Full pair-histogram kernel timing on the trained state (zbpe_bench_recount)."""
+        us, gbps, n, mm = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._check(self._L.zbpe_bench_recount(self._ctx, reps, ctypes.byref(us), ctypes.byref(gbps), ctypes.byref(n),
+                                               ctypes.byref(mm)), "zbpe_bench_recount")
+        return {"us": us.value, "GBps": gbps.value, "tokens": n.value, "mismatches": mm.value}
 
     def trace(self):
         """Per-merge rows of the last train (option "trace" = 1): float32 array [merges, len(TRACE_COLUMNS)]."""
