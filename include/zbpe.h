@@ -73,13 +73,16 @@ typedef struct zbpe_stats {
     /* ties decided by both the device's cluster test and the exact emulation, with the same winner
      * (options "exact_ties", "exact_ties_from" / "exact_ties_to"); a disagreement fails the train */
     uint64_t tie_crosschecks;
+    /* generateInitialTokens (basic_tokenizer.zig:155-170): the u8 -> u16 widening of the resident corpus
+     * (device time); train prints it like the reference, "generateInitialTokens runtime: S seconds" */
+    double generate_tokens_s;
 } zbpe_stats;
 
 /* Layout version of zbpe_stats. The struct is caller-allocated and has grown across versions: a
  * consumer compares zbpe_stats_size() with the size of the zbpe_stats of the header it was built against
  * before passing a zbpe_stats: the library writes zbpe_stats_size() bytes.
  *   1: up to tie_fallbacks ... list_builds;  2: + replications, phase split, sharded_merges;
- *   3: + tie_crosschecks. */
+ *   3: + tie_crosschecks, generate_tokens_s. */
 #define ZBPE_STATS_VERSION 3
 size_t zbpe_stats_size(void);
 
@@ -122,7 +125,9 @@ zbpe_status zbpe_train_resident(zbpe_ctx *ctx, uint16_t vocab_size, int verbose,
                                 uint64_t *out_counts, size_t *out_n_merges, zbpe_stats *stats);
 
 /* BasicTokenizer.encode (basic_tokenizer.zig:71-88): apply `n_merges` merges in order, left-greedy.
- * out: caller buffer of n u16; *out_len receives the encoded length. */
+ * out: caller buffer of n u16; *out_len receives the encoded length. Any u16 may appear in the table
+ * (as deserializeMerges allows, :342-344), 65535 included. Prints the generateInitialTokens runtime
+ * line like the reference's encode (:72). */
 zbpe_status zbpe_encode(zbpe_ctx *ctx, const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n,
                         uint16_t *out, size_t *out_len);
 
@@ -155,7 +160,8 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * (0: always stream the token stream; 1: token occurrence lists once counts are small), "list_ratio"
  * (train: list scan when list length * ratio < stream slots), "encode_list_ratio" (the same for encode), "list_start" (build the lists at a compaction
  * once top count * list_start < live tokens; 0: at the first compaction), "compact_den_lists" (compact_den
- * once lists are on). */
+ * once lists are on), "print_runtime" (0: no generateInitialTokens
+ * runtime line on stderr). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* printTimeStats (src/utils/time_statistics.zig:36-60): the reference's "Time statistics" text for

@@ -348,3 +348,46 @@ def test_list_neighbour_filter_agrees(nb):
         other = zbpe.synth_corpus(kind, seed + 100, n)
         assert np.array_equal(e.encode(m, other), O.encode(m, other)), (kind, nb)
         e.close()
+
+
+def test_encode_table_with_token_65535():
+    """deserializeMerges accepts any u16 (basic_tokenizer.zig:342-344), so a table may create or use token
+    65535 (the device's hole marker): encode renames it internally and must equal the reference's loop"""
+    text = synth_text(synth_goldens()[0])[:50000]
+    tables = [
+        [(101, 32, 65535), (65535, 116, 300), (116, 104, 301)],
+        [(32, 116, 65535), (104, 101, 300), (65535, 300, 301), (65535, 65535, 302)],
+        [(65535, 97, 256), (97, 98, 257)],  # a merge on a token nothing produces
+    ]
+    e = zbpe.Engine(0)
+    for tab in tables:
+        m = np.asarray(tab, dtype=np.uint16)
+        assert e.encode(m, text).tolist() == O.encode(m, text, literal=True).tolist()
+    e.close()
+
+
+def test_generate_initial_tokens_runtime_line(capfd):
+    """train and encode print generateInitialTokens' runtime line like the reference (:156-160, called by
+    train :150 and encode :72)"""
+    e = zbpe.Engine(0)
+    capfd.readouterr()
+    m, _, st = e.train(b"hello world hello", 300)
+    err = capfd.readouterr().err
+    assert err.count("generateInitialTokens runtime: ") == 1 and " seconds\n" in err and st.generate_tokens_s >= 0
+    e.encode(m, b"hello")
+    assert capfd.readouterr().err.startswith("generateInitialTokens runtime: ")
+    e.set_option("print_runtime", 0)
+    e.train(b"hello world hello", 300)
+    assert "generateInitialTokens" not in capfd.readouterr().err
+    e.close()
+
+
+def test_basic_tokenizer_time_stats_accumulate(capfd):
+    """TimeStats live as long as the tokenizer (time_statistics.zig:15-29): a second train adds to them"""
+    t = zbpe.BasicTokenizer()
+    t.train(c1_text(), 300)
+    calls = t.timeStats.replace_pair_calls
+    t.train(c1_text(), 300)
+    assert t.timeStats.replace_pair_calls == 2 * calls == 88
+    assert len(t.merges.merges) == 88  # merges append (:199)
+    t.deinit()

@@ -170,3 +170,14 @@ def test_c_abi_consumer_builds():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     subprocess.run(["make", "-s", "-C", os.path.join(root, "tests", "c_abi")], check=True)
     assert os.access(os.path.join(root, "tests", "c_abi", "main"), os.X_OK)
+
+
+def test_time_stats_printed_on_invalid_vocab(capfd):
+    """printTimeStats runs from train's defer (basic_tokenizer.zig:141-145), so it prints on
+    InvalidVocabSize too (no device work happens before the check)"""
+    t = zbpe.BasicTokenizer()
+    capfd.readouterr()
+    with pytest.raises(zbpe.InvalidVocabSize):
+        t.train(b"abc", 100)
+    err = capfd.readouterr().err
+    assert "Time statistics:" in err and "sortCodePointPairs: 0.000s total, 0 calls, nans avg" in err

@@ -833,6 +833,21 @@ zbpe_status Engine::alloc_stream(size_t n) {
     return ZBPE_OK;
 }
 
+// generateInitialTokens (basic_tokenizer.zig:155-170): the u8 -> u16 stream (alloc_stream's widen), timed
+// with events; like the reference it prints its runtime line to stderr (:156-160; train and encode both
+// call it, :150 and :72), on rank 0, unless option "print_runtime" is 0
+zbpe_status Engine::generate_initial_tokens(size_t n) {
+    HIP_OK(hipEventRecord(ev[6], stream));
+    CHECK(alloc_stream(n));
+    HIP_OK(hipEventRecord(ev[7], stream));
+    HIP_OK(hipEventSynchronize(ev[7]));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, ev[6], ev[7]));
+    gen_tokens_s = ms * 1e-3;
+    if (print_runtime && rank == 0) fprintf(stderr, "generateInitialTokens runtime: %.3f seconds\n", gen_tokens_s);
+    return ZBPE_OK;
+}
+
 // halo of this rank from the gathered boundary records (walks past shards with too few live tokens)
 void Engine::halo_from_boundaries() {
     Halo H = halo_empty();
@@ -862,7 +877,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     double ev_count = 0, ev_select = 0, ev_replace = 0;
 
     // ---- generateInitialTokens + initial histogram ------------------------------------------------
-    CHECK(alloc_stream(n));
+    CHECK(generate_initial_tokens(n));
+    stats.generate_tokens_s = gen_tokens_s;
     pres_vp = ((uint32_t)vocab_size + 63) & ~63u;
     pres_on = block_skip && pres_vp <= PRES_MAX_VP;
     CHECK(build_presence());
@@ -1160,8 +1176,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             if (hot_stale) CHECK(rebuild_hot());
             // about four hot entries per thread (the list grows by the new ids of the batch), and
             // the delta words to clear
-            const uint64_t hot_est = std::min<uint64_t>(T.hot_cap, (uint64_t)h_st->hot_len + (uint64_t)K * 1024 + 4096);
-            const uint64_t work = std::max<uint64_t>(hot_est / 4, 2ull * X / 4);
+            // (the grid only sets the parallelism: the argmax loops over whatever the hot list holds at run time)
+            const uint64_t hot_est = std::min<uint64_t>(T.hot_cap, (uint64_t)h_st->hot_len + (uint64_t)K * sel_growth + 4096);
+            const uint64_t work = std::max<uint64_t>(hot_est / 4, C ? 0ull : 2ull * X / 4);  // refresh blocks clear the deltas
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
@@ -1525,15 +1542,34 @@ zbpe_status Engine::bench_recount(int reps, double *avg_us, double *gbps, uint64
 }
 
 // encode (basic_tokenizer.zig:71-88): replay merges in rank order on the device
-zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8_t *text, size_t n, uint16_t *out,
+zbpe_status Engine::encode(const uint16_t *triples_in, size_t n_merges, const uint8_t *text, size_t n, uint16_t *out,
                            size_t *out_len) {
-    for (size_t k = 0; k < n_merges; k++) {
-        if (triples[3 * k + 2] == HOLE || triples[3 * k] == HOLE || triples[3 * k + 1] == HOLE)
-            return fail(ZBPE_INVALID_ARGUMENT, "merge %zu uses token 65535", k);
+    // Token 65535 is the stream's hole marker on the device. A merge table may still hold it (the reference
+    // parses any u16, deserializeMerges :342-344; a trained table never does: vocabSize is a u16, so new
+    // tokens stop at 65534): the table is encoded with 65535 renamed to a token id that no merge uses (it
+    // can then neither be in the input -- bytes are < 256 -- nor come from another merge, so the result is
+    // the same up to the name) and renamed back in the output.
+    const uint16_t *triples = triples_in;
+    std::vector<uint16_t> renamed;
+    uint32_t alias = 0;
+    {
+        bool uses_hole = false;
+        for (size_t i = 0; i < 3 * n_merges && !uses_hole; i++) uses_hole = triples_in[i] == HOLE;
+        if (uses_hole) {
+            std::vector<uint8_t> used(65536, 0);
+            for (size_t i = 0; i < 3 * n_merges; i++) used[triples_in[i]] = 1;
+            for (uint32_t t = 256; t < HOLE && !alias; t++)
+                if (!used[t]) alias = t;
+            if (!alias) return fail(ZBPE_INVALID_ARGUMENT, "merge table uses every token id 256..65535: no id to stand for 65535");
+            renamed.assign(triples_in, triples_in + 3 * n_merges);
+            for (auto &t : renamed)
+                if (t == HOLE) t = (uint16_t)alias;
+            triples = renamed.data();
+        }
     }
     CHECK(upload(text, n, false));
     trained = false;
-    CHECK(alloc_stream(n));
+    CHECK(generate_initial_tokens(n));
     HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
     // token occurrence lists (as in train): a merge's scan walks the shorter of its tokens' lists
     // when that is short; every merge's records become the list of its new token. Needs distinct
@@ -1665,6 +1701,9 @@ zbpe_status Engine::encode(const uint16_t *triples, size_t n_merges, const uint8
     if (n_live) HIP_OK(hipMemcpyAsync(out, d_tok[cur], (size_t)n_live * 2, hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
     *out_len = (size_t)n_live;
+    if (alias)
+        for (int64_t i = 0; i < n_live; i++)
+            if (out[i] == alias) out[i] = HOLE;
     return ZBPE_OK;
 }
 

@@ -185,8 +185,11 @@ struct Engine {
         double batch_s = 0;                                   // device span of the batches
     } run;
     uint64_t hot_target = 1u << 15;  // ids the hot list aims to hold after a rebuild
+    uint32_t sel_growth = 1024;      // hot-list growth per merge assumed when sizing zbpe_select_next's argmax grid
     uint64_t hot_rebuilds = 0, home_rebuilds = 0;
-    hipEvent_t ev[6] = {};
+    hipEvent_t ev[8] = {};
+    bool print_runtime = true;  // generateInitialTokens' runtime line on stderr (option "print_runtime")
+    double gen_tokens_s = 0;
 
     // policy knobs
     uint64_t compact_den = 8;     // compact when holes > slots / compact_den
@@ -229,6 +232,7 @@ struct Engine {
     zbpe_status merge_sync(uint32_t X);
     zbpe_status run_batch(uint32_t X0, uint32_t *done, bool *halted);
     zbpe_status alloc_stream(size_t n);
+    zbpe_status generate_initial_tokens(size_t n);
     zbpe_status build_presence();
     zbpe_status compact();
     zbpe_status compact_train(uint32_t X);

@@ -3291,12 +3291,24 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
 
 // ------------------------------------------------------------------------------------------
 // Fused end of merge X + start of merge X+1 (batch mode): one launch instead of select, collect,
-// refresh and decide. Blocks [0, sel_blocks) run the hot-list argmax and keep the keys at their
-// block's max; blocks [sel_blocks, grid) refresh one dirty home super-block each (when a home
-// histogram is kept). The last block to take the ticket (release / acquire at agent scope,
-// cdna_hip_programming.md §6 G16 counter form) reduces the argmax, rolls the merge, evaluates the
-// start of merge X+1 and, on a tie, gathers the tied keys for zbpe_tie_decide (the next launch:
-// the decision's carry code needs 256 VGPRs, more than a 1024-thread block may hold).
+// refresh and decide. Two roles, each with its own arrival count:
+//   - blocks [0, nref) (nref = home super-blocks, 0 without a home histogram) refresh one dirty home
+//     super-block each and clear merge X's deltas for merge X + 2; they arrive on eight per-XCD
+//     counters (N.rtk, parity X & 1; block_ticket_last_x). When merge X was tied (log[X].ties > 1: ties
+//     come in streaks) the arrivals are returning and elect the last refresh workgroup, which
+//     precomputes the tie decision's carries (refresh_prefix into N.cs) unless the argmax side has
+//     already stored st->ref_noprefix = X (merge X + 1 needs no decision), then arrives once more on the
+//     top counter.
+//   - blocks [nref, nref + sel_blocks) run the hot-list argmax and keep the keys at their block's max;
+//     the last of them through st->ticket (block_ticket_last: write-through partials, no fences)
+//     reduces, rolls merge X, evaluates the start of merge X + 1 and, on a tie, gathers the tied keys
+//     and takes the Zig-order decision in this launch (decide_body). Before deciding it spin-waits for
+//     the refresh arrivals (and, with precomputed carries, for the prefix's final arrival).
+// The wait only makes progress because the refresh workgroups -- lower workgroup ids -- are
+// dispatched before the argmax workgroups and never wait on them: the GPU dispatches a grid's
+// workgroups in id order, so every refresh workgroup is resident or finished by the time the last
+// argmax workgroup spins. The grid is sized (launch bounds: 4 waves per SIMD) so that every workgroup
+// fits one dispatch round.
 // ------------------------------------------------------------------------------------------
 constexpr int NEXT_THREADS = 512;  // launch bounds: 4 waves per SIMD (two workgroups per CU; the decision spills a little)
 constexpr int NEXT_CAND = 64;          // keys kept per argmax block at the block's max
@@ -3378,6 +3390,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         // atomics, per-XCD counters, then the top one) and arrives once more when done. Else a
         // workgroup's arrival is one non-returning add to its XCD's counter.
         const bool pfx = N.cs && N.B.log[X - 256].ties > 1;
+        // merge X's neighbour deltas, cleared for merge X + 2 by these workgroups (off the argmax's
+        // critical path: the argmax grid is sized by the hot list alone; nothing in this launch reads
+        // [0, 2X) -- the roll reads the tail words past it)
+        for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
         refresh_super(T, blockIdx.x, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), true,
                       home_dirty_bits(T, blockIdx.x));
         if (N.prof && tid == 0) atomicMax(&st->sel_tr, (unsigned long long)wall_clock64());
@@ -3427,7 +3443,8 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     const uint32_t bx = blockIdx.x - nref;  // argmax block index
     {
         const uint32_t G = N.sel_blocks * NEXT_THREADS;
-        for (uint32_t t = bx * NEXT_THREADS + tid; t < 2 * X; t += G) delta[t] = 0;
+        if (!nref)  // (no refresh workgroups: the argmax ones clear the deltas)
+            for (uint32_t t = bx * NEXT_THREADS + tid; t < 2 * X; t += G) delta[t] = 0;
         const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
         if (bx == 0 && tid >= 64 && tid < 128 && N.world == 1) {
             // wave 1 of block 0: the count of the stream's last pair (a tie needs it: Zig map capacity)
@@ -3647,8 +3664,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     // block's count: wait for all nref, then read them with sc1 loads) --------------------------------
     if (N.prof && tid == 0) sel_tick(st, 3, &pt);
     if (nref && tid < 64) {
-        // every refresh block is resident or done (they never wait), so this ends. pfx: the top
-        // counter reaches the groups + the prefix's arrival; else the XCD counters sum to nref
+        // every refresh block is resident or done (they never wait), so this ends. It relies on the GPU
+        // dispatching a grid's workgroups in id order: the refresh workgroups (ids [0, nref)) were
+        // dispatched before this argmax workgroup, so none of them waits for a slot this one holds.
+        // pfx: the top counter reaches the groups + the prefix's arrival; else the XCD counters sum to nref
         const uint32_t *rtk = N.rtk + (X & 1) * RTK_SET;
         if (pfx) {
             while (ld_wt(rtk + 8 * RTK_STRIDE) < min(nref, 8u) + 1u) __builtin_amdgcn_s_sleep(1);
@@ -3755,6 +3774,7 @@ __global__ void __launch_bounds__(256) zbpe_recount(ScanArgs A, Tables T, uint32
 constexpr int PH_THREADS = 1024;
 constexpr uint32_t PH_SLOTS = 16384;
 constexpr int PH_PROBES = 8;
+constexpr int PH_U = 4;  // 16-B vectors per lane in flight
 constexpr uint32_t PH_EMPTY = 0xFFFFFFFFu;  // (65535, 65535): two holes, never a pair
 __device__ inline void ph_count(uint32_t *s_key, uint32_t *s_cnt, const Tables &T, uint32_t *recount, DevState *st,
                                 uint32_t key) {
@@ -3782,25 +3802,48 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
     const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
     const int64_t nvec = (n + 7) / 8;
     const int lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * PH_THREADS;
-    for (int64_t base = (int64_t)blockIdx.x * PH_THREADS + (threadIdx.x & ~63); base < nvec; base += stride) {
-        const int64_t vi = base + lane;
-        const bool valid = vi < nvec;
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(tv + (valid ? vi : 0)));
-        const uint4 v = valid ? make_uint4(y.x, y.y, y.z, y.w) : make_uint4(0, 0, 0, 0);
-        uint32_t nx = (uint32_t)__shfl_down((int)(v.x & 0xFFFFu), 1);  // the next vector's first token
-        const int64_t p8 = vi * 8 + 8;                                  // its position
-        if (lane == 63 && valid && p8 < n) nx = tok[p8];
-        if (valid && p8 >= n) nx = p8 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY;
-        if (!valid) continue;
+    // a wave takes tiles of PH_U x 64 vectors: all PH_U loads are in flight before any counting
+    const int64_t wave = (int64_t)blockIdx.x * (PH_THREADS / 64) + (threadIdx.x >> 6);
+    const int64_t waves = (int64_t)gridDim.x * (PH_THREADS / 64);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    for (int64_t tile = wave * PH_U * 64; tile < nvec; tile += waves * PH_U * 64) {
+        uint4 v[PH_U];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int64_t p = vi * 8 + k;
-            if (p >= n) break;
-            const uint32_t b = k < 7 ? (p + 1 < n ? tok_at(v, k + 1) : (next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY)) : nx;
-            if (b == PH_EMPTY) continue;
-            ph_count(s_key, s_cnt, T, recount, st, pair_key(tok_at(v, k), b));
+        for (int u = 0; u < PH_U; u++) {
+            const int64_t vi = tile + u * 64 + lane;
+            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(tv + (vi < nvec ? vi : 0)));
+            v[u] = vi < nvec ? make_uint4(y.x, y.y, y.z, y.w) : make_uint4(0, 0, 0, 0);
+        }
+        const int64_t p_last = (tile + PH_U * 64) * 8;  // the token after the tile
+        const uint32_t after_tile = lane == 63 && p_last < n ? (uint32_t)tok[p_last] : PH_EMPTY;
+#pragma unroll
+        for (int u = 0; u < PH_U; u++) {
+            const int64_t vi = tile + u * 64 + lane;
+            // the next vector's first token: the next lane's, or (lane 63) the next row's lane 0 / the tile's end
+            uint32_t nx = (uint32_t)__shfl_down((int)(v[u].x & 0xFFFFu), 1);
+            const uint32_t row0 = u + 1 < PH_U ? (uint32_t)__shfl((int)(v[u + 1 < PH_U ? u + 1 : u].x & 0xFFFFu), 0) : after_tile;
+            if (lane == 63) nx = row0;
+            const int64_t p8 = vi * 8 + 8;
+            if (p8 >= n) nx = p8 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY;
+            if (vi >= nvec) continue;
+            // the 8 pairs' first probes are issued together (one LDS round trip for the common hit), then
+            // hits take a non-returning LDS add and misses walk the probe chain
+            uint32_t key[8], h[8], k0[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int64_t p = vi * 8 + k;
+                const uint32_t b = k < 7 ? (p + 1 < n ? tok_at(v[u], k + 1) : (p + 1 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY)) : nx;
+                key[k] = p < n && b != PH_EMPTY ? pair_key(tok_at(v[u], k), b) : PH_EMPTY;
+                h[k] = (key[k] * 0x9E3779B1u) >> (32 - 14);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) k0[k] = __hip_atomic_load(&s_key[h[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (key[k] == PH_EMPTY) continue;
+                if (k0[k] == key[k]) atomicAdd(&s_cnt[h[k]], 1u);
+                else ph_count(s_key, s_cnt, T, recount, st, key[k]);
+            }
         }
     }
     __syncthreads();

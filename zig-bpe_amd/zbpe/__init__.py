@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes
 import os
 import sys
+import time
 from dataclasses import dataclass, field
 from typing import Iterable, List, Optional, Sequence
 
@@ -138,6 +139,7 @@ class Stats(ctypes.Structure):
         ("comm_s", ctypes.c_double),
         ("sharded_merges", ctypes.c_uint64),
         ("tie_crosschecks", ctypes.c_uint64),
+        ("generate_tokens_s", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -500,7 +502,8 @@ class BasicTokenizer:
 
     def __init__(self, device: int = 0, engine: Optional[Engine] = None):
         self.merges = Merges()
-        self.timeStats: Optional[Stats] = None
+        # TimeStats.init (time_statistics.zig:15-29): created once, accumulated over every train call
+        self.timeStats: Stats = Stats()
         self._device = device
         self._engine = engine
 
@@ -523,17 +526,27 @@ class BasicTokenizer:
 
     # train (:140-153): appends to merges (the reference never clears them, :199)
     def train(self, text: bytes, vocabSize: int, verbose: bool = False) -> None:
-        if isinstance(text, str):
-            text = text.encode()
-        if vocabSize < vocabStart:
-            raise InvalidVocabSize(f"vocabSize {vocabSize} < 256")
-        if vocabSize > 0xFFFF:
-            raise InvalidArgument("vocabSize is a u16")
-        tri, _counts, st = self.engine.train(text, vocabSize, verbose)
-        for a, b, x in tri:
-            self.merges.put(CharPair(int(a), int(b)), int(x))
-        self.timeStats = st
-        sys.stderr.write(format_time_stats(st))  # the reference prints it at the end of train (:141-145)
+        # the reference prints printTimeStats from a defer (:141-145): on every way out, errors included,
+        # with the accumulated buckets and this call's own total time
+        start = time.perf_counter()
+        try:
+            if isinstance(text, str):
+                text = text.encode()
+            if vocabSize < vocabStart:
+                raise InvalidVocabSize(f"vocabSize {vocabSize} < 256")
+            if vocabSize > 0xFFFF:
+                raise InvalidArgument("vocabSize is a u16")
+            tri, _counts, st = self.engine.train(text, vocabSize, verbose)
+            for a, b, x in tri:
+                self.merges.put(CharPair(int(a), int(b)), int(x))
+            acc = self.timeStats
+            for k in ("count_pairs_s", "sort_pairs_s", "replace_pair_s", "other_s", "total_s", "count_pairs_calls",
+                      "sort_pairs_calls", "replace_pair_calls", "generate_tokens_s"):
+                setattr(acc, k, getattr(acc, k) + getattr(st, k))
+        finally:
+            shown = Stats.from_buffer_copy(self.timeStats)
+            shown.total_s = time.perf_counter() - start
+            sys.stderr.write(format_time_stats(shown))
 
     # encode (:71-88)
     def encode(self, text: bytes) -> List[int]:
