@@ -744,12 +744,56 @@ __device__ inline bool resolve_candidate(const ScanArgs &A, NeighbourHist &H, in
     return false;
 }
 // LDS neighbour histograms of one scan workgroup, shared by the stream and list forms (one allocation)
+// occurrence records a list walk stages per workgroup before one reservation in the arena (a counter
+// shared by every walking wave saturates at ~12 ns per atomic, MI355X_MICROARCH.md fanin; sized to keep
+// four scan workgroups per CU in 160 KiB of LDS)
+constexpr uint32_t LREC_CAP = 440;
 struct ScanLds {
     uint32_t left[LDS_BINS], right[LDS_BINS];
     uint32_t hleft[HASH_BINS], hright[HASH_BINS];
     uint32_t any;
     unsigned long long scanned;
+    uint32_t lrec[LREC_CAP];
+    uint32_t lrec_n, lrec_base;
 };
+// A list walk's wave with hit lanes: stage their record starts `pr` in the workgroup's LDS buffer; lanes
+// past its capacity reserve in the arena directly (one atomic per wave). Every lane of the wave calls it.
+__device__ inline void lrec_stage(const ScanArgs &A, ScanLds &S, bool hit, uint32_t pr, uint64_t hm) {
+    const int lane = threadIdx.x & 63;
+    uint32_t lbase = 0;
+    if (lane == 0) lbase = atomicAdd(&S.lrec_n, (uint32_t)__popcll(hm));
+    lbase = (uint32_t)__shfl((int)lbase, 0);
+    const uint32_t j = lbase + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));
+    if (hit && j < LREC_CAP) S.lrec[j] = pr;
+    const uint64_t over = __ballot(hit && j >= LREC_CAP);
+    if (!over) return;
+    uint32_t gbase = 0;
+    if (lane == 0) {
+        gbase = atomicAdd(A.rec_ctr, (uint32_t)__popcll(over));
+        atomicAdd(A.occ_out, (uint32_t)__popcll(over));
+    }
+    gbase = (uint32_t)__shfl((int)gbase, 0);
+    if (hit && j >= LREC_CAP) {
+        const uint32_t jr = gbase + (uint32_t)__popcll(over & ((1ull << lane) - 1ull));
+        if (jr < A.rec_cap) A.rec[jr] = pr;
+        else atomicOr(&A.st->error, 8u);
+    }
+}
+// after the walk (a barrier since the last lrec_stage): one arena reservation for the staged records,
+// then the copy. Every thread calls it; ends with a barrier.
+__device__ inline void lrec_flush(const ScanArgs &A, ScanLds &S) {
+    const uint32_t n = min(S.lrec_n, LREC_CAP);
+    if (threadIdx.x == 0 && n) {
+        S.lrec_base = atomicAdd(A.rec_ctr, n);
+        atomicAdd(A.occ_out, n);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t jr = S.lrec_base + i;
+        if (jr < A.rec_cap) A.rec[jr] = S.lrec[i];
+        else atomicOr(&A.st->error, 8u);
+    }
+}
 // zero the workgroup's neighbour histograms (every thread calls it, then a barrier)
 __device__ inline void scan_lds_clear(ScanLds &S) {
     for (int i = threadIdx.x; i < LDS_BINS; i += blockDim.x) { S.left[i] = 0; S.right[i] = 0; }
@@ -936,7 +980,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     const uint32_t *NB = A.nb, sh = by_b ? 16u : 0u;  // the build-time neighbour on the partner's side
     const uint32_t partner = by_b ? A.a : A.b, key = by_b ? A.b : A.a;
     scan_lds_clear(S);
-    if (threadIdx.x == 0) S.any = 0;
+    if (threadIdx.x == 0) { S.any = 0; S.lrec_n = 0; }
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{S.left, S.right, A.left, A.right, S.hleft, S.hright};
@@ -1031,17 +1075,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
             const uint64_t hm = __ballot(hit);
             if (!hm) continue;
             any = 1;
-            uint32_t base = 0;
-            if (lane == 0) {
-                base = atomicAdd(A.rec_ctr, (uint32_t)__popcll(hm));
-                atomicAdd(A.occ_out, (uint32_t)__popcll(hm));
-            }
-            base = (uint32_t)__shfl((int)base, 0);
-            if (hit) {
-                const uint32_t jr = base + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));
-                if (jr < A.rec_cap) A.rec[jr] = pr;
-                else atomicOr(&A.st->error, 8u);
-            }
+            lrec_stage(A, S, hit, pr, hm);
         }
     }
     xx = wave_sum(xx);
@@ -1049,7 +1083,10 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     if (lane == 0 && any) S.any = 1;
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
-    if (S.any) scan_lds_flush(S, A.left, A.right);
+    if (S.any) {
+        lrec_flush(A, S);
+        scan_lds_flush(S, A.left, A.right);
+    }
     if (PROF) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&A.st->pp_t[3], (unsigned long long)wall_clock64());
@@ -1067,7 +1104,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     uint32_t *s_left = S.left, *s_right = S.right;
     uint32_t &s_any = S.any;
     scan_lds_clear(S);
-    if (threadIdx.x == 0) s_any = 0;
+    if (threadIdx.x == 0) { s_any = 0; S.lrec_n = 0; }
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{s_left, s_right, A.left, A.right, S.hleft, S.hright};
@@ -1191,17 +1228,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
             const uint64_t m = __ballot(hit);
             if (!m) continue;
             any = 1;
-            uint32_t base = 0;
-            if (lane == 0) {
-                base = atomicAdd(A.rec_ctr, (uint32_t)__popcll(m));
-                atomicAdd(A.occ_out, (uint32_t)__popcll(m));
-            }
-            base = (uint32_t)__shfl((int)base, 0);
-            if (hit) {
-                const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                if (j < A.rec_cap) A.rec[j] = pr;
-                else atomicOr(&A.st->error, 8u);
-            }
+            lrec_stage(A, S, hit, pr, m);
         }
     }
     xx = wave_sum(xx);
@@ -1209,7 +1236,10 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     if (lane == 0 && any) s_any = 1;
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
-    if (s_any) scan_lds_flush(S, A.left, A.right);
+    if (s_any) {
+        lrec_flush(A, S);
+        scan_lds_flush(S, A.left, A.right);
+    }
     if (PROF) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&A.st->pp_t[3], (unsigned long long)wall_clock64());
