@@ -1306,39 +1306,53 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
       // the stream words just outside the tile (wave-uniform): the last one before it and the first
       // two after it (holes outside the stream)
       uint32_t ld_prev = 0xffffffffu, ld_nx = 0xffffffffu, ld_ny = 0xffffffffu;
-      // Branch-free: addresses are clamped into the stream and out-of-range values replaced after
-      // the load (a load under a branch makes the compiler wait for it at the join).
+      // Branch-free: addresses are clamped into the stream, and out-of-range values are replaced only
+      // when the tile is used (tile_values). A select right after the load would make the compiler
+      // wait for the load there -- for the prefetched next tile (PIPE) that is before this tile's
+      // phase 2, which then no longer overlaps the next tile's memory latency.
+      uint4 v_raw[UNROLL];
+      uint32_t raw_prev = 0xffffffffu;
+      uint2 raw_next = make_uint2(0xffffffffu, 0xffffffffu);
+      int64_t raw_vb = 0;
       auto load_tile = [&](int64_t vb) {
           {
               const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tok);
               const int64_t last = nvec * 4 - 1;  // last word of the stream
               const int64_t ip = vb > 0 ? vb * 4 - 1 : 0, in = min((vb + WT_VEC) * 4, last - 1);
-              const uint32_t wp = t32[ip];
-              const uint2 wn = *reinterpret_cast<const uint2 *>(t32 + (in & ~(int64_t)1));
-              const bool has_next = vb + WT_VEC < nvec;
-              ld_prev = vb > 0 ? wp : 0xffffffffu;
-              ld_nx = has_next ? wn.x : 0xffffffffu;
-              ld_ny = has_next ? wn.y : 0xffffffffu;
+              raw_prev = t32[ip];
+              raw_next = *reinterpret_cast<const uint2 *>(t32 + (in & ~(int64_t)1));
           }
+          raw_vb = vb;
 #pragma unroll
           for (int u = 0; u < UNROLL; u++) {
               const int64_t vi = vb + u * 64 + lane;
               const uint4 *src = reinterpret_cast<const uint4 *>(tok) + min(vi, nvec - 1);
-              uint4 x;
               if constexpr (NT) {
                   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
                   const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src));
-                  x = make_uint4(y.x, y.y, y.z, y.w);
+                  v_raw[u] = make_uint4(y.x, y.y, y.z, y.w);
               } else {
-                  x = *src;
+                  v_raw[u] = *src;
               }
-              v[u] = vi < nvec ? x : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+          }
+      };
+      auto tile_values = [&]() {
+          const int64_t vb = raw_vb;
+          const bool has_next = vb + WT_VEC < nvec;
+          ld_prev = vb > 0 ? raw_prev : 0xffffffffu;
+          ld_nx = has_next ? raw_next.x : 0xffffffffu;
+          ld_ny = has_next ? raw_next.y : 0xffffffffu;
+#pragma unroll
+          for (int u = 0; u < UNROLL; u++) {
+              const int64_t vi = vb + u * 64 + lane;
+              v[u] = vi < nvec ? v_raw[u] : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
           }
       };
       int64_t wt = wt0 + (int64_t)__builtin_ctzll(todo) * wstride;
       todo &= todo - 1;
       load_tile(wt * WT_VEC);
       for (;;) {
+        tile_values();
         const int64_t vbase = wt * WT_VEC;
         const uint32_t e_prev = ld_prev, e_nx = ld_nx, e_ny = ld_ny;  // this tile's (ld_* may be the next's soon)
         tiles++;
