@@ -234,9 +234,11 @@ def probe_roofline(eng, vocab: int, scan_log_out: str):
     import zbpe
 
     eng.set_option("timing_full", 1)
+    eng.set_option("merge_timing", 1)  # every merge: the list form's figure covers all its launches, late ones too
     eng.set_option("trace", 1)
     m, c, st = eng.train_resident(vocab)
     eng.set_option("timing_full", 0)
+    eng.set_option("merge_timing", 8)
     tr = eng.trace()
     eng.set_option("trace", 0)
     C = {k: i for i, k in enumerate(zbpe.TRACE_COLUMNS)}
@@ -268,8 +270,9 @@ def probe_roofline(eng, vocab: int, scan_log_out: str):
         "list_form": {"timed_launches": nl, "avg_launch_us": lms / max(nl, 1) * 1e3,
                       "avg_entries": lent / max(nl, 1),
                       "GBps": lent * LIST_ENTRY_BYTES / max(lms * 1e-3, 1e-12) / 1e9,
-                      "note": "bytes = 4 B list word + 16 B stream vector per walked entry; latency-bound "
-                              "(a chain of dependent loads and atomics per entry), not bandwidth-bound"},
+                      "note": "every list-form launch of the probe train (HIP events around each merge's scan: ~1 us of "
+                              "event gap each); bytes = 4 B list word + 16 B stream vector per walked entry; "
+                              "latency-bound (a chain of dependent loads and atomics per entry), not bandwidth-bound"},
         "merges": m, "counts": c, "live": live,
     }
 

@@ -13,7 +13,7 @@ for s in $STEPS; do
            cat gpurun_out/r03m/bench.json ;;
     prof) rm -rf gpurun_out/r03m/prof
           timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r03m/prof -o run -- \
-              python3 bench.py --steps 1 --warmup 0 --no-cpu --scan-log-out gpurun_out/r03m/prof_scanlog.json > gpurun_out/r03m/prof_bench.json 2> gpurun_out/r03m/prof.err || { tail gpurun_out/r03m/prof.err; exit 3; }
+              python3 bench.py --steps 1 --warmup 0 --no-cpu --no-extra --scan-log-out gpurun_out/r03m/prof_scanlog.json > gpurun_out/r03m/prof_bench.json 2> gpurun_out/r03m/prof.err || { tail gpurun_out/r03m/prof.err; exit 3; }
           python3 tools/prof_summary.py gpurun_out/r03m/prof > gpurun_out/r03m/prof_summary.txt
           python3 tools/scan_forms.py gpurun_out/r03m/prof gpurun_out/r03m/prof_scanlog.json > gpurun_out/r03m/scan_forms.json || exit 4
           cat gpurun_out/r03m/scan_forms.json

@@ -3820,9 +3820,14 @@ constexpr uint32_t PH_SLOTS = 16384;
 constexpr int PH_PROBES = 8;
 constexpr int PH_U = 4;  // 16-B vectors per lane in flight
 constexpr uint32_t PH_EMPTY = 0xFFFFFFFFu;  // (65535, 65535): two holes, never a pair
+// home pair of slots of a key: the even slot its hash picks and the next one (one 8-B LDS read; a
+// 4-slot group by 16-B reads was measured slower: 1.10 vs 0.92 ms at C4 t = 0)
+__device__ inline uint32_t ph_home(uint32_t key) { return ((key * 0x9E3779B1u) >> (32 - 14)) & ~1u; }
+// a key missing from its home pair: linear probing from the home pair (insert at the first empty slot),
+// else the global table's id and a global atomic
 __device__ inline void ph_count(uint32_t *s_key, uint32_t *s_cnt, const Tables &T, uint32_t *recount, DevState *st,
                                 uint32_t key) {
-    uint32_t h = (key * 0x9E3779B1u) >> (32 - 14);
+    uint32_t h = ph_home(key);
 #pragma unroll 1
     for (int q = 0; q < PH_PROBES; q++) {
         const uint32_t k = __hip_atomic_load(&s_key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3872,21 +3877,38 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
             if (vi >= nvec) continue;
             // the 8 pairs' first probes are issued together (one LDS round trip for the common hit), then
             // hits take a non-returning LDS add and misses walk the probe chain
-            uint32_t key[8], h[8], k0[8];
+            // hits take a non-returning LDS add; the misses of the vector's 8 pairs are taken together
+            // after them (one divergent slow path per vector, not one per pair: at 64 lanes some lane
+            // nearly always misses)
+            uint32_t key[8], h[8];
+            uint2 k0[8];
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const int64_t p = vi * 8 + k;
                 const uint32_t b = k < 7 ? (p + 1 < n ? tok_at(v[u], k + 1) : (p + 1 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY)) : nx;
                 key[k] = p < n && b != PH_EMPTY ? pair_key(tok_at(v[u], k), b) : PH_EMPTY;
-                h[k] = (key[k] * 0x9E3779B1u) >> (32 - 14);
+                h[k] = ph_home(key[k]);
             }
+            // (a plain LDS read: a slot's key only ever goes from empty to its final value, and a stale
+            // empty read just sends the pair to the probing path, which re-reads with atomics)
 #pragma unroll
-            for (int k = 0; k < 8; k++) k0[k] = __hip_atomic_load(&s_key[h[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            for (int k = 0; k < 8; k++) k0[k] = *reinterpret_cast<const uint2 *>(&s_key[h[k]]);
+            uint32_t miss = 0;
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 if (key[k] == PH_EMPTY) continue;
-                if (k0[k] == key[k]) atomicAdd(&s_cnt[h[k]], 1u);
-                else ph_count(s_key, s_cnt, T, recount, st, key[k]);
+                const uint32_t j = k0[k].x == key[k] ? 0u : k0[k].y == key[k] ? 1u : 2u;
+                if (j < 2) atomicAdd(&s_cnt[h[k] + j], 1u);
+                else miss |= 1u << k;
+            }
+            while (miss) {
+                const int k = __builtin_ctz(miss);
+                miss &= miss - 1;
+                uint32_t kk = key[0];
+#pragma unroll
+                for (int j = 1; j < 8; j++)
+                    if (k == j) kk = key[j];
+                ph_count(s_key, s_cnt, T, recount, st, kk);
             }
         }
     }
