@@ -391,3 +391,30 @@ def test_basic_tokenizer_time_stats_accumulate(capfd):
     assert t.timeStats.replace_pair_calls == 2 * calls == 88
     assert len(t.merges.merges) == 88  # merges append (:199)
     t.deinit()
+
+
+@pytest.mark.parametrize("variant,batch", [(v, 1) for v in range(7)] + [(7, 0), (7, 2)])
+@pytest.mark.parametrize("kind,n,vocab,seed", [("words_utf8", 300000, 900, 61), ("runs", 60000, 600, 62)])
+def test_scan_variants_agree_with_oracle(variant, batch, kind, n, vocab, seed):
+    """Every stream-form scan variant (engine.hip kScanVariants; 7 with cross-tile candidate batching
+    off / always) on streams with holes, lists off so every merge streams: oracle merges and counts."""
+    text = zbpe.synth_corpus(kind, seed, n)
+    r = O.train(text, vocab)
+    for merge_batch, skip in ((1, 0), (64, 1)):
+        e = zbpe.Engine(0)
+        e.set_option("scan_variant", variant)
+        e.set_option("scan_batch", batch)
+        e.set_option("list_mode", 0)
+        e.set_option("compact_den", 1 << 40)  # holes stay: windows and hole runs in the resolve paths
+        e.set_option("merge_batch", merge_batch)
+        e.set_option("block_skip", skip)
+        m, c, st = e.train(text, vocab)
+        assert m.tolist() == r.merges.tolist(), (merge_batch, skip)
+        assert c.tolist() == r.counts.tolist(), (merge_batch, skip)
+        assert e.verify_counts() == 0
+        e.close()
+
+
+def test_scan_batch_option_range(engine):
+    with pytest.raises(zbpe.ZbpeError):
+        engine.set_option("scan_batch", 3)

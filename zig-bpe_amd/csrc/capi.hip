@@ -129,6 +129,10 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "compact_den" && value > 0) e.compact_den = (uint64_t)value;
     else if (k == "scan_blocks_per_cu" && value > 0) e.scan_blocks_per_cu = (int)value;
     else if (k == "scan_variant") return e.set_scan_variant((int)value);
+    else if (k == "scan_batch") {
+        if (value < 0 || value > 2) return e.fail(ZBPE_INVALID_ARGUMENT, "scan_batch is 0, 1 or 2");
+        e.scan_batch = (int)value;
+    }
     else if (k == "block_skip") e.block_skip = value != 0;
     else if (k == "trace") e.trace_on = value != 0;
     else if (k == "merge_batch" && value >= 1) e.merge_batch = (uint32_t)std::min<int64_t>(value, zbpe::MAX_BATCH);

@@ -684,8 +684,9 @@ using ScanFn = void (*)(ScanArgs);
 static const ScanFn kScanVariants[] = {zbpe_scan_pairs_t<4, true, true, true, true>, zbpe_scan_pairs_t<8, true, true, true, true>,
                                        zbpe_scan_pairs_t<4, true, true>, zbpe_scan_pairs_t<4, true, false>,
                                        zbpe_scan_pairs_t<2, true, true, true, true>, zbpe_scan_pairs_t<4, true, true, false, true>,
-                                       zbpe_scan_pairs_t<4, false, true, true, true>};
-static const int kScanUnroll[] = {4, 8, 4, 4, 2, 4, 4};
+                                       zbpe_scan_pairs_t<4, false, true, true, true>,
+                                       zbpe_scan_pairs_t<4, true, true, true, true, false, true>};
+static const int kScanUnroll[] = {4, 8, 4, 4, 2, 4, 4, 4};
 static constexpr int kScanBlocksPerCuMax = 4;
 
 zbpe_status Engine::set_scan_variant(int v) {
@@ -700,12 +701,20 @@ zbpe_status Engine::set_scan_variant(int v) {
     return ZBPE_OK;
 }
 
-zbpe_status Engine::launch_scan(const ScanArgs &A, int grid) {
-    // default variant 0; when matches are dense (> 1/128 of the stream) the compacted phase 2
-    const int v = scan_variant;
+// Variant 0 by default; its batching twin (variant 7) once the pair is known to be sparse: count_hint
+// (a bound on the pair's count: the top count when the merges were enqueued, which never rises) times
+// SCAN_BATCH_DENSITY below the stream's slots. (Batching resolves a sparse tile's few candidates with
+// those of other tiles, +9..20 % at densities 1e-4..2e-3; variant 7 is ~7 % slower on dense tiles,
+// tools/scan_bands.py, profiles/r03_scan_bands_batch.jsonl.)
+static constexpr int kScanBatchVariant = 7;
+zbpe_status Engine::launch_scan(const ScanArgs &A, int grid, uint64_t count_hint) {
+    int v = scan_variant;
+    if (v == 0 && scan_batch == 1 && !A.prof && count_hint && count_hint * SCAN_BATCH_DENSITY < (uint64_t)A.n) v = kScanBatchVariant;
     // option sel_prof: the probed instantiation of the default variant
     const ScanFn f = A.prof && v == 0 ? zbpe_scan_pairs_t<4, true, true, true, true, true> : kScanVariants[v];
-    hipLaunchKernelGGL(f, dim3(grid > 0 ? grid : scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, A);
+    ScanArgs B = A;
+    B.batch = scan_batch;
+    hipLaunchKernelGGL(f, dim3(grid > 0 ? grid : scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, B);
     LAUNCH_OK();
     return ZBPE_OK;
 }
@@ -1149,7 +1158,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         set_list_nb(A);
         // a batch that follows one of list scans only launches a smaller grid (fewer idle workgroups
         // to dispatch); a stream scan still completes on it, only slower
-        CHECK(launch_scan(A, list_streak ? list_grid : 0));
+        CHECK(launch_scan(A, list_streak ? list_grid : 0, top0));
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 2], stream));
         CHECK(comm_sum(left, 2ull * X + 2));
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 3], stream));
@@ -1307,7 +1316,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
     set_list_nb(A);
     HIP_OK(hipEventRecord(ev[0], stream));
     if (!self) {
-        CHECK(launch_scan(A));
+        CHECK(launch_scan(A, 0, top));
         stats.scan_launches++;
     } else {
         stats.self_pair_merges++;

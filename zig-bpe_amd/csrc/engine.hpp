@@ -33,6 +33,7 @@ struct Engine {
     size_t text_cap = 0, n_text = 0;
     bool uploaded = false, trained = false, stream_ready = false;
     int scan_variant = 0;
+    int scan_batch = 1;  // ScanArgs::batch of stream-form launches (option scan_batch)
     uint16_t *d_tok[2] = {nullptr, nullptr};
     size_t tok_cap0 = 0, tok_cap1 = 0;
     int cur = 0;
@@ -245,7 +246,7 @@ struct Engine {
     zbpe_status launch_argmax(uint32_t X, int roll);
     int argmax_blocks(uint32_t X) const;
     int scan_grid(int64_t slots) const;
-    zbpe_status launch_scan(const ScanArgs &A, int grid = 0);
+    zbpe_status launch_scan(const ScanArgs &A, int grid = 0, uint64_t count_hint = 0);
     bool self_list_ok(uint32_t a, bool training);
     zbpe_status rebuild_hot();
     zbpe_status rebuild_home(uint64_t cap);

@@ -420,8 +420,14 @@ struct ScanArgs {
     // the neighbours of every list entry when the lists were built (Engine::build_lists; nullptr:
     // none): nb[e] = pred << 16 | succ, the live tokens before / after position lists[e] at that time
     const uint32_t *nb;
+    // stream form, sparse tiles' candidates batched across tiles (scan_pairs_body BATCH): 0 off, 1 when
+    // the pair is sparse (count * SCAN_BATCH_DENSITY < slots; count unknown: on), 2 always
+    int batch;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
+// batching pays below about one occurrence per 400 slots and costs above it (tools/scan_bands.py:
+// +19 % at 5e-4, -10 % at 5e-3, where most tiles are dense and each one flushes a short batch)
+constexpr uint64_t SCAN_BATCH_DENSITY = 400;
 // the device-held parts of the arguments: pair (batch mode), halo (batch mode, multi-GPU), record
 // window in the arena
 __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
@@ -442,7 +448,7 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
     }
     return ScanArgs{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
                     A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
-                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb};
+                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb, A0.batch};
 }
 
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
@@ -812,7 +818,7 @@ __device__ inline void scan_lds_flush(ScanLds &S, uint32_t *g_left, uint32_t *g_
         if (r) atomicAdd(&g_right[r >> 16], r & 0xffffu);
     }
 }
-template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool BATCH = false>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S);
 template <bool PROF = false, int NT = SCAN_THREADS>
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
@@ -823,7 +829,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
                                                                          ScanLds &S, uint32_t vb, uint32_t vg);
 // one pair scan with resolved arguments: the list form when the shorter token list is short
 // enough, else the stream form
-template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false>
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false, bool BATCH = false>
 __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S) {
     // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
     const uint32_t lists_x = A.st->lists_x;
@@ -855,12 +861,12 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
-    scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT>(A, S);
+    scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH>(A, S);
 }
 // PROF (option sel_prof): the pipeline probes; a separate instantiation, so the production kernel's
 // code and register allocation are untouched by them
-template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false, bool PROF = false>
-__global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
+template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false, bool PROF = false, bool BATCH = false>
+__global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(4))) zbpe_scan_pairs_t(ScanArgs A0) {
     if (PROF && blockIdx.x == 0 && threadIdx.x == 0) {  // the last select's end -> this scan's start
         DevState *st = A0.st;
         const unsigned long long now = wall_clock64();
@@ -871,7 +877,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_pairs_t(ScanArgs A0) {
     if (A0.dyn && A0.st->halt) return;
     __shared__ ScanLds S;
     const ScanArgs A = scan_args_resolve(A0);
-    scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF>(A, S);
+    scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF, BATCH>(A, S);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1245,7 +1251,15 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
         if (threadIdx.x == 0) atomicMax(&A.st->pp_t[3], (unsigned long long)wall_clock64());
     }
 }
-template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT>
+// BATCH: a sparse tile's candidates are not resolved on the spot. Each is saved with its window (the
+// vectors before and at it, the words after: 48 B from the lanes' registers by shuffles) in a per-wave
+// LDS buffer (in the staged tile's space, 85 records at UNROLL 4), and the buffer -- candidates of many
+// tiles -- is resolved one candidate per lane once it could not take another sparse tile (the next
+// tile's loads already issued, so they overlap it). A tile with more than CB_DENSE candidates flushes the
+// buffer and takes the compacted path on its staged tile. (At 1-4 candidates per tile, resolving in
+// place spent as many wave instructions as streaming the tile: SQ_INSTS_VALU x1.9 at density 5e-4.)
+constexpr uint32_t CB_DENSE = 32;
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool BATCH>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S) {
     constexpr int STAGE = 2;                      // vectors per lane per record-staging step
     constexpr uint32_t WREC = 64 * STAGE * 8 / 2;  // at most one occurrence per 2 tokens
@@ -1287,6 +1301,86 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             any = 1;
         }
     }
+    // BATCH: candidates saved with their windows (12 words each: position, the word before the previous
+    // vector, the previous vector, the vector, the two words after it), ncb of them (wave-uniform)
+    uint32_t ncb = 0;
+    uint32_t *cbuf = reinterpret_cast<uint32_t *>(s_tile[wib]);
+    bool batch_on = false;
+    if constexpr (BATCH) {
+        const uint64_t cnt = A.count_deltas ? A.st->top_count : 0u;
+        batch_on = A.batch == 2 || (A.batch == 1 && (cnt == 0 || cnt * SCAN_BATCH_DENSITY < (uint64_t)A.n));
+    }
+    constexpr uint32_t CB_REC = 64 * UNROLL * 4 / 12;  // records the buffer holds
+    auto flush_batch = [&]() {
+        wave_lds_sync();
+        for (uint32_t j0 = 0; j0 < ncb; j0 += 64) {
+        bool hit = false;
+        uint32_t pr = 0;
+        if (j0 + (uint32_t)lane < ncb) {
+            const uint4 *rp = reinterpret_cast<const uint4 *>(cbuf + 12 * (j0 + lane));
+            const uint4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+            const int64_t p = r0.x;
+            const uint32_t w_pp = r0.y;
+            const uint4 pv = make_uint4(r0.z, r0.w, r1.x, r1.y), cv = make_uint4(r1.z, r1.w, r2.x, r2.y);
+            const uint32_t nx = r2.z, ny = r2.w;
+            const int64_t vi = p >> 3;
+            const int k = (int)(p & 7);
+            int64_t start = p;
+            bool fast = true;  // decide in a window (else occ_slow), unless known to be no occurrence
+            bool none = false;
+            bool in_prev = false;  // the window is the previous vector's
+            int ks = k;
+            if (by_b) {  // the occurrence starts at the live slot before p (window slot k + 2)
+                uint32_t tl = HOLE;
+                int l = -1;
+#pragma unroll
+                for (int i = 0; i < 10; i++) {
+                    const uint32_t t = i < 2 ? (i ? pv.w >> 16 : pv.w & 0xffffu) : tok_at(cv, i - 2);
+                    if (i < k + 2 && t != HOLE) { l = i; tl = t; }
+                }
+                if (l >= 0) {
+                    none = tl != A.a;
+                    start = vi * 8 + l - 2;
+                    in_prev = l < 2;
+                    ks = in_prev ? 6 + l : l - 2;
+                } else {  // a run of holes reaches past the window (q < 0: the left shard owns it)
+                    start = prev_live_h(A, p);
+                    none = start < 0 || tok[start] != A.a;
+                    fast = false;
+                }
+            }
+            int r = none ? 0 : -1;
+            if (!none && fast)
+                r = occ_fast1(A, H, in_prev ? vi - 1 : vi, ks, xx, in_prev ? w_pp : pv.w, in_prev ? pv : cv,
+                              in_prev ? cv.x : nx, in_prev ? cv.y : ny);
+            if (r < 0) r = occ_slow(A, H, start, xx);
+            hit = r != 0;
+            pr = (uint32_t)start;
+        }
+        const uint64_t hm = __ballot(hit);
+        if (hm) {
+            any = 1;
+            const uint32_t nh = (uint32_t)__popcll(hm);
+            if (nbuf + nh > WREC) {
+                wave_lds_sync();
+                wave_flush_records(A, wrec, nbuf);
+                nbuf = 0;
+                wave_lds_sync();
+            }
+            // presence: one atomic per run of hits in one block (the records come in stream order
+            // within a tile)
+            const uint32_t blk = hit ? pr / PRES_BLK : 0xffffffffu;
+            const uint32_t blk_up = (uint32_t)__shfl_up((int)blk, 1);
+            if (hit) {
+                wrec[nbuf + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = pr;
+                if (A.pres && (lane == 0 || blk_up != blk)) pres_set(A, pr);
+            }
+            nbuf += nh;
+        }
+        }
+        ncb = 0;
+        wave_lds_sync();
+    };
     for (int64_t wt0 = (int64_t)blockIdx.x * (SCAN_THREADS / 64) + wib; wt0 < nwt; wt0 += 64 * wstride) {
       // block skipping: lane j looks up the presence bit of this wave's j-th next tile, so the
       // lookups of 64 tiles cost one load latency instead of one per tile
@@ -1384,7 +1478,60 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             for (int u = 0; u < UNROLL; u++) cand |= (uint64_t)match8(v[u], key_tok) << (8 * u);
         }
         const bool tile_cand = __ballot(cand != 0) != 0;
-        if (tile_cand) {
+        bool batched = false;  // (wave-uniform) this tile's candidates went to the batch buffer
+        if constexpr (BATCH) {
+            if (tile_cand) {
+                const uint32_t cnt = (uint32_t)__popcll(cand);
+                const uint32_t incl = wave_incl_scan(cnt);
+                const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+                batched = batch_on && total <= CB_DENSE;  // (ncb <= CB_REC - CB_DENSE here: it fits)
+                if (batched) {
+                    uint32_t slot = ncb + incl - cnt;  // this lane's next record
+#pragma unroll
+                    for (int u = 0; u < UNROLL; u++) {
+                        const uint32_t cu = (uint32_t)(cand >> (8 * u)) & 0xffu;
+                        if (!__ballot(cu != 0)) continue;
+                        // the window of vector (u, lane) from the lanes' registers
+                        const uint4 vp = u > 0 ? v[u > 0 ? u - 1 : 0] : make_uint4(0, 0, 0, 0);
+                        uint4 pv;
+                        pv.x = (uint32_t)__shfl_up((int)v[u].x, 1);
+                        pv.y = (uint32_t)__shfl_up((int)v[u].y, 1);
+                        pv.z = (uint32_t)__shfl_up((int)v[u].z, 1);
+                        pv.w = (uint32_t)__shfl_up((int)v[u].w, 1);
+                        uint32_t wpp = (uint32_t)__shfl_up((int)v[u].w, 2);
+                        const uint32_t r63x = (uint32_t)__shfl((int)vp.x, 63), r63y = (uint32_t)__shfl((int)vp.y, 63);
+                        const uint32_t r63z = (uint32_t)__shfl((int)vp.z, 63), r63w = (uint32_t)__shfl((int)vp.w, 63);
+                        const uint32_t r62w = (uint32_t)__shfl((int)vp.w, 62);
+                        uint32_t nx = (uint32_t)__shfl_down((int)v[u].x, 1), ny = (uint32_t)__shfl_down((int)v[u].y, 1);
+                        const uint4 vn = u + 1 < UNROLL ? v[u + 1 < UNROLL ? u + 1 : u] : make_uint4(0, 0, 0, 0);
+                        const uint32_t n0x = (uint32_t)__shfl((int)vn.x, 0), n0y = (uint32_t)__shfl((int)vn.y, 0);
+                        if (lane == 0) {
+                            pv = u > 0 ? make_uint4(r63x, r63y, r63z, r63w) : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, e_prev);
+                            wpp = u > 0 ? r62w : 0xffffffffu;
+                        } else if (lane == 1) {
+                            wpp = u > 0 ? r63w : e_prev;
+                        }
+                        if (lane == 63) {
+                            nx = u + 1 < UNROLL ? n0x : e_nx;
+                            ny = u + 1 < UNROLL ? n0y : e_ny;
+                        }
+                        uint32_t c = cu;
+                        while (c) {
+                            const int k = __builtin_ctz(c);
+                            c &= c - 1;
+                            const uint32_t pos = (uint32_t)((vbase + u * 64 + lane) * 8 + k);
+                            uint4 *rp = reinterpret_cast<uint4 *>(cbuf + 12 * slot);
+                            rp[0] = make_uint4(pos, wpp, pv.x, pv.y);
+                            rp[1] = make_uint4(pv.z, pv.w, v[u].x, v[u].y);
+                            rp[2] = make_uint4(v[u].z, v[u].w, nx, ny);
+                            slot++;
+                        }
+                    }
+                    ncb += total;
+                }
+            }
+        }
+        if (!BATCH && tile_cand) {
 #pragma unroll
             for (int u = 0; u < UNROLL; u++) s_tile[wib][u * 64 + lane] = v[u];
         }
@@ -1396,6 +1543,14 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             wt_next = wt0 + (int64_t)__builtin_ctzll(todo) * wstride;
             todo &= todo - 1;
             if (PIPE) load_tile(wt_next * WT_VEC);
+        }
+        if constexpr (BATCH) {
+            // (a dense tile: the buffer is resolved first, it is the staged tile's space)
+            if (ncb > CB_REC - CB_DENSE || (ncb && tile_cand && !batched)) flush_batch();
+            if (tile_cand && !batched) {
+#pragma unroll
+                for (int u = 0; u < UNROLL; u++) s_tile[wib][u * 64 + lane] = v[u];
+            }
         }
         // window of vector vi of this tile: tok[8 vi - 2 .. 8 vi + 11] from the LDS tile and the edge words
         auto tile_window = [&](int64_t vi, uint32_t &pw, uint4 &cv, uint32_t &nx, uint32_t &ny) {
@@ -1451,7 +1606,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             if (r < 0) r = occ_slow(A, H, start, xx);
             return r != 0;
         };
-        if (tile_cand) {
+        if (tile_cand && !batched) {
         wave_lds_sync();  // the staged tile is visible to every lane of the wave
         if constexpr (COMPACT) {
             // phase 2, dense form: the tile's candidates are compacted into a per-wave LDS list and
@@ -1555,6 +1710,9 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
         wt = wt_next;
         if (!PIPE) load_tile(wt * WT_VEC);
       }
+    }
+    if constexpr (BATCH) {
+        if (ncb) flush_batch();
     }
     if (nbuf) {
         wave_lds_sync();
