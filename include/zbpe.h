@@ -204,7 +204,7 @@ zbpe_status zbpe_trace(zbpe_ctx *ctx, float *rows, size_t cap_rows, size_t *n_ro
 
 /* Profiling diagnostic: the device's per-merge log of the last train, ZBPE_MERGE_LOG_COLS u32 per merge:
  * {pair (first | second << 16), count, live tokens, tied pairs, scan form (1 list), walked list entries,
- * live occurrences of the list's token, 0}. Rows of merges the synchronous path finished are zero
+ * live occurrences of the list's token, 1 when the walk read only the pair's successor range}. Rows of merges the synchronous path finished are zero
  * beyond what it logs. Copies up to cap_rows rows; *n_rows = merges of the last train. */
 #define ZBPE_MERGE_LOG_COLS 8
 zbpe_status zbpe_merge_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_t *n_rows);

@@ -418,3 +418,44 @@ def test_scan_variants_agree_with_oracle(variant, batch, kind, n, vocab, seed):
 def test_scan_batch_option_range(engine):
     with pytest.raises(zbpe.ZbpeError):
         engine.set_option("scan_batch", 3)
+
+
+@pytest.mark.parametrize("min_len,max_rows", [(1, 65536), (64, 8), (1 << 30, 4096)], ids=["all_lists", "few_rows", "none"])
+def test_list_successor_ranges_agree(min_len, max_rows):
+    """Successor-sorted long lists (options list_ranges, range_min_len, range_max_rows): a scan of two
+    pre-build tokens walks only a's entries whose build-time successor was b. Every list sorted, a few
+    rows, or none: the oracle's merges and counts; the merge log shows range walks of ~count entries."""
+    for kind, seed, n, vocab in (("words_utf8", 75, 400000, 1000), ("runs", 76, 60000, 500), ("uniform", 77, 30000, 700)):
+        text = zbpe.synth_corpus(kind, seed, n)
+        r = O.train(text, vocab)
+        for merge_batch in (1, 64):
+            e = zbpe.Engine(0)
+            e.set_option("list_start", 0)
+            e.set_option("list_ratio", 1)
+            e.set_option("compact_den", 2)
+            e.set_option("range_min_len", min_len)
+            e.set_option("range_max_rows", max_rows)
+            e.set_option("merge_batch", merge_batch)
+            m, c, st = e.train(text, vocab)
+            assert m.tolist() == r.merges.tolist() and c.tolist() == r.counts.tolist(), (kind, merge_batch)
+            assert e.verify_counts() == 0
+            L = e.merge_log()
+            ranged = L[:, 7] == 1
+            if min_len == 1 and merge_batch == 64 and kind == "words_utf8":
+                assert ranged.sum() > 0, kind
+                # a range holds the pair's occurrences at the build, so at least its count
+                assert np.all(L[ranged, 5] >= L[ranged, 1]), kind
+            if min_len == 1 << 30:
+                assert ranged.sum() == 0
+            e.close()
+
+
+def test_list_ranges_on_c2_bit_exact():
+    g = [x for x in synth_goldens() if x["n"] >= (1 << 20)]
+    for gg in g[:1]:
+        e = zbpe.Engine(0)
+        e.set_option("list_start", 0)
+        e.set_option("range_min_len", 256)
+        m, c, st = e.train(synth_text(gg), gg["vocab_size"])
+        assert m.tolist() == gg["merges"] and c.tolist() == gg["counts"]
+        e.close()

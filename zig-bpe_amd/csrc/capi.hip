@@ -133,6 +133,10 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
         if (value < 0 || value > 2) return e.fail(ZBPE_INVALID_ARGUMENT, "scan_batch is 0, 1 or 2");
         e.scan_batch = (int)value;
     }
+    else if (k == "list_ranges") e.list_ranges = value != 0;
+    else if (k == "range_min_len" && value >= 1 && value < (1ll << 32)) e.range_min_len = (uint32_t)value;
+    else if (k == "range_max_rows" && value >= 0 && value <= 65536) e.range_max_rows = (uint32_t)value;
+    else if (k == "range_max_len" && value >= 1 && value < (1ll << 32)) e.range_max_len = (uint32_t)value;
     else if (k == "block_skip") e.block_skip = value != 0;
     else if (k == "trace") e.trace_on = value != 0;
     else if (k == "merge_batch" && value >= 1) e.merge_batch = (uint32_t)std::min<int64_t>(value, zbpe::MAX_BATCH);
@@ -214,7 +218,7 @@ zbpe_status zbpe_merge_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_
     const size_t k = std::min(cap_rows, *n_rows);
     for (size_t i = 0; i < k; i++) {
         const zbpe::MergeLog &m = L[i];
-        const uint32_t r[ZBPE_MERGE_LOG_COLS] = {m.key, m.count, m.live, m.ties, m.mode, m.list_len, m.key_live, 0};
+        const uint32_t r[ZBPE_MERGE_LOG_COLS] = {m.key, m.count, m.live, m.ties, m.mode, m.list_len, m.key_live, m.range};
         memcpy(rows + i * ZBPE_MERGE_LOG_COLS, r, sizeof r);
     }
     return ZBPE_OK;

@@ -60,6 +60,10 @@ void Engine::release() {
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_cs); f(d_rtk); f(d_sizes);
     f(d_enc_cnt); f(d_enc_ctr); f(d_nb); f(d_ord_pos); f(d_ord_ent); f(d_sort_tmp);
+    f(d_dir); f(d_dir_row); f(d_row_tok); f(d_dir_tmp); f(d_sort_hist);
+    d_dir = d_dir_row = d_row_tok = d_sort_hist = nullptr; d_dir_tmp = nullptr;
+    dir_cap = dir_row_cap = row_tok_cap = dir_tmp_cap = sort_hist_cap = 0;
+    dirs_built = false;
     d_ord_pos = nullptr; d_ord_ent = nullptr; d_sort_tmp = nullptr; ord_pos_cap = ord_ent_cap = sort_tmp_cap = 0;
     if (h_ord) (void)hipHostFree(h_ord);
     h_ord = nullptr; h_ord_cap = 0;
@@ -289,7 +293,7 @@ zbpe_status Engine::compact_train(uint32_t X) {
     const bool want = list_mode && pres_vp <= PRES_MAX_VP && (uint64_t)n_slots < 0xF0000000ull &&
                       (lists_on || list_start == 0 || (uint64_t)h_st->top_count * list_start * ranks < live_ref);
     if (want && !(dist() && replicate_late)) {  // sharded: lists come with the replication (run_batch)
-        CHECK(build_lists(X, list_ratio));
+        CHECK(build_lists(X, list_ratio, true));
     } else {
         HIP_OK(hipMemsetAsync(&d_st->arena_top, 0, 4, stream));
         HIP_OK(hipMemsetAsync(&d_st->arena_rep, 0, 4, stream));
@@ -386,7 +390,7 @@ zbpe_status Engine::max_over_ranks(uint32_t v, uint32_t *out) {
     return ZBPE_OK;
 }
 
-zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio) {
+zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio, bool ranges) {
     const int64_t n = n_slots;
     if (dist()) {  // (sharded, replicate_late off) the arena limit stays replicated: grown from the largest shard
         uint32_t nmax = 0;
@@ -410,6 +414,34 @@ zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio) {
     zbpe_list_scatter<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt, T.lst_off,
                                                                        T.lst_len, d_lists, list_nb ? d_nb : nullptr);
     LAUNCH_OK();
+    // successor ranges: training on one stream (a shard's edge entries have no successor in it)
+    dirs_built = false;
+    if (ranges && list_ranges && list_nb && (!dist() || replicated) && lists_x + 1 <= DIR_MAX_TOK && range_max_rows) {
+        dir_w = lists_x + 2;
+        CHECK(ensure(&d_dir_row, dir_row_cap, 65536, "list directory rows"));
+        CHECK(ensure(&d_row_tok, row_tok_cap, 2 * (size_t)range_max_rows + 4, "list directory tokens"));
+        CHECK(ensure(&d_dir, dir_cap, (size_t)range_max_rows * dir_w, "list directory"));
+        CHECK(ensure(&d_dir_tmp, dir_tmp_cap, (size_t)n + 64, "list sort copy"));
+        // chunks: at most one partial chunk per row beyond the entries' whole chunks
+        const uint64_t max_chunks = (uint64_t)n / SORT_CHUNK + range_max_rows + 1;
+        CHECK(ensure(&d_sort_hist, sort_hist_cap, (size_t)max_chunks * (lists_x + 1), "list sort chunk histograms"));
+        uint32_t *row_ch0 = d_row_tok + range_max_rows, *rows = row_ch0 + range_max_rows + 1;
+        zbpe_dir_rows<<<1, 1024, 0, stream>>>(T.lst_len, lists_x, range_min_len, range_max_len, range_max_rows, d_dir_row, d_row_tok,
+                                              row_ch0, rows);
+        LAUNCH_OK();
+        zbpe_list_sort_hist<<<(unsigned)max_chunks, DIR_THREADS, 0, stream>>>(d_lists, d_nb, d_dir_tmp, T.lst_off, T.lst_len, rows, d_row_tok,
+                                                                               row_ch0, lists_x, d_sort_hist);
+        LAUNCH_OK();
+        zbpe_list_sort_cols<<<dim3((lists_x + 1 + 255) / 256, std::min<uint32_t>(range_max_rows, 64)), 256, 0, stream>>>(d_sort_hist, rows, row_ch0, lists_x,
+                                                                                                  d_dir, dir_w);
+        LAUNCH_OK();
+        zbpe_list_sort_row<<<std::min<uint32_t>(range_max_rows, 1024), DIR_THREADS, 0, stream>>>(T.lst_off, T.lst_len, rows, d_row_tok, lists_x, d_dir, dir_w);
+        LAUNCH_OK();
+        zbpe_list_sort_scatter<<<(unsigned)max_chunks, DIR_THREADS, 0, stream>>>(d_lists, d_nb, d_dir_tmp, T.lst_off, T.lst_len, rows,
+                                                                                  d_row_tok, row_ch0, lists_x, d_sort_hist, d_dir, dir_w);
+        LAUNCH_OK();
+        dirs_built = true;
+    }
     if (dist()) {  // arena_rep (the replicated fill that halts are decided on) >= every rank's arena_top
         CHECK(sync_state());
         uint32_t top_max = 0;
@@ -427,6 +459,9 @@ zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio) {
 // list scans may filter list entries by their build-time neighbours (kernels.hpp scan_dispatch)
 void Engine::set_list_nb(ScanArgs &A) const {
     A.nb = lists_on && nb_built ? d_nb : nullptr;
+    A.dir_row = lists_on && dirs_built && A.nb && A.count_deltas ? d_dir_row : nullptr;
+    A.dir = d_dir;
+    A.dir_w = dir_w;
 }
 
 static uint32_t count_bin_lo(int b) {
@@ -1100,7 +1135,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         HIP_OK(hipEventRecord(ev[3], stream));
         CHECK(compact());  // this shard's live tokens, contiguous
         CHECK(replicate());
-        CHECK(build_lists(X0, list_ratio));
+        CHECK(build_lists(X0, list_ratio, true));
         HIP_OK(hipEventRecord(ev[4], stream));
         HIP_OK(hipEventSynchronize(ev[4]));
         float ms;

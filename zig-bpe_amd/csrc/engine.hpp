@@ -129,6 +129,16 @@ struct Engine {
     // build-time neighbours of the list entries (the filtered list walk; option "list_nb")
     uint32_t *d_nb = nullptr;  // pred << 16 | succ of every list entry at the build
     size_t nb_cap = 0;
+    // successor ranges of the long lists (zbpe_list_sort_succ): rows, the token of each row, the sort's copy
+    uint32_t *d_dir = nullptr, *d_dir_row = nullptr, *d_row_tok = nullptr, *d_sort_hist = nullptr;
+    uint2 *d_dir_tmp = nullptr;
+    size_t dir_cap = 0, dir_row_cap = 0, row_tok_cap = 0, dir_tmp_cap = 0, sort_hist_cap = 0;
+    uint32_t dir_w = 0;
+    bool dirs_built = false;
+    uint32_t list_ranges = 1;            // option "list_ranges": successor-sorted long lists (0: off)
+    uint32_t range_min_len = 1u << 14;   // option "range_min_len": lists that get a directory row
+    uint32_t range_max_rows = 4096;      // option "range_max_rows"
+    uint32_t range_max_len = 0xFFFFFFFEu;  // option "range_max_len": longer lists keep the filtered walk
     bool list_nb = true, nb_built = false;
     bool list_streak = false;   // the last batch used list scans only
     int list_grid = 0;          // scan grid after such a batch (option "list_grid"; 0 = the full grid)
@@ -240,7 +250,7 @@ struct Engine {
     bool holes_over() const;
     zbpe_status max_over_ranks(uint32_t v, uint32_t *out);
     zbpe_status grow_arena(uint64_t need);
-    zbpe_status build_lists(uint32_t lists_x, uint32_t ratio);
+    zbpe_status build_lists(uint32_t lists_x, uint32_t ratio, bool ranges = false);
     void set_list_nb(ScanArgs &A) const;
     zbpe_status replicate();
     zbpe_status launch_argmax(uint32_t X, int roll);

@@ -423,6 +423,11 @@ struct ScanArgs {
     // stream form, sparse tiles' candidates batched across tiles (scan_pairs_body BATCH): 0 off, 1 when
     // the pair is sparse (count * SCAN_BATCH_DENSITY < slots; count unknown: on), 2 always
     int batch;
+    // successor ranges of the long lists (Engine::build_lists, zbpe_list_sort_succ; nullptr: none):
+    // dir_row[t] = t's row or NO_LIST; entries of t's list with build-time successor s (s < lists_x,
+    // lists_x for the stream's end) at [dir[row * dir_w + s], dir[row * dir_w + s + 1])
+    const uint32_t *dir_row, *dir;
+    uint32_t dir_w;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // batching pays below about one occurrence per 400 slots and costs above it (tools/scan_bands.py:
@@ -448,7 +453,8 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
     }
     return ScanArgs{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
                     A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
-                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb, A0.batch};
+                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb, A0.batch,
+                    A0.dir_row, A0.dir, A0.dir_w};
 }
 
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
@@ -826,7 +832,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
                                                                      uint32_t vb, uint32_t vg);
 template <bool PROF = false, int NT = SCAN_THREADS>
 __device__ __attribute__((always_inline)) inline void scan_list_filtered(const ScanArgs A, bool by_b, uint32_t off, uint32_t len,
-                                                                         ScanLds &S, uint32_t vb, uint32_t vg);
+                                                                         ScanLds &S, uint32_t vb, uint32_t vg, bool all = false);
 // one pair scan with resolved arguments: the list form when the shorter token list is short
 // enough, else the stream form
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false, bool BATCH = false>
@@ -836,8 +842,27 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
     if (A.lists && A.a != A.b && A.st->lists_valid) {
         // lengths and offsets in one round trip
         const uint32_t la = A.lst_len[A.a], lb = A.lst_len[A.b], oa = A.lst_off[A.a], ob = A.lst_off[A.b];
+        const uint32_t ra = A.dir_row ? A.dir_row[A.a] : NO_LIST;
         const bool by_b = lb < la;
         const uint32_t len = by_b ? lb : la;
+        // a's list sorted by build-time successor (a long list): by the invariant below, every occurrence
+        // is in the range of successor b -- about the pair's count of entries, wherever a's list is
+        if (ra != NO_LIST && A.a < lists_x && A.b < lists_x) {
+            const uint64_t rb = (uint64_t)ra * A.dir_w + A.b;
+            const uint32_t r0 = A.dir[rb], r1 = A.dir[rb + 1];
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                A.st->scan_mode = 1;
+                if (A.log) {
+                    A.log[A.X - 256].mode = 1;
+                    A.log[A.X - 256].list_len = r1 - r0;
+                    A.log[A.X - 256].key_live = A.tokcnt ? (uint32_t)A.tokcnt[A.a] : 0u;
+                    A.log[A.X - 256].range = 1;
+                }
+                if (PROF) A.st->pp_t[4] = 1;
+            }
+            scan_list_filtered<PROF>(A, false, r0, r1 - r0, S, blockIdx.x, gridDim.x, true);
+            return;
+        }
         // Both tokens existed when the lists were built: since then a position's successor (its
         // predecessor) has only ever changed into a token created after the build (a merge at the
         // successor turns it into the new token; a hole appears only where the position itself is
@@ -971,14 +996,17 @@ __global__ void __launch_bounds__(256) zbpe_encode_apply_batch(uint16_t *tok, in
 // a late merge's scan, not the bytes.
 constexpr int LIST_EPT = 16;  // the most entries a thread filters
 // (vb, vg: this workgroup's index among the vg workgroups that walk the list; NT threads each)
+// all: every entry of [off, off + len) is a candidate (a successor range, zbpe_list_sort_succ: no
+// neighbour words to filter), at most four per thread.
 template <bool PROF, int NT>
 __device__ __attribute__((always_inline)) inline void scan_list_filtered(const ScanArgs A, bool by_b, uint32_t off, uint32_t len,
-                                                                         ScanLds &S, uint32_t vb, uint32_t vg) {
+                                                                         ScanLds &S, uint32_t vb, uint32_t vg, bool all) {
     // entries per thread: about one match per two lanes (a wave resolves its matches 64 at a time, one
     // latency chain per round): the list's length over the pair's count (training; encode: 4)
     const uint32_t cnt = A.count_deltas ? A.st->top_count : 0u;
     const uint32_t ratio = cnt ? len / cnt : 8u;
-    const uint32_t ept = ratio >= 32 ? 16u : ratio >= 16 ? 8u : ratio >= 8 ? 4u : ratio >= 4 ? 2u : 1u;
+    const uint32_t ept = all ? (ratio >= 4 ? 4u : ratio >= 2 ? 2u : 1u)
+                             : ratio >= 32 ? 16u : ratio >= 16 ? 8u : ratio >= 8 ? 4u : ratio >= 4 ? 2u : 1u;
     const uint32_t per_block = NT * ept;
     const uint32_t ab = off & ~7u;                    // 16-B aligned start of the neighbour words
     const uint32_t span = off + len - ab;             // entries from ab to the list's end
@@ -999,7 +1027,13 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     for (uint32_t b0 = vb * per_block; b0 < span; b0 += gstride) {
         const uint32_t e0 = ab + b0 + threadIdx.x * ept;  // this thread's first entry (absolute)
         uint32_t mk = 0;
-        if (e0 < off + len) {
+        if (all) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t e = e0 + k;
+                mk |= ((uint32_t)k < ept && e >= off && e < off + len) ? (1u << k) : 0u;
+            }
+        } else if (e0 < off + len) {
             if (ept >= 8) {  // 16-B aligned words (ab and ept are multiples of 8)
                 const uint4 *q = reinterpret_cast<const uint4 *>(NB + e0);
                 const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -1855,6 +1889,203 @@ __global__ void __launch_bounds__(LIST_THREADS) zbpe_list_scatter(const uint16_t
                     const uint32_t pd = k > 0 ? tok_at(v, k - 1) : before;
                     nb[j] = pd << 16 | sc;
                 }
+            }
+        }
+    }
+}
+
+// Successor ranges (round 3). A long list (at least min_len entries) gets a directory row, and its
+// entries (positions and neighbour words together) are reordered by build-time successor: a chunked
+// counting sort over the lists_x + 1 successor bins (lists_x: the stream's end) -- per chunk of
+// SORT_CHUNK entries an LDS histogram and a copy to tmp; per (row, bin) the chunks' exclusive offsets;
+// per row the bins' offsets (the row); per chunk the scatter back from tmp. A scan of (a, b) with both
+// tokens older than the build then walks only the entries of a's list whose successor was b
+// (scan_dispatch), about the pair's count instead of the list's length.
+constexpr uint32_t DIR_MAX_TOK = 36 * 1024;  // successor bins of one sorting workgroup (144 KiB of LDS)
+constexpr int DIR_THREADS = 1024;
+constexpr uint32_t SORT_CHUNK = 1u << 18;  // list entries per sorting workgroup
+// one block: rows in token order for lists of min_len..max_len entries (at most max_rows); every other
+// token NO_LIST. rows[0] = rows, rows[1] = chunks, row_tok[r], row_ch0[r] = the row's first chunk
+__global__ void __launch_bounds__(1024) zbpe_dir_rows(const uint32_t *__restrict__ lst_len, uint32_t ntok, uint32_t min_len,
+                                                      uint32_t max_len, uint32_t max_rows, uint32_t *__restrict__ dir_row,
+                                                      uint32_t *__restrict__ row_tok, uint32_t *__restrict__ row_ch0,
+                                                      uint32_t *__restrict__ rows) {
+    __shared__ uint32_t s_part[1024], s_ch[1024];
+    constexpr uint32_t PER = 65536 / 1024;
+    const uint32_t t0 = threadIdx.x * PER;
+    auto want = [&](uint32_t t) { return t < ntok && lst_len[t] != NO_LIST && lst_len[t] >= min_len && lst_len[t] <= max_len; };
+    uint32_t c = 0;
+    for (uint32_t t = t0; t < t0 + PER; t++) c += want(t) ? 1u : 0u;
+    s_part[threadIdx.x] = c;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
+        const uint32_t v = threadIdx.x >= (uint32_t)off ? s_part[threadIdx.x - off] : 0;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    // this thread's rows (below max_rows) and their chunks
+    uint32_t r = s_part[threadIdx.x] - c, ch = 0;
+    for (uint32_t t = t0, q = r; t < t0 + PER; t++)
+        if (want(t)) { if (q < max_rows) ch += (lst_len[t] + SORT_CHUNK - 1) / SORT_CHUNK; q++; }
+    s_ch[threadIdx.x] = ch;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = threadIdx.x >= (uint32_t)off ? s_ch[threadIdx.x - off] : 0;
+        __syncthreads();
+        s_ch[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t c0 = s_ch[threadIdx.x] - ch;
+    for (uint32_t t = t0; t < t0 + PER; t++) {
+        uint32_t row = NO_LIST;
+        if (want(t)) {
+            if (r < max_rows) {
+                row = r;
+                row_tok[r] = t;
+                row_ch0[r] = c0;
+                c0 += (lst_len[t] + SORT_CHUNK - 1) / SORT_CHUNK;
+            }
+            r++;
+        }
+        dir_row[t] = row;
+    }
+    if (threadIdx.x == 1023) {
+        const uint32_t nr = min(s_part[1023], max_rows);
+        rows[0] = nr;
+        rows[1] = s_ch[1023];
+        row_ch0[nr] = s_ch[1023];
+    }
+}
+// the chunk's row (binary search over the rows' first chunks) and its entries [b0, b1) of the list
+struct SortChunk {
+    uint32_t r, t, off, b0, b1;
+};
+__device__ inline bool sort_chunk(uint32_t c, const uint32_t *rows, const uint32_t *row_tok, const uint32_t *row_ch0,
+                                  const uint32_t *lst_off, const uint32_t *lst_len, SortChunk &k) {
+    const uint32_t nr = rows[0];
+    if (c >= rows[1]) return false;
+    uint32_t lo = 0, hi = nr;  // row_ch0[lo] <= c < row_ch0[lo + 1]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (row_ch0[mid] <= c) lo = mid; else hi = mid;
+    }
+    k.r = lo;
+    k.t = row_tok[lo];
+    k.off = lst_off[k.t];
+    const uint32_t len = lst_len[k.t];
+    k.b0 = (c - row_ch0[lo]) * SORT_CHUNK;
+    k.b1 = min(len, k.b0 + SORT_CHUNK);
+    return true;
+}
+__device__ inline uint32_t succ_bin(uint32_t w, uint32_t ntok) {
+    const uint32_t s = w & 0xFFFFu;
+    return s < ntok ? s : ntok;
+}
+// per chunk: LDS histogram of the successor bins -> chunk_hist[c][bin]; the entries copied to tmp
+__global__ void __launch_bounds__(DIR_THREADS) zbpe_list_sort_hist(const uint32_t *__restrict__ lists, const uint32_t *__restrict__ nb,
+                                                                   uint2 *__restrict__ tmp, const uint32_t *__restrict__ lst_off,
+                                                                   const uint32_t *__restrict__ lst_len, const uint32_t *__restrict__ rows,
+                                                                   const uint32_t *__restrict__ row_tok, const uint32_t *__restrict__ row_ch0,
+                                                                   uint32_t ntok, uint32_t *__restrict__ chunk_hist) {
+    __shared__ uint32_t h[DIR_MAX_TOK + 1];
+    SortChunk k;
+    if (!sort_chunk(blockIdx.x, rows, row_tok, row_ch0, lst_off, lst_len, k)) return;
+    const uint32_t nbin = ntok + 1, tid = threadIdx.x;
+    for (uint32_t i = tid; i < nbin; i += DIR_THREADS) h[i] = 0;
+    __syncthreads();
+    for (uint32_t i0 = k.b0 + tid; i0 < k.b1; i0 += 4 * DIR_THREADS) {  // four entries per thread per step
+        uint32_t w[4], q[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + u * DIR_THREADS;
+            w[u] = i < k.b1 ? nb[k.off + i] : 0u;
+            q[u] = i < k.b1 ? lists[k.off + i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + u * DIR_THREADS;
+            if (i < k.b1) {
+                atomicAdd(&h[succ_bin(w[u], ntok)], 1u);
+                tmp[k.off + i] = make_uint2(q[u], w[u]);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nbin; i += DIR_THREADS) chunk_hist[(uint64_t)blockIdx.x * nbin + i] = h[i];
+}
+// per (row, bin): the row's chunks' exclusive offsets within the bin (in place); the bin's size -> dir
+__global__ void __launch_bounds__(256) zbpe_list_sort_cols(uint32_t *__restrict__ chunk_hist, const uint32_t *__restrict__ rows,
+                                                           const uint32_t *__restrict__ row_ch0, uint32_t ntok,
+                                                           uint32_t *__restrict__ dir, uint32_t dir_w) {
+    const uint32_t nbin = ntok + 1, b = blockIdx.x * 256 + threadIdx.x, nr = rows[0];
+    if (b >= nbin) return;
+    for (uint32_t r = blockIdx.y; r < nr; r += gridDim.y) {
+        uint32_t run = 0;
+        for (uint32_t c = row_ch0[r]; c < row_ch0[r + 1]; c++) {
+            const uint64_t i = (uint64_t)c * nbin + b;
+            const uint32_t v = chunk_hist[i];
+            chunk_hist[i] = run;
+            run += v;
+        }
+        dir[(uint64_t)r * dir_w + b] = run;
+    }
+}
+// per row: the bins' exclusive offsets -> the row (absolute arena indices; the entry past the last bin
+// is the list's end)
+__global__ void __launch_bounds__(DIR_THREADS) zbpe_list_sort_row(const uint32_t *__restrict__ lst_off, const uint32_t *__restrict__ lst_len,
+                                                                  const uint32_t *__restrict__ rows, const uint32_t *__restrict__ row_tok,
+                                                                  uint32_t ntok, uint32_t *__restrict__ dir, uint32_t dir_w) {
+    __shared__ uint32_t s_w[DIR_THREADS / 64];
+    const uint32_t nr = rows[0];
+    for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {  // (block-uniform)
+    const uint32_t t = row_tok[r], off = lst_off[t], len = lst_len[t], nbin = ntok + 1, tid = threadIdx.x;
+    uint32_t *D = dir + (uint64_t)r * dir_w;
+    const uint32_t per = (nbin + DIR_THREADS - 1) / DIR_THREADS, b0 = min(nbin, tid * per), b1 = min(nbin, b0 + per);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; b++) sum += D[b];
+    const uint32_t incl = wave_incl_scan(sum);
+    if ((tid & 63) == 63) s_w[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t base = incl - sum;
+    for (uint32_t w = 0; w < (tid >> 6); w++) base += s_w[w];
+    for (uint32_t b = b0; b < b1; b++) {
+        const uint32_t c = D[b];
+        D[b] = off + base;
+        base += c;
+    }
+    if (tid == 0) D[nbin] = off + len;
+    __syncthreads();  // s_w reused by the next row
+    }
+}
+// per chunk: cursors = bin start + the chunk's offset within the bin; the chunk's entries scattered
+// from tmp back into the list
+__global__ void __launch_bounds__(DIR_THREADS) zbpe_list_sort_scatter(uint32_t *__restrict__ lists, uint32_t *__restrict__ nb,
+                                                                      const uint2 *__restrict__ tmp, const uint32_t *__restrict__ lst_off,
+                                                                      const uint32_t *__restrict__ lst_len, const uint32_t *__restrict__ rows,
+                                                                      const uint32_t *__restrict__ row_tok, const uint32_t *__restrict__ row_ch0,
+                                                                      uint32_t ntok, const uint32_t *__restrict__ chunk_hist,
+                                                                      const uint32_t *__restrict__ dir, uint32_t dir_w) {
+    __shared__ uint32_t h[DIR_MAX_TOK + 1];
+    SortChunk k;
+    if (!sort_chunk(blockIdx.x, rows, row_tok, row_ch0, lst_off, lst_len, k)) return;
+    const uint32_t nbin = ntok + 1, tid = threadIdx.x;
+    const uint32_t *D = dir + (uint64_t)k.r * dir_w;
+    for (uint32_t i = tid; i < nbin; i += DIR_THREADS) h[i] = D[i] + chunk_hist[(uint64_t)blockIdx.x * nbin + i];
+    __syncthreads();
+    for (uint32_t i0 = k.b0 + tid; i0 < k.b1; i0 += 4 * DIR_THREADS) {
+        uint2 e[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + u * DIR_THREADS;
+            e[u] = i < k.b1 ? tmp[k.off + i] : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (i0 + u * DIR_THREADS < k.b1) {
+                const uint32_t j = atomicAdd(&h[succ_bin(e[u].y, ntok)], 1u);  // absolute arena index
+                lists[j] = e[u].x;
+                nb[j] = e[u].y;
             }
         }
     }

@@ -100,7 +100,7 @@ struct MergeLog {
     uint32_t mode;     // 0: stream scan, 1: list scan
     uint32_t list_len; // list scan: entries of the walked occurrence list
     uint32_t key_live; // list scan: live occurrences of the list's token (the walk's useful entries)
-    uint32_t pad;
+    uint32_t range;    // list scan: 1 when it walked only the pair's successor range of a's list
 };
 
 struct Tables {

@@ -152,7 +152,7 @@ EXPORTS = (
     "zbpe_set_option", "zbpe_format_time_stats", "zbpe_bench_scan", "zbpe_bench_train_scan", "zbpe_merge_log", "zbpe_trace", "zbpe_scan_log", "zbpe_zig_order_winner", "zbpe_version",
     "zbpe_stats_size", "zbpe_bench_recount",
 )
-MERGE_LOG_COLUMNS = ("key", "count", "live", "ties", "list_scan", "list_len", "key_live", "zero")
+MERGE_LOG_COLUMNS = ("key", "count", "live", "ties", "list_scan", "list_len", "key_live", "range")
 TRACE_COLUMNS = ("merge", "count", "live", "slots", "streamed", "scan_ms", "replace_ms", "select_ms", "wall_ms",
                  "self_pair", "ties")
 
