@@ -157,6 +157,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "list_start" && value >= 0) e.list_start = (uint64_t)value;
     else if (k == "hot_target" && value > 0) e.hot_target = (uint64_t)value;
     else if (k == "sel_growth" && value >= 0) e.sel_growth = (uint32_t)value;
+    else if (k == "sel_margin" && value >= 0 && value < (1ll << 31)) e.sel_margin = (uint32_t)value;
     else if (k == "print_runtime") e.print_runtime = value != 0;
     else if (k == "encode_batch" && value >= 1) e.enc_batch = (uint32_t)value;
     else if (k == "self_list_ratio" && value >= 0) e.self_list_ratio = (uint32_t)value;

@@ -1221,8 +1221,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             // about four hot entries per thread (the list grows by the new ids of the batch), and
             // the delta words to clear
             // (the grid only sets the parallelism: the argmax loops over whatever the hot list holds at run time)
-            const uint64_t hot_est = std::min<uint64_t>(T.hot_cap, (uint64_t)h_st->hot_len + (uint64_t)K * sel_growth + 4096);
-            const uint64_t work = std::max<uint64_t>(hot_est / 4, C ? 0ull : 2ull * X / 4);  // refresh blocks clear the deltas
+            const uint64_t hot_est = std::min<uint64_t>(T.hot_cap, (uint64_t)h_st->hot_len + (uint64_t)K * sel_growth + sel_margin);
+            const uint64_t work = std::max<uint64_t>(hot_est / SEL_U, C ? 0ull : 2ull * X / 4);  // refresh blocks clear the deltas
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,

@@ -195,8 +195,10 @@ struct Engine {
         double tm_count = 0, tm_select = 0, tm_replace = 0, tm_comm = 0;  // stage times of the timed batch merges
         double batch_s = 0;                                   // device span of the batches
     } run;
-    uint64_t hot_target = 1u << 15;  // ids the hot list aims to hold after a rebuild
-    uint32_t sel_growth = 1024;      // hot-list growth per merge assumed when sizing zbpe_select_next's argmax grid
+    uint64_t hot_target = 1u << 11;  // ids the hot list aims to hold after a rebuild (short: one argmax
+                                     // workgroup, no ticket; a rebuild every few hundred merges)
+    uint32_t sel_growth = 16;        // hot-list growth per merge assumed when sizing zbpe_select_next's argmax grid
+    uint32_t sel_margin = 0;         // + this many entries (option "sel_margin")
     uint64_t hot_rebuilds = 0, home_rebuilds = 0;
     hipEvent_t ev[8] = {};
     bool print_runtime = true;  // generateInitialTokens' runtime line on stderr (option "print_runtime")

@@ -3746,6 +3746,7 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
 constexpr int NEXT_THREADS = 512;  // launch bounds: 4 waves per SIMD (two workgroups per CU; the decision spills a little)
 constexpr int NEXT_CAND = 64;          // keys kept per argmax block at the block's max
 constexpr int NEXT_MAX_SEL = 1024;     // argmax blocks (the reducer keeps one LDS entry per block)
+constexpr int SEL_U = 8;               // hot entries per argmax thread per step (loads issued together)
 constexpr int NEXT_TIE_LDS = 512;      // tied keys the decision reads from LDS (more: from N.tie_list)
 struct NextArgs {
     BeginArgs B;          // merge X + 1 (B.X < x_end)
@@ -3874,6 +3875,11 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         }
     }
     const uint32_t bx = blockIdx.x - nref;  // argmax block index
+    // one argmax workgroup (a short hot list): it is the last one by construction -- no ticket, no
+    // partials through global memory
+    const bool single = N.sel_blocks == 1;
+    __shared__ uint32_t s_lastpair;
+    MaxRec R{0, 0, NO_ID};
     {
         const uint32_t G = N.sel_blocks * NEXT_THREADS;
         if (!nref)  // (no refresh workgroups: the argmax ones clear the deltas)
@@ -3894,35 +3900,39 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
                     lt[got++] = (uint32_t)__shfl((int)t, l);
                 }
             }
-            if (lane == 0)
-                __hip_atomic_store(N.lastpair, got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                const uint32_t lp = got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0u;
+                __hip_atomic_store(N.lastpair, lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_lastpair = lp;
+            }
         }
-        // four hot entries per thread per step, every load of a step issued together
+        // SEL_U hot entries per thread per step, every load of a step issued together
         MaxRec r{0, 0, NO_ID};
-        uint32_t ids[4] = {NO_ID, NO_ID, NO_ID, NO_ID}, cs[4] = {0, 0, 0, 0}, ks[4] = {0, 0, 0, 0};
+        uint32_t ids[SEL_U], cs[SEL_U], ks[SEL_U];
+#pragma unroll
+        for (int u = 0; u < SEL_U; u++) { ids[u] = NO_ID; cs[u] = 0; ks[u] = 0; }
         bool one_step = true;
-        for (uint32_t i0 = bx * NEXT_THREADS + tid; i0 < nh; i0 += 4 * G) {
+        for (uint32_t i0 = bx * NEXT_THREADS + tid; i0 < nh; i0 += SEL_U * G) {
             one_step = i0 == bx * NEXT_THREADS + tid;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < SEL_U; u++) {
                 const unsigned long long e = i0 + u * G < nh ? T.hot[i0 + u * G] : (unsigned long long)NO_ID;
                 ids[u] = (uint32_t)e;
                 ks[u] = (uint32_t)(e >> 32);  // the key rides along: the block's keys at its max come from registers
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) cs[u] = ids[u] != NO_ID ? T.id_cnt[ids[u]] : 0u;
+            for (int u = 0; u < SEL_U; u++) cs[u] = ids[u] != NO_ID ? T.id_cnt[ids[u]] : 0u;
 #pragma unroll
-            for (int u = 0; u < 4; u++)
+            for (int u = 0; u < SEL_U; u++)
                 if (cs[u] >= theta && cs[u]) r = max_combine(r, MaxRec{cs[u], 1u, ids[u]});
         }
         if (tid == 0) s_nc = 0;
-        const MaxRec R = block_max(r, sm);
+        R = block_max(r, sm);
         // the block's keys at its max (from the registers when the thread's entries fit one step)
         if (R.cnt && r.cnt == R.cnt) {
-            if (one_step && 4 * G >= nh) {
+            if (one_step && SEL_U * G >= nh) {
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < SEL_U; u++) {
                     if (ids[u] != NO_ID && cs[u] == R.cnt) {
                         const uint32_t j = atomicAdd(&s_nc, 1u);
                         if (j < NEXT_CAND) s_key[j] = ks[u];
@@ -3941,9 +3951,9 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         }
         __syncthreads();
         // write-through stores: the last block reads them (block_ticket_last)
-        if (tid < min(s_nc, (uint32_t)NEXT_CAND))
+        if (!single && tid < min(s_nc, (uint32_t)NEXT_CAND))
             __hip_atomic_store(&N.cand[bx * NEXT_CAND + tid], s_key[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tid == 0) {
+        if (!single && tid == 0) {
             __hip_atomic_store(&partial[bx].cnt, R.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&partial[bx].ties, R.cnt ? s_nc : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&partial[bx].id, R.id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3952,7 +3962,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         }
     }
     if (N.prof && tid == 0) atomicMax(&st->sel_ta, (unsigned long long)wall_clock64());
-    if (!block_ticket_last(&st->ticket, N.sel_blocks, &s_flag)) return;
+    if (!single && !block_ticket_last(&st->ticket, N.sel_blocks, &s_flag)) return;
     const bool pfx = nref && N.cs && N.B.log[X - 256].ties > 1;  // the refresh precomputes the carries (its predicate)
     // the next launch's refresh count (the launch before this one used it and has ended)
     if (tid < 9) st_wt(N.rtk + ((X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
@@ -3970,16 +3980,27 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     }
     // ---- the last block: argmax, roll of merge X -------------------------------------------------
     // the stream's last pair count (block 0 stored it write-through): in flight with the partials
-    const uint32_t lastpair_wt = tid == 0 && N.world == 1 ? ld_wt(N.lastpair) : NO_ID;
-    MaxRec q{0, 0, NO_ID};
-    for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
-        const MaxRec p{ld_wt(&partial[b].cnt), ld_wt(&partial[b].ties), ld_wt(&partial[b].id)};
-        s_pc[b] = p.cnt;
-        s_pt[b] = p.ties;
-        s_pk[b] = ld_wt(N.pkey + b);  // (with the partial: no second round trip once the max is known)
-        q = max_combine(q, p);
+    const uint32_t lastpair_wt = tid == 0 && N.world == 1 ? (single ? s_lastpair : ld_wt(N.lastpair)) : NO_ID;
+    MaxRec Q = R;
+    if (single) {  // (s_nc, s_key from the argmax above; the barrier after it published them)
+        if (tid == 0) {
+            s_pc[0] = R.cnt;
+            s_pt[0] = R.cnt ? s_nc : 0u;
+            s_pk[0] = s_nc == 1 ? s_key[0] : NO_ID;
+        }
+        Q.ties = R.cnt ? s_nc : 0u;
+        __syncthreads();
+    } else {
+        MaxRec q{0, 0, NO_ID};
+        for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
+            const MaxRec p{ld_wt(&partial[b].cnt), ld_wt(&partial[b].ties), ld_wt(&partial[b].id)};
+            s_pc[b] = p.cnt;
+            s_pt[b] = p.ties;
+            s_pk[b] = ld_wt(N.pkey + b);  // (with the partial: no second round trip once the max is known)
+            q = max_combine(q, p);
+        }
+        Q = block_max(q, sm);  // (its barriers also publish s_pc / s_pt)
     }
-    const MaxRec Q = block_max(q, sm);  // (its barriers also publish s_pc / s_pt)
     if (Q.ties == 1 && Q.cnt) {  // the unique max: its block kept its key
         for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS)
             if (s_pc[b] == Q.cnt) s_key[0] = s_pk[b];
@@ -4084,7 +4105,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
             const uint32_t mid = (lo + hi) >> 1;
             if (s_to[mid] <= e) lo = mid; else hi = mid;
         }
-        const uint32_t key = ld_wt(N.cand + s_tb[lo] * NEXT_CAND + (e - s_to[lo]));
+        const uint32_t key = single ? s_key[e] : ld_wt(N.cand + s_tb[lo] * NEXT_CAND + (e - s_to[lo]));
         const uint64_t ent = ((uint64_t)(zig_pair_hash(key) & cap_mask) << 32) | key;
         if (total <= NEXT_TIE_LDS) s_tl[e] = ent;
         else N.tie_list[e] = ent;
