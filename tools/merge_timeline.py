@@ -56,14 +56,15 @@ def analyse(d, logp):
     if len(scans) < len(slog):
         sys.exit(f"{len(scans)} scans in the trace, {len(slog)} in the log")
     scans = scans[len(scans) - len(slog):]
-    buckets = [(0, 2000), (2000, 8000), (8000, 20000), (20000, 1 << 30)]
+    buckets = [(0, 100), (100, 500), (500, 2000), (2000, 8000), (8000, 20000), (20000, 1 << 30)]
     dens_acc = {}
     acc = {b: {} for b in buckets}
 
     def add(b, k, v):
-        a = acc[b].setdefault(k, [0.0, 0])
+        a = acc[b].setdefault(k, [0.0, 0, []])
         a[0] += v
         a[1] += 1
+        a[2].append(v)
 
     for j, x in enumerate(slog):
         if x < 0:
@@ -95,7 +96,8 @@ def analyse(d, logp):
     out = {}
     for b in buckets:
         out[f"merges [{b[0]}, {b[1] if b[1] < 1 << 30 else 'end'})"] = {
-            k: {"avg_us": round(v[0] / v[1], 2), "n": v[1]} for k, v in sorted(acc[b].items())}
+            k: {"avg_us": round(v[0] / v[1], 2), "p50_us": round(sorted(v[2])[len(v[2]) // 2], 2), "n": v[1]}
+            for k, v in sorted(acc[b].items())}
     # kernel time of the measured train by kernel (from its first pair scan to the end of the trace)
     t0 = ks[scans[0]][0]
     tot = {}

@@ -134,6 +134,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
         e.scan_batch = (int)value;
     }
     else if (k == "list_ranges") e.list_ranges = value != 0;
+    else if (k == "scan_plan") e.scan_plan = value != 0;
     else if (k == "range_min_len" && value >= 1 && value < (1ll << 32)) e.range_min_len = (uint32_t)value;
     else if (k == "range_max_rows" && value >= 0 && value <= 65536) e.range_max_rows = (uint32_t)value;
     else if (k == "range_max_len" && value >= 1 && value < (1ll << 32)) e.range_max_len = (uint32_t)value;

@@ -244,6 +244,7 @@ zbpe_status Engine::maybe_grow_tables(uint32_t X, uint32_t k) {
 }
 
 zbpe_status Engine::compact() {
+    layout_gen++;
     const int64_t ntiles = (n_slots + COMPACT_TILE - 1) / COMPACT_TILE;
     if (ntiles == 0) return ZBPE_OK;
     CHECK(ensure(&d_tile_cnt, tile_cnt_cap, ntiles, "compaction tiles"));
@@ -312,6 +313,7 @@ zbpe_status Engine::compact_train(uint32_t X) {
 // replicas. The pair table is already identical on every rank, so from here each rank computes
 // the same merges with no collective; the halo is empty and positions are global.
 zbpe_status Engine::replicate() {
+    layout_gen++;
     CHECK(ensure(&d_sizes, sizes_cap, 2 * (size_t)world + 2, "shard sizes"));
     const uint32_t mine = (uint32_t)n_live;
     HIP_OK(hipMemcpyAsync(d_sizes, &mine, 4, hipMemcpyHostToDevice, stream));
@@ -391,6 +393,7 @@ zbpe_status Engine::max_over_ranks(uint32_t v, uint32_t *out) {
 }
 
 zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio, bool ranges) {
+    layout_gen++;
     const int64_t n = n_slots;
     if (dist()) {  // (sharded, replicate_late off) the arena limit stays replicated: grown from the largest shard
         uint32_t nmax = 0;
@@ -711,7 +714,7 @@ zbpe_status Engine::resolve_tie(uint32_t top, uint32_t ties, uint32_t *winner) {
     return ZBPE_OK;
 }
 
-using ScanFn = void (*)(ScanArgs);
+using ScanFn = void (*)(const DevState *, ScanArgs);
 // 0 is the default: unroll 4, non-temporal loads, two-token-window candidate test, candidates
 // compacted per wave and resolved one per lane on the LDS-staged tile. The others for A/B runs
 // (tools/scan_density.py): 2 resolves per vector in its lane (slower at every density measured:
@@ -749,7 +752,7 @@ zbpe_status Engine::launch_scan(const ScanArgs &A, int grid, uint64_t count_hint
     const ScanFn f = A.prof && v == 0 ? zbpe_scan_pairs_t<4, true, true, true, true, true> : kScanVariants[v];
     ScanArgs B = A;
     B.batch = scan_batch;
-    hipLaunchKernelGGL(f, dim3(grid > 0 ? grid : scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, B);
+    hipLaunchKernelGGL(f, dim3(grid > 0 ? grid : scan_grid(A.n)), dim3(SCAN_THREADS), 0, stream, (const DevState *)B.st, B);
     LAUNCH_OK();
     return ZBPE_OK;
 }
@@ -1191,6 +1194,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                    pres_on ? d_pres : nullptr, pres_vp, X, T.tok_cnt, 1, dist() ? d_halo : nullptr,
                    lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log, nullptr, (int)sel_prof};
         set_list_nb(A);
+        A.gen = layout_gen;
         // a batch that follows one of list scans only launches a smaller grid (fewer idle workgroups
         // to dispatch); a stream scan still completes on it, only slower
         CHECK(launch_scan(A, list_streak ? list_grid : 0, top0));
@@ -1200,11 +1204,11 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
                       1, dist() ? d_halo : nullptr, 1, (int)sel_prof};
         if (!replace_split) {
-            zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
+            zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R, T);
         } else {  // profiling: apply and count update as two launches
-            zbpe_replace<<<ab, 256, 0, stream>>>(R, T, d_st);
+            zbpe_replace<<<ab, 256, 0, stream>>>(d_st, R, T);
             R.apply_blocks = 0;
-            zbpe_replace<<<update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
+            zbpe_replace<<<update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R, T);
         }
         LAUNCH_OK();
         if (dist()) {
@@ -1226,8 +1230,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
-                       dist() ? world : 1, (int)sel_prof, cs, d_rtk};
-            zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(T, d_st, d_partial, d_tok[cur], slots, left, X, N);
+                       dist() ? world : 1, (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
+                       scan_plan && lists_on ? 1 : 0};
+            zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(d_st, T, d_partial, d_tok[cur], slots, left, X, N);
             LAUNCH_OK();
         } else {
             CHECK(launch_argmax(X, 1));
@@ -1386,7 +1391,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top / 256 + 1);
         ReplaceArgs R{d_tok[cur], n_slots, d_lists, (uint32_t)lists_cap, left, right, tail, a, b, X, key, ab, halo,
                       (self && dist()) ? d_x0 : nullptr, 0, nullptr, 1};
-        zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(R, T, d_st);
+        zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R, T);
         LAUNCH_OK();
     }
     if (dist()) {  // boundary tokens of every shard for the next merge's halos

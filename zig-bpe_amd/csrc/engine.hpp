@@ -136,6 +136,8 @@ struct Engine {
     uint32_t dir_w = 0;
     bool dirs_built = false;
     uint32_t list_ranges = 1;            // option "list_ranges": successor-sorted long lists (0: off)
+    uint32_t scan_plan = 1;              // option "scan_plan": the select stores the next merge's list plan (0: off)
+    uint32_t layout_gen = 1;             // bumped by every list build / compaction / replication (a stored scan plan of another is stale)
     uint32_t range_min_len = 1u << 14;   // option "range_min_len": lists that get a directory row
     uint32_t range_max_rows = 4096;      // option "range_max_rows"
     uint32_t range_max_len = 0xFFFFFFFEu;  // option "range_max_len": longer lists keep the filtered walk

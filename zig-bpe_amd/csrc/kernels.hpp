@@ -13,7 +13,21 @@
 
 #include "types.hpp"
 
+#ifndef ZBPE_LP_CACHE
+#define ZBPE_LP_CACHE 1  // zbpe_select_next: the stream's last pair id cached in the state head (0: looked up every merge)
+#endif
 namespace zbpe {
+// DevState's hot header in one round trip: every word is loaded here at kernel entry, before any
+// branch on them (the empty asm makes each value live at this point, so the compiler issues the
+// scalar loads together and waits once instead of loading each word where it is first used)
+__device__ __attribute__((always_inline)) inline StateHead load_head(const DevState *st) {
+    StateHead h = *reinterpret_cast<const StateHead *>(st);
+    asm volatile("" ::"s"(h.halt), "s"(h.cur_key), "s"(h.arena_top), "s"(h.lists_valid), "s"(h.lists_x), "s"(h.top_count),
+                 "s"(h.theta), "s"(h.rec_count));
+    asm volatile("" ::"s"(h.plan_x), "s"(h.plan_key), "s"(h.plan_gen), "s"(h.plan_la), "s"(h.plan_lb), "s"(h.plan_oa),
+                 "s"(h.plan_ob), "s"(h.plan_r0), "s"(h.plan_r1), "s"(h.lp_key), "s"(h.lp_id));
+    return h;
+}
 // ------------------------------------------------------------------------------------------
 // Zig 0.13 std.hash.Wyhash(seed 0) of the 4-byte key
 // ------------------------------------------------------------------------------------------
@@ -428,6 +442,12 @@ struct ScanArgs {
     // lists_x for the stream's end) at [dir[row * dir_w + s], dir[row * dir_w + s + 1])
     const uint32_t *dir_row, *dir;
     uint32_t dir_w;
+    uint32_t gen;           // the host's layout generation (Engine::layout_gen): a scan plan of another one is stale
+    // filled by scan_args_resolve from the state head (host: 0): the top count, and the scan plan
+    // zbpe_select_next stored for this merge (plan_ok; pl = la, lb, oa, ob, r0, r1: DevState::plan_*)
+    uint32_t top_count;
+    uint32_t plan_ok;
+    uint32_t pl[6];
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // batching pays below about one occurrence per 400 slots and costs above it (tools/scan_bands.py:
@@ -435,11 +455,12 @@ constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 constexpr uint64_t SCAN_BATCH_DENSITY = 400;
 // the device-held parts of the arguments: pair (batch mode), halo (batch mode, multi-GPU), record
 // window in the arena
-__device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
+// (H: the state head, load_head at kernel entry)
+__device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0, const StateHead &H) {
     uint32_t a = A0.a, b = A0.b;
     Halo h = A0.halo;
     if (A0.dyn) {
-        const uint32_t k = A0.st->cur_key;
+        const uint32_t k = H.cur_key;
         a = k & 0xFFFF;
         b = k >> 16;
         if (A0.dhalo) h = *A0.dhalo;
@@ -447,14 +468,18 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0) {
     uint32_t *rec = A0.rec;
     uint32_t cap = A0.rec_cap;
     if (A0.rec_arena) {
-        const uint32_t top = A0.st->arena_top;
+        const uint32_t top = H.arena_top;
         rec += top;
         cap = cap > top ? cap - top : 0;
     }
-    return ScanArgs{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
-                    A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
-                    A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb, A0.batch,
-                    A0.dir_row, A0.dir, A0.dir_w};
+    ScanArgs A{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
+               A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
+               A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb, A0.batch,
+               A0.dir_row, A0.dir, A0.dir_w, A0.gen, H.top_count, 0u, {}};
+    // batch mode: the plan the select stored with this merge's pair, for the current lists
+    A.plan_ok = A0.dyn && H.plan_x == A0.X && H.plan_key == pair_key(a, b) && H.plan_gen == A0.gen ? 1u : 0u;
+    A.pl[0] = H.plan_la; A.pl[1] = H.plan_lb; A.pl[2] = H.plan_oa; A.pl[3] = H.plan_ob; A.pl[4] = H.plan_r0; A.pl[5] = H.plan_r1;
+    return A;
 }
 
 // Positions outside the shard address the halo: p >= n is right[p-n], p < 0 is left[-p-1].
@@ -836,20 +861,32 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
 // one pair scan with resolved arguments: the list form when the shorter token list is short
 // enough, else the stream form
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false, bool BATCH = false>
-__device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S) {
+__device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S, const StateHead &H) {
     // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
-    const uint32_t lists_x = A.st->lists_x;
-    if (A.lists && A.a != A.b && A.st->lists_valid) {
-        // lengths and offsets in one round trip
-        const uint32_t la = A.lst_len[A.a], lb = A.lst_len[A.b], oa = A.lst_off[A.a], ob = A.lst_off[A.b];
-        const uint32_t ra = A.dir_row ? A.dir_row[A.a] : NO_LIST;
+    const uint32_t lists_x = H.lists_x;
+    if (A.lists && A.a != A.b && H.lists_valid) {
+        // lengths, offsets and the successor range: from the select's plan (no load here), else two
+        // round trips
+        uint32_t la, lb, oa, ob, r0 = NO_LIST, r1 = NO_LIST;
+        bool ranged;
+        if (A.plan_ok) {
+            la = A.pl[0]; lb = A.pl[1]; oa = A.pl[2]; ob = A.pl[3]; r0 = A.pl[4]; r1 = A.pl[5];
+            ranged = A.dir_row && r0 != NO_LIST && A.a < lists_x && A.b < lists_x;
+        } else {
+            la = A.lst_len[A.a]; lb = A.lst_len[A.b]; oa = A.lst_off[A.a]; ob = A.lst_off[A.b];
+            const uint32_t ra = A.dir_row ? A.dir_row[A.a] : NO_LIST;
+            ranged = ra != NO_LIST && A.a < lists_x && A.b < lists_x;
+            if (ranged) {
+                const uint64_t rb = (uint64_t)ra * A.dir_w + A.b;
+                r0 = A.dir[rb];
+                r1 = A.dir[rb + 1];
+            }
+        }
         const bool by_b = lb < la;
         const uint32_t len = by_b ? lb : la;
         // a's list sorted by build-time successor (a long list): by the invariant below, every occurrence
         // is in the range of successor b -- about the pair's count of entries, wherever a's list is
-        if (ra != NO_LIST && A.a < lists_x && A.b < lists_x) {
-            const uint64_t rb = (uint64_t)ra * A.dir_w + A.b;
-            const uint32_t r0 = A.dir[rb], r1 = A.dir[rb + 1];
+        if (ranged) {
             if (blockIdx.x == 0 && threadIdx.x == 0) {
                 A.st->scan_mode = 1;
                 if (A.log) {
@@ -891,7 +928,9 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
 // PROF (option sel_prof): the pipeline probes; a separate instantiation, so the production kernel's
 // code and register allocation are untouched by them
 template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false, bool PROF = false, bool BATCH = false>
-__global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(4))) zbpe_scan_pairs_t(ScanArgs A0) {
+// stp == A0.st, as the leading pointer argument: a build with kernarg preloading (Makefile KP=1) has it in
+// SGPRs at entry, so the state head load needs no kernarg round trip first (aggregates are not preloaded)
+__global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(4))) zbpe_scan_pairs_t(const DevState *stp, ScanArgs A0) {
     if (PROF && blockIdx.x == 0 && threadIdx.x == 0) {  // the last select's end -> this scan's start
         DevState *st = A0.st;
         const unsigned long long now = wall_clock64();
@@ -899,10 +938,11 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
         if (st->pp_t[7]) { P[8] += now - st->pp_t[7]; P[9]++; st->pp_t[7] = 0; }
         st->pp_t[0] = now;
     }
-    if (A0.dyn && A0.st->halt) return;
+    const StateHead H = load_head(stp);
+    if (A0.dyn && H.halt) return;
     __shared__ ScanLds S;
-    const ScanArgs A = scan_args_resolve(A0);
-    scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF, BATCH>(A, S);
+    const ScanArgs A = scan_args_resolve(A0, H);
+    scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF, BATCH>(A, S, H);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -944,7 +984,10 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_encode_scan_batch(ScanArgs 
     A.rec_ctr = &ctr[j];
     A.rec_arena = 0;
     A.dyn = 0;
-    scan_dispatch<4, true, true, true, true>(A, S);
+    const StateHead H = load_head(A0.st);
+    A.top_count = H.top_count;
+    A.plan_ok = 0;
+    scan_dispatch<4, true, true, true, true>(A, S, H);
 }
 __global__ void __launch_bounds__(256) zbpe_encode_apply_batch(uint16_t *tok, int64_t n, EncBatch E, const uint32_t *__restrict__ scratch,
                                                                int32_t *cnt, uint32_t *ctr, uint32_t *arena, DevState *st, Tables T) {
@@ -1003,7 +1046,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
                                                                          ScanLds &S, uint32_t vb, uint32_t vg, bool all) {
     // entries per thread: about one match per two lanes (a wave resolves its matches 64 at a time, one
     // latency chain per round): the list's length over the pair's count (training; encode: 4)
-    const uint32_t cnt = A.count_deltas ? A.st->top_count : 0u;
+    const uint32_t cnt = A.count_deltas ? A.top_count : 0u;
     const uint32_t ratio = cnt ? len / cnt : 8u;
     const uint32_t ept = all ? (ratio >= 4 ? 4u : ratio >= 2 ? 2u : 1u)
                              : ratio >= 32 ? 16u : ratio >= 16 ? 8u : ratio >= 8 ? 4u : ratio >= 4 ? 2u : 1u;
@@ -1341,7 +1384,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
     uint32_t *cbuf = reinterpret_cast<uint32_t *>(s_tile[wib]);
     bool batch_on = false;
     if constexpr (BATCH) {
-        const uint64_t cnt = A.count_deltas ? A.st->top_count : 0u;
+        const uint64_t cnt = A.count_deltas ? A.top_count : 0u;
         batch_on = A.batch == 2 || (A.batch == 1 && (cnt == 0 || cnt * SCAN_BATCH_DENSITY < (uint64_t)A.n));
     }
     constexpr uint32_t CB_REC = 64 * UNROLL * 4 / 12;  // records the buffer holds
@@ -2280,11 +2323,12 @@ __device__ inline void update_preload(const uint32_t *left, const uint32_t *righ
         dv[k] = real && k < per && t < X ? delta[t] : 0u;
     }
 }
-__global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, DevState *st) {
+__global__ void __launch_bounds__(256) zbpe_replace(DevState *st, ReplaceArgs R, Tables T) {
     uint32_t dv[UPD_MAX_PER];
     const uint32_t per = update_per(R.X);
     if (blockIdx.x >= R.apply_blocks) update_preload(R.left, R.right, R.X, blockIdx.x - R.apply_blocks, per, dv);
-    const uint32_t theta = st->theta;
+    const StateHead H = load_head(st);  // (with the deltas: one round trip)
+    const uint32_t theta = H.theta;
     if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the list scan's stamps
         const unsigned long long now = wall_clock64();
         if (st->pp_t[4]) {
@@ -2300,18 +2344,18 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
         st->pp_t[5] = now;
     }
     if (R.dyn) {
-        if (st->halt) return;
-        R.top_key = st->cur_key;
+        if (H.halt) return;
+        R.top_key = H.cur_key;
         R.a = R.top_key & 0xFFFF;
         R.b = R.top_key >> 16;
     }
     if (blockIdx.x < R.apply_blocks) {
         if (R.rec_arena) {
-            const uint32_t top = st->arena_top;
+            const uint32_t top = H.arena_top;
             R.rec += top;
             R.rec_cap = R.rec_cap > top ? R.rec_cap - top : 0;
         }
-        const uint32_t cnt = min(st->rec_count, R.rec_cap);
+        const uint32_t cnt = min(H.rec_count, R.rec_cap);
         uint32_t made = 0;  // an occurrence whose b lies in the next shard makes no hole here
         for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += R.apply_blocks * 256) {
             const int64_t p = R.rec[i];
@@ -2350,7 +2394,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(ReplaceArgs R, Tables T, Dev
         return;
     }
     const uint32_t ublk = blockIdx.x - R.apply_blocks;
-    if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != st->top_count) atomicOr(&st->error, 64u);  // occurrences != count
+    if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) atomicOr(&st->error, 64u);  // occurrences != count
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof);
     if (R.prof) {
         __syncthreads();
@@ -2563,7 +2607,7 @@ __global__ void zbpe_self_x0(const uint32_t *__restrict__ fns, int rank, uint8_t
     *x0 = x;
 }
 __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, const uint8_t *__restrict__ carry_in) {
-    const ScanArgs A = scan_args_resolve(A0);
+    const ScanArgs A = scan_args_resolve(A0, load_head(A0.st));
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
     __shared__ uint32_t s_rec[SELF_TILE / 2];
     __shared__ uint8_t s_wave[SELF_THREADS / 64];
@@ -2645,7 +2689,7 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
 // trailing a of an odd run or the token after the run. Two walks: count, then (after one atomic per
 // wave for the records) emit. O(list length) instead of three passes over the stream.
 __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_self_list(ScanArgs A0) {
-    const ScanArgs A = scan_args_resolve(A0);
+    const ScanArgs A = scan_args_resolve(A0, load_head(A0.st));
     const uint32_t a = A.a, len = A.lst_len[a];
     if (len == NO_LIST || (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len)) return;
     const uint32_t *L = A.lists + A.lst_off[a];
@@ -3628,6 +3672,36 @@ __device__ inline void refresh_prefix(const HomeView &V, uint32_t *cs) {
 }
 constexpr int DECIDE_THREADS = 256;
 // two smallest of two (smallest, second smallest) pairs
+// Scan plan of the next merge (zbpe_select_next): what scan_dispatch would load first -- both tokens'
+// list lengths and offsets, and the successor range of (a, b) in a's sorted list -- loaded by one lane
+// of the select while its other waves work (the decision's carries), so the scan starts walking after
+// one state round trip instead of three. Token xn (made by the merge this launch rolled) has its
+// records as its list: offset xoff, length xlen (select_finish stores them in this launch).
+struct PlanCtx {
+    const uint32_t *lst_off, *lst_len, *dir_row, *dir;
+    uint32_t dir_w, lists_x, xn, xoff, xlen;
+};
+__device__ inline void plan_compute(const PlanCtx &P, uint32_t key, uint32_t *out) {
+    const uint32_t a = key & 0xFFFF, b = key >> 16;
+    uint32_t la = P.lst_len[a], lb = P.lst_len[b], oa = P.lst_off[a], ob = P.lst_off[b];
+    const uint32_t ra = P.dir_row && a < P.lists_x && b < P.lists_x && b + 1 < P.dir_w ? P.dir_row[a] : NO_LIST;
+    uint32_t r0 = NO_LIST, r1 = NO_LIST;
+    if (ra != NO_LIST) {
+        const uint64_t rb = (uint64_t)ra * P.dir_w + b;
+        r0 = P.dir[rb];
+        r1 = P.dir[rb + 1];
+    }
+    if (a == P.xn) { la = P.xlen; oa = P.xoff; }
+    if (b == P.xn) { lb = P.xlen; ob = P.xoff; }
+    out[0] = la; out[1] = lb; out[2] = oa; out[3] = ob; out[4] = r0; out[5] = r1;
+}
+// the plan of merge x1 = key (after the state's cur_key for it is stored; the next kernel boundary orders both)
+__device__ inline void plan_store(DevState *st, uint32_t x1, uint32_t key, uint32_t gen, const uint32_t *pl) {
+    st->plan_la = pl[0]; st->plan_lb = pl[1]; st->plan_oa = pl[2]; st->plan_ob = pl[3]; st->plan_r0 = pl[4]; st->plan_r1 = pl[5];
+    st->plan_gen = gen;
+    st->plan_key = key;
+    st->plan_x = x1;
+}
 __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uint64_t b2) {
     const uint64_t a1 = m1, a2 = m2;
     m1 = min(a1, b1);
@@ -3639,8 +3713,12 @@ __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uin
 template <int NT = DECIDE_THREADS>
 __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
-                                   const uint32_t *cs = nullptr) {
+                                   const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
+                                   uint32_t plan_gen = 0) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
+    // plan (NT >= 256): wave 3 finds the smallest home's key itself and loads its scan plan during the
+    // carries; the commit below stores it with cur_key
+    __shared__ uint32_t s_plan[6];
     // three waves at once, one barrier: wave 0 reduces the tied keys (the two smallest home << 32 |
     // key, the largest home) and finds the end of the smallest home's run; wave 1 the carry into
     // slot 0; wave 2 the last free slot of the map's last 4096 slots (where a run wrapping past
@@ -3680,6 +3758,13 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
         const int64_t lf = wave_last_free(V, ws, V.C, wave_carry_into(V, ws));
         if (lane == 0) s_last = lf;
     }
+    if (NT >= 256 && plan_on && w == 3 && len) {
+        uint64_t m1 = ~0ull;
+        for (uint32_t i = lane; i < len; i += 64) m1 = min(m1, list[i]);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) m1 = min(m1, (uint64_t)__shfl_xor(m1, off));
+        if (lane == 0) plan_compute(plan, (uint32_t)m1, s_plan);
+    }
     __syncthreads();
     if (!ws && !cs) {  // a map of at most 4096 slots: the last free slot needs the carry into slot 0
         if (w == 2) {
@@ -3712,6 +3797,7 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
         } else {
             st->cur_key = key;
             log[st->cur_x - 256] = MergeLog{key, st->top_count, (uint32_t)st->live_tokens, st->tie_count};
+            if (NT >= 256 && plan_on && len) plan_store(st, st->cur_x, key, plan_gen, s_plan);
         }
     }
 }
@@ -3763,6 +3849,11 @@ struct NextArgs {
     int prof;             // option sel_prof: accumulate phase times into st->sel_prof
     uint32_t *cs;         // [nsb + 1] refresh_prefix's carries (nullptr: the decision computes them; nsb > NEXT_THREADS)
     uint32_t *rtk;        // [RTK_WORDS] refresh arrival counters
+    // the next merge's scan plan (DevState::plan_*): the scan's successor directory (ScanArgs::dir_row,
+    // dir, dir_w; dir_row nullptr: no ranges) and the host's layout generation; plan 0: none
+    const uint32_t *dir_row, *dir;
+    uint32_t dir_w, gen;
+    int plan;
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -3806,7 +3897,7 @@ __device__ inline MaxRec block_max(MaxRec r, MaxRec *sm) {
     __syncthreads();
     return q;
 }
-__global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, DevState *st, MaxRec *__restrict__ partial,
+__global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st, Tables T, MaxRec *__restrict__ partial,
                                                                  const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
                                                                  uint32_t X, NextArgs N) {
     // blocks [0, nref) refresh the home super-blocks (the longest role: dispatched first, one
@@ -3851,7 +3942,18 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         }
         return;
     }
-    if (st->halt) return;
+    // Issued before the state head (they do not depend on it), so that head, hot entries and tail tokens
+    // take one round trip together: the first step of hot entries (bounded by the capacity, filtered by
+    // the list length once the head is in) and wave 1's last 64 stream slots (the stream's last pair)
+    const uint32_t bx = blockIdx.x - nref;  // argmax block index
+    const uint32_t G = N.sel_blocks * NEXT_THREADS, i00 = bx * NEXT_THREADS + tid;
+    unsigned long long e0[SEL_U];
+#pragma unroll
+    for (int u = 0; u < SEL_U; u++) e0[u] = i00 + u * G < T.hot_cap ? T.hot[i00 + u * G] : (unsigned long long)NO_ID;
+    const bool lp_wave = bx == 0 && tid >= 64 && tid < 128 && N.world == 1;
+    const uint32_t t_tail = lp_wave && n - 1 - (int64_t)(tid - 64) >= 0 ? tok[n - 1 - (int64_t)(tid - 64)] : HOLE;
+    const StateHead H0 = load_head(st);
+    if (H0.halt) return;
     __shared__ MaxRec sm[NEXT_THREADS / WAVE];
     __shared__ uint32_t s_flag, s_nc, s_h, s_tie, s_len, s_ntb, s_ovf;
     __shared__ uint32_t s_key[NEXT_CAND];
@@ -3874,25 +3976,40 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
             st->pp_t[5] = st->pp_t[6] = 0;
         }
     }
-    const uint32_t bx = blockIdx.x - nref;  // argmax block index
     // one argmax workgroup (a short hot list): it is the last one by construction -- no ticket, no
     // partials through global memory
     const bool single = N.sel_blocks == 1;
     __shared__ uint32_t s_lastpair;
     MaxRec R{0, 0, NO_ID};
     {
-        const uint32_t G = N.sel_blocks * NEXT_THREADS;
         if (!nref)  // (no refresh workgroups: the argmax ones clear the deltas)
             for (uint32_t t = bx * NEXT_THREADS + tid; t < 2 * X; t += G) delta[t] = 0;
-        const uint32_t nh = min(st->hot_len, T.hot_cap), theta = st->theta;
-        if (bx == 0 && tid >= 64 && tid < 128 && N.world == 1) {
-            // wave 1 of block 0: the count of the stream's last pair (a tie needs it: Zig map capacity)
+        const uint32_t nh = min(H0.hot_len, T.hot_cap), theta = H0.theta;
+        // SEL_U hot entries per thread per step, every load of a step issued together (the first step's
+        // entries were loaded at entry); their counts are gathered here, beside wave 1's cached last-pair
+        // words, so both wait together
+        MaxRec r{0, 0, NO_ID};
+        uint32_t ids[SEL_U], cs[SEL_U], ks[SEL_U];
+#pragma unroll
+        for (int u = 0; u < SEL_U; u++) {
+            const unsigned long long e = i00 + u * G < nh ? e0[u] : (unsigned long long)NO_ID;
+            ids[u] = (uint32_t)e;
+            ks[u] = (uint32_t)(e >> 32);  // the key rides along: the block's keys at its max come from registers
+        }
+#pragma unroll
+        for (int u = 0; u < SEL_U; u++) cs[u] = ids[u] != NO_ID ? T.id_cnt[ids[u]] : 0u;
+        if (lp_wave) {
+            // wave 1 of block 0: the count of the stream's last pair (a tie needs it: Zig map capacity).
+            // The pair id of the last lookup (state head) is checked and its count loaded with the hot
+            // counts (the tail tokens came with the head); a changed tail looks the key up.
             const uint32_t lane = tid - 64;
+            const uint32_t cid = H0.lp_id < T.id_cap ? H0.lp_id : 0u;
+            const uint32_t c_key = T.id_key[cid], c_cnt = T.id_cnt[cid], c_nid = st->num_ids;
             uint32_t lt[2] = {HOLE, HOLE};
             int got = 0;
             for (int64_t e = n; e > 0 && got < 2; e -= 64) {
                 const int64_t p = e - 1 - lane;
-                const uint32_t t = p >= 0 ? tok[p] : HOLE;
+                const uint32_t t = e == n ? t_tail : p >= 0 ? tok[p] : HOLE;
                 uint64_t live = __ballot(t != HOLE);
                 while (live && got < 2) {  // lowest lane = highest position
                     const int l = __builtin_ctzll(live);
@@ -3901,19 +4018,26 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
                 }
             }
             if (lane == 0) {
-                const uint32_t lp = got == 2 ? ht_find_count(T, pair_key(lt[1], lt[0])) : 0u;
+                uint32_t lp = 0;
+                if (got == 2) {
+                    const uint32_t key = pair_key(lt[1], lt[0]);
+                    if (ZBPE_LP_CACHE && key == H0.lp_key && c_key == key && H0.lp_id < c_nid && H0.lp_id < T.id_cap) {
+                        lp = c_cnt;
+                    } else {
+                        const uint32_t id = ht_find(T, key);
+                        lp = id == NO_ID ? 0u : T.id_cnt[id];
+                        if (id != NO_ID) { st->lp_key = key; st->lp_id = id; }
+                    }
+                }
                 __hip_atomic_store(N.lastpair, lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 s_lastpair = lp;
             }
         }
-        // SEL_U hot entries per thread per step, every load of a step issued together
-        MaxRec r{0, 0, NO_ID};
-        uint32_t ids[SEL_U], cs[SEL_U], ks[SEL_U];
 #pragma unroll
-        for (int u = 0; u < SEL_U; u++) { ids[u] = NO_ID; cs[u] = 0; ks[u] = 0; }
-        bool one_step = true;
-        for (uint32_t i0 = bx * NEXT_THREADS + tid; i0 < nh; i0 += SEL_U * G) {
-            one_step = i0 == bx * NEXT_THREADS + tid;
+        for (int u = 0; u < SEL_U; u++)
+            if (cs[u] >= theta && cs[u]) r = max_combine(r, MaxRec{cs[u], 1u, ids[u]});
+        const bool one_step = SEL_U * G >= nh;  // (every entry was in the first step)
+        for (uint32_t i0 = i00 + SEL_U * G; i0 < nh; i0 += SEL_U * G) {
 #pragma unroll
             for (int u = 0; u < SEL_U; u++) {
                 const unsigned long long e = i0 + u * G < nh ? T.hot[i0 + u * G] : (unsigned long long)NO_ID;
@@ -4005,7 +4129,20 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
         for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS)
             if (s_pc[b] == Q.cnt) s_key[0] = s_pk[b];
     }
+    // a tied top pair's key (select_finish defers it; only the host reads it, after a halt): loaded now
+    // straight into LDS by the last wave, which has nothing else to do (an LDS-DMA load makes its wave's
+    // next LDS read wait for it), and stored by it at the launch's end
+    constexpr uint32_t KEY_TID = NEXT_THREADS - 64;
+    __shared__ uint32_t s_qkey;
+    if (tid == KEY_TID && Q.cnt && Q.ties > 1)
+        __builtin_amdgcn_global_load_lds(&T.id_key[Q.id], (__attribute__((address_space(3))) void *)&s_qkey, 4, 0, 0);
     __syncthreads();
+    // the next merge's scan plan: its list loads (one lane of wave 1) overlap the roll and begin below;
+    // for an untied next merge the key is known now, a tied one's comes from the decision (decide_body)
+    __shared__ uint32_t s_plan[6];
+    const PlanCtx plan{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, X, H0.arena_top, H0.rec_count};  // (X's list: the roll's lst_off / lst_len, from the same words)
+    const bool plan_on = N.plan && T.lst_off && H0.lists_valid;
+    if (plan_on && tid == 64 && Q.ties == 1 && Q.cnt) plan_compute(plan, s_key[0], s_plan);
     if (N.prof && tid == 0) sel_tick(st, 1, &pt);
     if (tid == 0) {
         FinishOut fo;
@@ -4029,9 +4166,13 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
     if (N.prof && tid == 0) sel_tick(st, 2, &pt);
     // the tied top pair's key, deferred by select_finish (stored on every way out below)
     auto put_key = [&]() {
-        if (tid == 0 && Q.cnt && Q.ties > 1) st->top_key = T.id_key[Q.id];
+        if (tid == KEY_TID && Q.cnt && Q.ties > 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            st->top_key = s_qkey;
+        }
     };
     if (s_h || !s_tie) {
+        if (plan_on && tid == 64 && !s_h && Q.ties == 1 && Q.cnt) plan_store(st, N.B.X, s_key[0], N.gen, s_plan);
         if (N.prof && tid == 0) st->pp_t[7] = wall_clock64();
         put_key();
         return;
@@ -4144,7 +4285,8 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(Tables T, De
             atomicAdd(&st->sel_prof[11], __hip_atomic_load(&st->sel_prof_pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t0);
         }
     }
-    decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr);
+    decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
+                              plan_on, plan, N.gen);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }

@@ -1,6 +1,7 @@
 // Types and constants shared by the device code (kernels.hpp) and the host engine.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace zbpe {
@@ -23,11 +24,31 @@ __host__ __device__ constexpr inline uint32_t pair_key(uint32_t first, uint32_t 
 
 // Device-resident state. Host reads a copy after each merge (one small D2H per merge).
 struct DevState {
+    // ---- hot header (the first 96 B): the words the merge kernels read first, loaded together in one
+    // scalar round trip at kernel entry (StateHead; a chain of dependent state loads was several
+    // round trips of each late merge's launches)
+    uint32_t halt;           // HaltReason; every merge-loop kernel returns at once while set
+    uint32_t cur_key;        // the pair this merge replaces (after the tie-break)
+    uint32_t arena_top;      // arena entries in use (lists, then this merge's records)
+    uint32_t lists_valid;    // 1: token occurrence lists describe the current stream
+    uint32_t lists_x;        // tokens < lists_x existed when the lists were built (their entries carry neighbours)
+    uint32_t top_count;      // argmax result
+    uint32_t theta;          // hot-list threshold: every live id with count >= theta is in the hot list
+    uint32_t hot_len;        // ids appended to the hot list (may exceed its capacity -> rebuild); follows theta
+    uint32_t rec_count;      // occurrences recorded by the last scan
+    // scan plan of merge plan_x (pair plan_key), written by zbpe_select_next with cur_key: the list
+    // lengths / offsets of both tokens and the successor range of (a, b) in a's sorted list (NO_LIST:
+    // none), valid while the host's layout generation (lists, stream positions) is plan_gen
+    uint32_t plan_x, plan_key, plan_gen;
+    uint32_t plan_la, plan_lb, plan_oa, plan_ob, plan_r0, plan_r1;
+    // the stream's last pair (zbpe_select_next): its key and pair id when last looked up, so that the
+    // count is one load beside the tail tokens' (the key only changes when a merge reaches the tail)
+    uint32_t lp_key, lp_id;
+    uint32_t head_pad[4];
+    // ---- the rest
     uint32_t num_ids;        // pair ids allocated
     int32_t live;            // D_t: pairs with count > 0
-    uint32_t rec_count;      // occurrences recorded by the last scan
     uint32_t xx;             // adjacent occurrences: (b,a) -> (X,X)
-    uint32_t top_count;      // argmax result
     uint32_t tie_count;
     uint32_t top_id;
     uint32_t top_key;
@@ -40,8 +61,6 @@ struct DevState {
     uint32_t mismatches;
     uint32_t last_occ;       // occurrences merged by the last merge (copied by zbpe_reset_merge)
     uint32_t total_occ;      // running sum of last_occ (encode bookkeeping)
-    uint32_t theta;          // hot-list threshold: every live id with count >= theta is in the hot list
-    uint32_t hot_len;        // ids appended to the hot list (may exceed its capacity -> rebuild)
     uint32_t pad_dirty;
     uint32_t ticket;         // zbpe_select: blocks done (the last one reduces), reset by it
     uint32_t last_gocc;      // occurrences merged by the last merge on all ranks
@@ -53,18 +72,13 @@ struct DevState {
     unsigned long long scanned_slots;  // stream slots the scans actually streamed (block skipping)
     // device-resident merge loop (Engine::run_batch): the host enqueues a batch of merges whose
     // kernels read the pair from here; a merge the device cannot finish alone halts the batch
-    uint32_t halt;           // HaltReason; every merge-loop kernel returns at once while set
     uint32_t halt_at;        // merge token X of the halted merge
     uint32_t cur_x;          // merge token X being processed
-    uint32_t cur_key;        // the pair this merge replaces (after the tie-break)
     uint32_t tie_on;         // 1: this merge's top count is tied (the tie kernels run)
-    uint32_t lists_valid;    // 1: token occurrence lists describe the current stream
     long long live_tokens;   // live tokens of this shard (rolled by zbpe_select)
-    uint32_t arena_top;      // arena entries in use (lists, then this merge's records)
     uint32_t arena_rep;      // sum of the merges' global occurrence counts since the arena was emptied: the same on
                              // every rank and >= any rank's arena_top, so halts decided on it keep ranks in step
     uint32_t scan_mode;      // last pair scan: 0 streamed the token stream, 1 walked an occurrence list
-    uint32_t lists_x;        // tokens < lists_x existed when the lists were built (their entries carry neighbours)
     // option sel_prof: zbpe_select_next phase times (wall_clock64 ticks, summed over merges)
     unsigned long long sel_t0, sel_ta, sel_tr;  // start; latest argmax / refresh block finish
     unsigned long long sel_prof[12];  // [8] tie decisions, [9] their carries, [10] refresh wait, [6]/[11] prefix start/end
@@ -78,6 +92,17 @@ struct DevState {
     // last refresh workgroup skips the decision's carries (zeroed with the state at each train)
     uint32_t ref_noprefix;
 };
+// DevState's hot header as one value (StateHead load_head(st))
+struct StateHead {
+    uint32_t halt, cur_key, arena_top, lists_valid, lists_x, top_count, theta, hot_len, rec_count;
+    uint32_t plan_x, plan_key, plan_gen, plan_la, plan_lb, plan_oa, plan_ob, plan_r0, plan_r1;
+    uint32_t lp_key, lp_id;
+    uint32_t pad[4];
+};
+static_assert(sizeof(StateHead) == 96, "state head: 24 words");
+static_assert(offsetof(DevState, rec_count) == 32 && offsetof(DevState, plan_r1) == 68 && offsetof(DevState, hot_len) == 28 &&
+                  offsetof(DevState, lp_id) == 76,
+              "StateHead mirrors DevState's first words");
 // zbpe_select_next's refresh arrival counters (a device buffer): per launch parity X & 1, eight
 // per-XCD counters (workgroup i counts in i % 8) and a top counter, each on its own 128-B line. The
 // select of X - 1 zeroes parity X & 1; the host zeroes both before a batch that does not continue one.
