@@ -1204,11 +1204,11 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
                       1, dist() ? d_halo : nullptr, 1, (int)sel_prof};
         if (!replace_split) {
-            zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R, T);
+            zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
         } else {  // profiling: apply and count update as two launches
-            zbpe_replace<<<ab, 256, 0, stream>>>(d_st, R, T);
+            zbpe_replace<<<ab, 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
             R.apply_blocks = 0;
-            zbpe_replace<<<update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R, T);
+            zbpe_replace<<<update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
         }
         LAUNCH_OK();
         if (dist()) {
@@ -1232,7 +1232,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
                        dist() ? world : 1, (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
                        scan_plan && lists_on ? 1 : 0};
-            zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(d_st, T, d_partial, d_tok[cur], slots, left, X, N);
+            zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hot_cap, C ? nsb : 0u, sel,
+                                                                                 d_tok[cur], slots, T, d_partial, left, X, N);
             LAUNCH_OK();
         } else {
             CHECK(launch_argmax(X, 1));
@@ -1391,7 +1392,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top / 256 + 1);
         ReplaceArgs R{d_tok[cur], n_slots, d_lists, (uint32_t)lists_cap, left, right, tail, a, b, X, key, ab, halo,
                       (self && dist()) ? d_x0 : nullptr, 0, nullptr, 1};
-        zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R, T);
+        zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
         LAUNCH_OK();
     }
     if (dist()) {  // boundary tokens of every shard for the next merge's halos

@@ -938,7 +938,14 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
         if (st->pp_t[7]) { P[8] += now - st->pp_t[7]; P[9]++; st->pp_t[7] = 0; }
         st->pp_t[0] = now;
     }
-    const StateHead H = load_head(stp);
+    // the state head and the argument words a list walk needs, fetched together (one round trip, not a
+    // chain of kernarg cache misses in the order the code first uses them): one asm consumes them all
+    const StateHead H = *reinterpret_cast<const StateHead *>(stp);
+    asm volatile("" ::"s"(A0.dyn), "s"(A0.X), "s"(A0.gen), "s"(A0.rec_arena), "s"(A0.rec_cap), "s"(A0.count_deltas),
+                 "s"(A0.tok), "s"(A0.lists), "s"(A0.rec), "s"(A0.left), "s"(A0.right), "s"(A0.dir_row), "s"(A0.xx_out),
+                 "s"(A0.occ_out), "s"(A0.n), "s"(H.halt), "s"(H.cur_key), "s"(H.arena_top), "s"(H.lists_valid),
+                 "s"(H.lists_x), "s"(H.top_count), "s"(H.plan_x), "s"(H.plan_key), "s"(H.plan_gen), "s"(H.plan_la),
+                 "s"(H.plan_lb), "s"(H.plan_oa), "s"(H.plan_ob), "s"(H.plan_r0), "s"(H.plan_r1));
     if (A0.dyn && H.halt) return;
     __shared__ ScanLds S;
     const ScanArgs A = scan_args_resolve(A0, H);
@@ -2323,10 +2330,13 @@ __device__ inline void update_preload(const uint32_t *left, const uint32_t *righ
         dv[k] = real && k < per && t < X ? delta[t] : 0u;
     }
 }
-__global__ void __launch_bounds__(256) zbpe_replace(DevState *st, ReplaceArgs R, Tables T) {
+// The leading scalar arguments (kernarg-preloaded) are what the delta loads need (== R.left, R.X,
+// R.apply_blocks; right = left + X), so they issue at entry beside the state head.
+__global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t *__restrict__ left, uint32_t Xp, uint32_t apply_blocks,
+                                                    ReplaceArgs R, Tables T) {
     uint32_t dv[UPD_MAX_PER];
-    const uint32_t per = update_per(R.X);
-    if (blockIdx.x >= R.apply_blocks) update_preload(R.left, R.right, R.X, blockIdx.x - R.apply_blocks, per, dv);
+    const uint32_t per = update_per(Xp);
+    if (blockIdx.x >= apply_blocks) update_preload(left, left + Xp, Xp, blockIdx.x - apply_blocks, per, dv);
     const StateHead H = load_head(st);  // (with the deltas: one round trip)
     const uint32_t theta = H.theta;
     if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the list scan's stamps
@@ -2349,7 +2359,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, ReplaceArgs R,
         R.a = R.top_key & 0xFFFF;
         R.b = R.top_key >> 16;
     }
-    if (blockIdx.x < R.apply_blocks) {
+    if (blockIdx.x < apply_blocks) {
         if (R.rec_arena) {
             const uint32_t top = H.arena_top;
             R.rec += top;
@@ -2357,7 +2367,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, ReplaceArgs R,
         }
         const uint32_t cnt = min(H.rec_count, R.rec_cap);
         uint32_t made = 0;  // an occurrence whose b lies in the next shard makes no hole here
-        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += R.apply_blocks * 256) {
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += apply_blocks * 256) {
             const int64_t p = R.rec[i];
             R.tok[p] = (uint16_t)R.X;
             const int64_t q = next_live(R.tok, R.n, p);
@@ -2393,7 +2403,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, ReplaceArgs R,
         }
         return;
     }
-    const uint32_t ublk = blockIdx.x - R.apply_blocks;
+    const uint32_t ublk = blockIdx.x - apply_blocks;
     if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) atomicOr(&st->error, 64u);  // occurrences != count
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof);
     if (R.prof) {
@@ -3897,12 +3907,17 @@ __device__ inline MaxRec block_max(MaxRec r, MaxRec *sm) {
     __syncthreads();
     return q;
 }
-__global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st, Tables T, MaxRec *__restrict__ partial,
-                                                                 const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
-                                                                 uint32_t X, NextArgs N) {
+// The leading scalar arguments (kernarg-preloaded: in SGPRs at entry) are what the first loads need -- the
+// state, the hot list and its capacity, the role split (nref = the refresh workgroups), the argmax grid
+// and the stream's tail -- so those loads issue at entry, before any kernarg round trip.
+__global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st, const unsigned long long *__restrict__ hot,
+                                                                 uint32_t hot_cap, uint32_t nref_arg, uint32_t sel_blocks,
+                                                                 const uint16_t *__restrict__ tok, int64_t n, Tables T,
+                                                                 MaxRec *__restrict__ partial, uint32_t *delta, uint32_t X,
+                                                                 NextArgs N) {
     // blocks [0, nref) refresh the home super-blocks (the longest role: dispatched first, one
     // workgroup per CU at this kernel's VGPR count), blocks [nref, nref + sel_blocks) run the argmax
-    const uint32_t nref = N.V.C ? N.V.nsb : 0u;
+    const uint32_t nref = nref_arg;  // == N.V.C ? N.V.nsb : 0
     const uint32_t tid = threadIdx.x;
     if (blockIdx.x < nref) {
         // refresh role, off the argmax's ticket: the last argmax block reduces, rolls and starts
@@ -3946,10 +3961,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     // take one round trip together: the first step of hot entries (bounded by the capacity, filtered by
     // the list length once the head is in) and wave 1's last 64 stream slots (the stream's last pair)
     const uint32_t bx = blockIdx.x - nref;  // argmax block index
-    const uint32_t G = N.sel_blocks * NEXT_THREADS, i00 = bx * NEXT_THREADS + tid;
+    const uint32_t G = sel_blocks * NEXT_THREADS, i00 = bx * NEXT_THREADS + tid;
     unsigned long long e0[SEL_U];
 #pragma unroll
-    for (int u = 0; u < SEL_U; u++) e0[u] = i00 + u * G < T.hot_cap ? T.hot[i00 + u * G] : (unsigned long long)NO_ID;
+    for (int u = 0; u < SEL_U; u++) e0[u] = i00 + u * G < hot_cap ? hot[i00 + u * G] : (unsigned long long)NO_ID;
     const bool lp_wave = bx == 0 && tid >= 64 && tid < 128 && N.world == 1;
     const uint32_t t_tail = lp_wave && n - 1 - (int64_t)(tid - 64) >= 0 ? tok[n - 1 - (int64_t)(tid - 64)] : HOLE;
     const StateHead H0 = load_head(st);
@@ -3978,7 +3993,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     // one argmax workgroup (a short hot list): it is the last one by construction -- no ticket, no
     // partials through global memory
-    const bool single = N.sel_blocks == 1;
+    const bool single = sel_blocks == 1;
     __shared__ uint32_t s_lastpair;
     MaxRec R{0, 0, NO_ID};
     {
@@ -4086,7 +4101,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     if (N.prof && tid == 0) atomicMax(&st->sel_ta, (unsigned long long)wall_clock64());
-    if (!single && !block_ticket_last(&st->ticket, N.sel_blocks, &s_flag)) return;
+    if (!single && !block_ticket_last(&st->ticket, sel_blocks, &s_flag)) return;
     const bool pfx = nref && N.cs && N.B.log[X - 256].ties > 1;  // the refresh precomputes the carries (its predicate)
     // the next launch's refresh count (the launch before this one used it and has ended)
     if (tid < 9) st_wt(N.rtk + ((X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
@@ -4116,7 +4131,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         __syncthreads();
     } else {
         MaxRec q{0, 0, NO_ID};
-        for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
+        for (uint32_t b = tid; b < sel_blocks; b += NEXT_THREADS) {
             const MaxRec p{ld_wt(&partial[b].cnt), ld_wt(&partial[b].ties), ld_wt(&partial[b].id)};
             s_pc[b] = p.cnt;
             s_pt[b] = p.ties;
@@ -4126,7 +4141,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         Q = block_max(q, sm);  // (its barriers also publish s_pc / s_pt)
     }
     if (Q.ties == 1 && Q.cnt) {  // the unique max: its block kept its key
-        for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS)
+        for (uint32_t b = tid; b < sel_blocks; b += NEXT_THREADS)
             if (s_pc[b] == Q.cnt) s_key[0] = s_pk[b];
     }
     // a tied top pair's key (select_finish defers it; only the host reads it, after a halt): loaded now
@@ -4179,7 +4194,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     // ---- merge X+1 ties: gather the keys of the blocks whose max is the top count ----------------
     const uint32_t top = Q.cnt, total = Q.ties;
-    for (uint32_t b = tid; b < N.sel_blocks; b += NEXT_THREADS) {
+    for (uint32_t b = tid; b < sel_blocks; b += NEXT_THREADS) {
         if (s_pc[b] == top) {
             if (s_pt[b] > NEXT_CAND) atomicOr(&s_ovf, 1u);
             atomicAdd(&s_len, s_pt[b]);
@@ -4225,9 +4240,9 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     __shared__ uint32_t s_tb[NEXT_MAX_SEL], s_to[NEXT_MAX_SEL + 1];
     if (tid < 64) {
         uint32_t k = 0, o = 0;
-        for (uint32_t b0 = 0; b0 < N.sel_blocks; b0 += 64) {
+        for (uint32_t b0 = 0; b0 < sel_blocks; b0 += 64) {
             const uint32_t b = b0 + tid;
-            const bool t = b < N.sel_blocks && s_pc[b] == top;
+            const bool t = b < sel_blocks && s_pc[b] == top;
             const uint32_t c = t ? s_pt[b] : 0u;
             const uint64_t m = __ballot(t);
             const uint32_t below = (uint32_t)__popcll(m & ((1ull << tid) - 1ull));
