@@ -1106,32 +1106,44 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
                 }
             }
         }
-        const uint32_t c = (uint32_t)__popc(mk);
-        const uint32_t incl = wave_incl_scan(c);
-        const uint32_t M = (uint32_t)__shfl((int)incl, 63);
+        // a successor range: the wave's matches are the in-range entries of its chunk, contiguous, so
+        // match j is entry lo + j (no scan, no shuffle search)
+        uint32_t c = 0, incl = 0, M, lo = 0;
+        if (all) {
+            const uint32_t cs = ab + b0 + (threadIdx.x & ~63u) * ept;
+            const uint32_t hi = min(cs + 64u * ept, off + len);
+            lo = max(cs, off);
+            M = hi > lo ? hi - lo : 0u;
+        } else {
+            c = (uint32_t)__popc(mk);
+            incl = wave_incl_scan(c);
+            M = (uint32_t)__shfl((int)incl, 63);
+        }
         for (uint32_t r0 = 0; r0 < M; r0 += 64) {
             const uint32_t j = r0 + lane;
             int64_t p = -1;
             int owner = 0;  // the lane holding match j: the first whose inclusive count exceeds j
-            {
-                int lo = 0, hi = 63;
+            if (all) {
+                if (j < M) p = (int64_t)A.lists[lo + j];
+            } else {
+                int lo2 = 0, hi = 63;
                 const uint32_t jj = j < M ? j : 0u;
 #pragma unroll
                 for (int s2 = 0; s2 < 6; s2++) {
-                    const int mid = (lo + hi) >> 1;
+                    const int mid = (lo2 + hi) >> 1;
                     const uint32_t v = (uint32_t)__shfl((int)incl, mid);
                     if (v > jj) hi = mid;
-                    else lo = mid + 1;
+                    else lo2 = mid + 1;
                 }
-                owner = lo;
-            }
-            const uint32_t o_incl = (uint32_t)__shfl((int)incl, owner), o_c = (uint32_t)__shfl((int)c, owner);
-            const uint32_t o_mk = (uint32_t)__shfl((int)mk, owner);
-            if (j < M) {
-                uint32_t rank = j - (o_incl - o_c), m = o_mk;  // the rank-th set bit of the owner's mask
-                for (uint32_t q = 0; q < rank; q++) m &= m - 1;
-                const uint32_t e = ab + b0 + ((threadIdx.x & ~63u) + (uint32_t)owner) * ept + (uint32_t)__ffs(m) - 1;
-                p = (int64_t)A.lists[e];
+                owner = lo2;
+                const uint32_t o_incl = (uint32_t)__shfl((int)incl, owner), o_c = (uint32_t)__shfl((int)c, owner);
+                const uint32_t o_mk = (uint32_t)__shfl((int)mk, owner);
+                if (j < M) {
+                    uint32_t rank = j - (o_incl - o_c), m = o_mk;  // the rank-th set bit of the owner's mask
+                    for (uint32_t q = 0; q < rank; q++) m &= m - 1;
+                    const uint32_t e = ab + b0 + ((threadIdx.x & ~63u) + (uint32_t)owner) * ept + (uint32_t)__ffs(m) - 1;
+                    p = (int64_t)A.lists[e];
+                }
             }
             // the entry's stream window in one round trip (vector, the word before, the two after)
             const int64_t vi = p < 0 ? 0 : (p >> 3);
