@@ -188,6 +188,68 @@ def fnv64(tokens) -> int:
     return int(lib().zref_fnv64(_p(tt), ctypes.c_size_t(len(t))))
 
 
+_FAST = os.path.join(_HERE, "libzfast.so")
+_fast = None
+
+
+def fast_lib() -> ctypes.CDLL:
+    """oracle/zig_fast.cpp: the second restatement (incremental counts + a literal Zig-map replay at
+    every tied merge), fast enough for C4 in full."""
+    global _fast
+    if _fast is None:
+        src = os.path.join(_HERE, "zig_fast.cpp")
+        if not os.path.exists(_FAST) or os.path.getmtime(_FAST) < os.path.getmtime(src):
+            subprocess.run(["make", "-s", "-C", _HERE, "libzfast.so"], check=True)
+        L = ctypes.CDLL(_FAST)
+        L.zfast_train.restype = ctypes.c_int
+        L.zfast_pair_hash.restype = ctypes.c_uint64
+        L.zfast_pair_hash.argtypes = [ctypes.c_uint32]
+        L.zfast_final_capacity.restype = ctypes.c_uint32
+        L.zfast_final_capacity.argtypes = [ctypes.c_uint64, ctypes.c_int]
+        _fast = L
+    return _fast
+
+
+@dataclass
+class FastResult:
+    merges: np.ndarray      # (M, 3) uint16
+    counts: np.ndarray      # (M,) uint64
+    ties: np.ndarray        # (M,) uint32
+    distinct: np.ndarray    # (M,) uint32
+    len_after: np.ndarray   # (M,) uint64 stream length after each merge
+    tokens: np.ndarray      # final stream
+    restarts: int           # runs restarted because a replay overruled a predicted winner
+    ties_sync: int          # tied merges replayed before the merge
+    ties_async: int         # tied merges replayed by the worker threads (and confirmed)
+
+
+def fast_train(text: bytes, vocab_size: int, threads: int = 4, sync_limit: int = 1 << 20, fnv_every: int = 0,
+               progress: Optional[str] = None) -> FastResult:
+    L = fast_lib()
+    cap = max(vocab_size - 256, 1)
+    n = len(text)
+    tri = np.zeros(3 * cap, np.uint16)
+    cnt = np.zeros(cap, np.uint64)
+    ties = np.zeros(cap, np.uint32)
+    dist = np.zeros(cap, np.uint32)
+    lens = np.zeros(cap, np.uint64)
+    fin = np.zeros(max(n, 1), np.uint16)
+    info = np.zeros(4, np.uint64)
+    nm, nf = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    buf = np.frombuffer(text, np.uint8) if n else np.zeros(1, np.uint8)
+    rc = L.zfast_train(_p(buf), ctypes.c_size_t(n), ctypes.c_uint32(vocab_size), ctypes.c_int(threads),
+                       ctypes.c_uint64(sync_limit), ctypes.c_uint32(fnv_every),
+                       progress.encode() if progress else None, _p(tri), _p(cnt), _p(ties), _p(dist), _p(lens),
+                       ctypes.byref(nm), _p(fin), ctypes.byref(nf), _p(info))
+    if rc == 1:
+        raise ValueError("InvalidVocabSize")
+    if rc != 0:
+        raise MemoryError(f"zfast_train rc {rc}")
+    m = nm.value
+    return FastResult(tri[: 3 * m].reshape(m, 3).copy(), cnt[:m].copy(), ties[:m].copy(), dist[:m].copy(),
+                      lens[:m].copy(), fin[: nf.value].copy(), int(info[0]), int(info[1]), int(info[2]))
+
+
 def wyhash(seed: int, data: bytes) -> int:
     return int(lib().zref_wyhash(ctypes.c_uint64(seed), data, ctypes.c_size_t(len(data))))
 

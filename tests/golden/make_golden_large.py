@@ -61,6 +61,20 @@ def run(name: str, log: str, max_merges: int = 0) -> None:
     print(name, "rc", rc, "merges", nm.value, "final tokens", nt.value, "seconds", round(st.total_s, 1), flush=True)
 
 
+def run_fast(name: str, log: str, threads: int = 7) -> None:
+    """The second oracle (oracle/zig_fast.cpp: incremental counts, a literal Zig-map replay at every
+    tied merge) over the whole run; C4 in a few hours on 8 cores."""
+    import oracle as O
+    import zbpe
+    kind, seed, n, vocab, _ = RUNS[name]
+    text = zbpe.synth_corpus(kind, seed, n, threads=8)
+    print(name, "corpus sha256", hashlib.sha256(text).hexdigest(), flush=True)
+    os.makedirs(os.path.dirname(os.path.abspath(log)), exist_ok=True)
+    r = O.fast_train(text, vocab, threads=threads, fnv_every=FNV_EVERY, progress=os.path.abspath(log))
+    print(name, "merges", len(r.merges), "final tokens", len(r.tokens), "restarts", r.restarts,
+          "ties replayed before the merge", r.ties_sync, "ties replayed by workers", r.ties_async, flush=True)
+
+
 def convert(name: str, log: str) -> str:
     kind, seed, n, vocab, fname = RUNS[name]
     merges, counts, ties, distinct, lens, fnv, done = [], [], [], [], [], [], None
@@ -106,6 +120,8 @@ if __name__ == "__main__":
     cmd, name, log = sys.argv[1], sys.argv[2], sys.argv[3]
     if cmd == "run":
         run(name, log, int(sys.argv[4]) if len(sys.argv) > 4 else 0)
+    elif cmd == "run-fast":
+        run_fast(name, log, int(sys.argv[4]) if len(sys.argv) > 4 else 7)
     elif cmd == "convert":
         convert(name, log)
     else:

@@ -214,7 +214,7 @@ int main() {
     // grid barrier: all blocks resident (grid <= CUs)
     unsigned *cnt, *gen, *err;
     CK(hipMalloc(&cnt, 4)); CK(hipMalloc(&gen, 4)); CK(hipMalloc(&err, 4));
-    for (int grid : {8, 64, 256}) {
+    for (int grid : {8, 32, 64, 128, 256, 512, 1024}) {
         CK(hipMemset(cnt, 0, 4)); CK(hipMemset(gen, 0, 4)); CK(hipMemset(err, 0, 4));
         const int iters = 2000;
         barrier_k<<<grid, 256, 0, s>>>(cnt, gen, 10, err);
