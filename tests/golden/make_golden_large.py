@@ -14,6 +14,12 @@ keeps its prefix; `convert` turns a (possibly partial) log into the committed JS
   python tests/golden/make_golden_large.py run c4 /tmp/zbpe_golden/c4.log [max_merges]
   python tests/golden/make_golden_large.py convert c3 /tmp/zbpe_golden/c3.log
 
+The second oracle (oracle/zig_fast.cpp) runs C4 to the end in a few hours on 8 cores and gives the full golden
+(large_c4_words_utf8_1GiB_v32000.json, every tie confirmed by a literal map replay):
+
+  python tests/golden/make_golden_large.py run-fast c4 /tmp/zbpe_golden/c4fast.log [threads]
+  python tests/golden/make_golden_large.py convert-fast c4 /tmp/zbpe_golden/c4fast.log
+
 The JSON holds, per merge k: the triple, the top count, the number of pairs tied at it, the distinct
 pairs D_k and the stream length after the merge, plus FNV-1a-64 checksums of the stream every
 `FNV_EVERY` merges (tests/test_gpu_large.py compares the device's run with all of it).
@@ -116,6 +122,71 @@ def convert(name: str, log: str) -> str:
     return path
 
 
+def convert_fast(name: str, log: str) -> str:
+    """The fast oracle's progress log -> the full-sequence golden (large_<...>.json without `_prefix`). A run
+    that restarted (a replay overruled a predicted tie winner) logs `restart`; only the last attempt counts.
+    `complete` needs the final `done` line and a confirming replay for every tied merge."""
+    kind, seed, n, vocab, fname = RUNS[name]
+    # C4: the full golden beside the literal oracle's prefix; other runs keep the literal oracle's file
+    fname = fname.replace("_prefix", "") if "_prefix" in fname else fname.replace(".json", "_fast.json")
+    merges, counts, ties, distinct, lens, fnv, done = [], [], [], [], [], {}, None
+    ok, bad, restarts, sync, timing = set(), 0, 0, 0, None
+    with open(log) as f:
+        for line in f:
+            p = line.split()
+            if not p:
+                continue
+            if p[0] == "restart":
+                restarts += 1
+                merges, counts, ties, distinct, lens, fnv, ok, bad, sync = [], [], [], [], [], {}, set(), 0, 0
+            elif p[0] == "fnv":
+                fnv[int(p[1])] = [int(p[1]), int(p[2]), p[3]]
+            elif p[0] == "done":
+                done = [int(p[1]), int(p[2]), p[3]]
+            elif p[0] == "tie":
+                if p[2] == "ok":
+                    ok.add(int(p[1]))
+                    sync += p[-1] == "sync"
+                else:
+                    bad += 1
+            elif p[0] == "timing":
+                timing = {p[i]: float(p[i + 1]) for i in range(1, len(p) - 1, 2)}
+            elif len(p) == 8 and p[0].isdigit():
+                k = int(p[0])
+                assert k == len(merges), (k, len(merges))
+                merges.append([int(p[1]), int(p[2]), int(p[3])])
+                counts.append(int(p[4]))
+                ties.append(int(p[5]))
+                distinct.append(int(p[6]))
+                lens.append(int(p[7]))
+    tied = [k for k, t in enumerate(ties) if t > 1]
+    confirmed = all(k in ok for k in tied)
+    import zbpe
+    corpus_sha = hashlib.sha256(zbpe.synth_corpus(kind, seed, n, threads=8)).hexdigest()
+    complete = done is not None and done[0] == vocab - 256 == len(merges) and confirmed and bad == 0
+    if done is not None and done[0] == len(merges):
+        fnv[done[0]] = done
+    out = {
+        "source": "oracle/zig_fast.cpp zfast_train (incremental restatement of basic_tokenizer.zig:140-306: exact "
+                  "incremental counts, a literal Zig 0.13 HashMapUnmanaged replay in first-occurrence order at every "
+                  "tied merge), tests/golden/make_golden_large.py run-fast / convert-fast",
+        "kind": kind, "seed": seed, "n": n, "vocab_size": vocab, "corpus_sha256": corpus_sha,
+        "complete": complete, "n_merges": len(merges),
+        "merges": merges, "counts": counts, "ties": ties, "distinct": distinct, "len_after": lens,
+        "fnv64_after": [fnv[k] for k in sorted(fnv)],
+        "tie_replays": {"replayed": len(ok & set(tied)), "before_the_merge": sync, "mismatches": bad,
+                        "restarts": restarts},
+        "oracle_timing_s": timing,
+    }
+    path = os.path.join(HERE, fname)
+    with open(path, "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+        f.write("\n")
+    print(path, len(merges), "merges", len(tied), "tied", len(ok), "replays confirmed", bad, "mismatches",
+          "complete" if complete else "INCOMPLETE")
+    return path
+
+
 if __name__ == "__main__":
     cmd, name, log = sys.argv[1], sys.argv[2], sys.argv[3]
     if cmd == "run":
@@ -124,5 +195,7 @@ if __name__ == "__main__":
         run_fast(name, log, int(sys.argv[4]) if len(sys.argv) > 4 else 7)
     elif cmd == "convert":
         convert(name, log)
+    elif cmd == "convert-fast":
+        convert_fast(name, log)
     else:
         raise SystemExit(f"unknown command {cmd}")

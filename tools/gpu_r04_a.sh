@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 120 ./tools/launch_lat > gpurun_out/launch_lat.jsonl 2>&1 || exit 1
+timeout -k 10 300 python tools/hist_bench.py --at 0 --at 20000 > gpurun_out/hist_dense.jsonl 2>&1 || exit 2
+timeout -k 10 300 python tools/hist_bench.py --at 0 --opt dense_hist=0 > gpurun_out/hist_hash.jsonl 2>&1 || exit 3
+timeout -k 10 900 python -u -m pytest tests/test_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_quick.log 2>&1 || exit 4

@@ -17,13 +17,17 @@ def main():
     p.add_argument("--n-bytes", type=int, default=1 << 30)
     p.add_argument("--at", type=int, action="append", default=[])
     p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--opt", action="append", default=[], help="engine option k=v (e.g. dense_hist=0)")
     a = p.parse_args()
     e = zbpe.Engine(0)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        e.set_option(k, int(v))
     e.upload(zbpe.synth_corpus("words_utf8", 0x5EED0004, a.n_bytes, threads=16))
     for k in a.at or [0, 20000]:
         _, _, st = e.train_resident(256 + k)
         r = e.bench_recount(a.reps)
-        r.update(merges=k, distinct_pairs=int(st.distinct_pairs), frac=r["GBps"] / 8000.0)
+        r.update(merges=k, distinct_pairs=int(st.distinct_pairs), frac=r["GBps"] / 8000.0, opts=a.opt)
         print(json.dumps(r), flush=True)
     e.close()
 

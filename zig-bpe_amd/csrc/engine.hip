@@ -120,7 +120,9 @@ zbpe_status Engine::init(int dev) {
     // the initial byte-pair histogram keeps 128 KiB of bins in LDS
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_count_byte_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4));
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_pres_build, hipFuncAttributeMaxDynamicSharedMemorySize, PRES_MAX_VP * 4));
-    HIP_OK(hipFuncSetAttribute((const void *)zbpe_pair_hist, hipFuncAttributeMaxDynamicSharedMemorySize, PH_SLOTS * 8));
+    HIP_OK(hipFuncSetAttribute((const void *)zbpe_pair_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, PH_SLOTS * 8));
+    HIP_OK(hipFuncSetAttribute((const void *)zbpe_pair_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               PH_DENSE * 4 + PH_SLOTS / 2 * 8));
     CHECK(set_scan_variant(0));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dev));
@@ -193,7 +195,7 @@ zbpe_status Engine::sync_state() {
     if (h_st->error & 512u)
         return fail(ZBPE_INVALID_ARGUMENT, "a byte pair occurs 2^32 times or more in the corpus: pair counts are u32 on the device");
     if (h_st->error)
-        return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow, 16 home count range, 32 dirty list overflow, 64 occurrences != count, 128 tie collection)",
+        return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow, 16 home count range, 32 dirty list overflow, 64 occurrences != count, 128 tie collection, 1024 select wait timed out)",
                     h_st->error);
     return ZBPE_OK;
 }
@@ -425,8 +427,10 @@ zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio, bool ranges) {
         CHECK(ensure(&d_row_tok, row_tok_cap, 2 * (size_t)range_max_rows + 4, "list directory tokens"));
         CHECK(ensure(&d_dir, dir_cap, (size_t)range_max_rows * dir_w, "list directory"));
         CHECK(ensure(&d_dir_tmp, dir_tmp_cap, (size_t)n + 64, "list sort copy"));
-        // chunks: at most one partial chunk per row beyond the entries' whole chunks
-        const uint64_t max_chunks = (uint64_t)n / SORT_CHUNK + range_max_rows + 1;
+        // chunks: at most one partial chunk per row beyond the entries' whole chunks; a row is a list of
+        // >= range_min_len entries, so there are at most n / range_min_len of them
+        const uint64_t rows_bound = std::min<uint64_t>(range_max_rows, (uint64_t)n / std::max<uint32_t>(range_min_len, 1) + 1);
+        const uint64_t max_chunks = (uint64_t)n / SORT_CHUNK + rows_bound + 1;
         CHECK(ensure(&d_sort_hist, sort_hist_cap, (size_t)max_chunks * (lists_x + 1), "list sort chunk histograms"));
         uint32_t *row_ch0 = d_row_tok + range_max_rows, *rows = row_ch0 + range_max_rows + 1;
         zbpe_dir_rows<<<1, 1024, 0, stream>>>(T.lst_len, lists_x, range_min_len, range_max_len, range_max_rows, d_dir_row, d_row_tok,
@@ -747,7 +751,9 @@ zbpe_status Engine::set_scan_variant(int v) {
 static constexpr int kScanBatchVariant = 7;
 zbpe_status Engine::launch_scan(const ScanArgs &A, int grid, uint64_t count_hint) {
     int v = scan_variant;
-    if (v == 0 && scan_batch == 1 && !A.prof && count_hint && count_hint * SCAN_BATCH_DENSITY < (uint64_t)A.n) v = kScanBatchVariant;
+    if (v == 0 && !A.prof &&
+        (scan_batch == 2 || (scan_batch == 1 && count_hint && count_hint * SCAN_BATCH_DENSITY < (uint64_t)A.n)))
+        v = kScanBatchVariant;
     // option sel_prof: the probed instantiation of the default variant
     const ScanFn f = A.prof && v == 0 ? zbpe_scan_pairs_t<4, true, true, true, true, true> : kScanVariants[v];
     ScanArgs B = A;
@@ -807,7 +813,7 @@ zbpe_status Engine::bench_train_scan(int reps, int grid, double *avg_us, uint32_
         LAUNCH_OK();
         HIP_OK(hipMemsetAsync(tail, 0, 8, stream));
         HIP_OK(hipEventRecord(ev[0], stream));
-        CHECK(launch_scan(A, grid));
+        CHECK(launch_scan(A, grid, h_st->top_count));  // the variant training picks for this pair
         HIP_OK(hipEventRecord(ev[1], stream));
         HIP_OK(hipEventSynchronize(ev[1]));
         float ms;
@@ -1088,13 +1094,15 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         const unsigned long long *P = h_st->sel_prof;
         const double calls = std::max(1.0, (double)P[7]), us = 0.01;
         fprintf(stderr, "sel_prof: %llu last-block calls; avg us: argmax+ticket %.2f, reduce %.2f, finish+begin %.2f, "
-                        "tie gather %.2f, decide %.2f; argmax blocks done %.2f, refresh blocks done %.2f\n",
+                        "tie gather %.2f, decide %.2f; argmax blocks done %.2f\n",
                 P[7], P[0] * us / calls, P[1] * us / calls, P[2] * us / calls, P[3] * us / calls, P[4] * us / calls,
-                P[5] * us / calls, P[6] * us / calls);
-        const double nd = std::max(1.0, (double)P[8]);
+                P[5] * us / calls);
+        const double nd = std::max(1.0, (double)P[8]), nr = std::max(1.0, (double)P[13]), np = std::max(1.0, (double)P[14]);
         fprintf(stderr, "sel_prof: %llu tie decisions; avg us per decision: gather %.2f, refresh wait %.2f, carries %.2f, "
-                        "decision total %.2f; refresh prefix start %.2f, end %.2f (from the first argmax block's start)\n", P[8],
-                P[3] * us / nd, P[10] * us / nd, P[9] * us / nd, P[4] * us / nd, P[6] * us / nd, P[11] * us / nd);
+                        "decision total %.2f; latest refresh block done %.2f (%llu samples); refresh prefix start %.2f, end %.2f "
+                        "(%llu samples; all from the first argmax block's start)\n", P[8],
+                P[3] * us / nd, P[10] * us / nd, P[9] * us / nd, P[4] * us / nd, P[12] * us / nr, P[13], P[6] * us / np,
+                P[11] * us / np, P[14]);
         static const char *bucket[3] = {"merges < 7936", "merges 7936-19743", "merges >= 19744"};
         for (int k = 0; k < 3; k++) {
             const unsigned long long *Q = h_st->pipe_prof[k];
@@ -1459,9 +1467,6 @@ zbpe_status Engine::verify_counts(uint64_t *mismatches) {
     return recount_check(mismatches, nullptr);
 }
 
-// Diagnostic download of the live token stream (holes squeezed out) into the spare stream buffer,
-// leaving the current buffer, its holes and the occurrence lists as they are. out == nullptr or a
-// short cap: only *n_tokens.
 // the live tokens of the current stream, holes squeezed out, into the spare stream buffer (the current
 // buffer, its holes and the occurrence lists stay as they are); *total: their number
 zbpe_status Engine::compact_to_spare(uint64_t *total) {
@@ -1551,8 +1556,13 @@ zbpe_status Engine::recount_check(uint64_t *mismatches, uint32_t *first_bad_key)
 // the full pair histogram (zbpe_pair_hist) of the compacted stream in the spare buffer into d_recount
 zbpe_status Engine::launch_pair_hist(uint64_t total) {
     const int32_t next_tok = dist() && halo.nright > 0 ? (int32_t)halo_right(halo, 0) : -1;  // the pair leaving the shard
-    zbpe_pair_hist<<<std::max(1, num_cus), PH_THREADS, PH_SLOTS * 8, stream>>>(d_tok[cur ^ 1], (int64_t)total, next_tok, T,
-                                                                                d_recount, d_st);
+    // a stream of bytes (no merge yet on this context): the dense form for its ASCII pairs
+    if (run.merges == 0 && dense_hist)
+        zbpe_pair_hist<true><<<std::max(1, num_cus), PH_THREADS, PH_DENSE * 4 + PH_SLOTS / 2 * 8, stream>>>(
+            d_tok[cur ^ 1], (int64_t)total, next_tok, T, d_recount, d_st);
+    else
+        zbpe_pair_hist<false><<<std::max(1, num_cus), PH_THREADS, PH_SLOTS * 8, stream>>>(d_tok[cur ^ 1], (int64_t)total, next_tok,
+                                                                                        T, d_recount, d_st);
     LAUNCH_OK();
     return ZBPE_OK;
 }

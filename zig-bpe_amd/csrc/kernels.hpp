@@ -817,7 +817,8 @@ __device__ inline void lrec_stage(const ScanArgs &A, ScanLds &S, bool hit, uint3
     }
 }
 // after the walk (a barrier since the last lrec_stage): one arena reservation for the staged records,
-// then the copy. Every thread calls it; ends with a barrier.
+// then the copy. Every thread calls it. It does NOT end with a barrier: a caller that reuses S.lrec or
+// S.lrec_base afterwards must barrier first (today the next walk's setup does).
 __device__ inline void lrec_flush(const ScanArgs &A, ScanLds &S) {
     const uint32_t n = min(S.lrec_n, LREC_CAP);
     if (threadIdx.x == 0 && n) {
@@ -3856,6 +3857,7 @@ constexpr int NEXT_CAND = 64;          // keys kept per argmax block at the bloc
 constexpr int NEXT_MAX_SEL = 1024;     // argmax blocks (the reducer keeps one LDS entry per block)
 constexpr int SEL_U = 8;               // hot entries per argmax thread per step (loads issued together)
 constexpr int NEXT_TIE_LDS = 512;      // tied keys the decision reads from LDS (more: from N.tie_list)
+constexpr unsigned long long SPIN_LIMIT_TICKS = 2000000ull;  // 20 ms of wall_clock64 (100 MHz): bounded spin-waits
 struct NextArgs {
     BeginArgs B;          // merge X + 1 (B.X < x_end)
     uint32_t x_end;       // vocab size: no merge starts at x_end
@@ -4290,9 +4292,18 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // dispatching a grid's workgroups in id order: the refresh workgroups (ids [0, nref)) were
         // dispatched before this argmax workgroup, so none of them waits for a slot this one holds.
         // pfx: the top counter reaches the groups + the prefix's arrival; else the XCD counters sum to nref
+        // Bounded: a wait past SPIN_LIMIT_TICKS (a broken dispatch-order assumption) sets error bit 1024
+        // (sync_state fails the train) and the decision goes on with whatever summaries it reads.
         const uint32_t *rtk = N.rtk + (X & 1) * RTK_SET;
+        const unsigned long long t_spin = wall_clock64();
         if (pfx) {
-            while (ld_wt(rtk + 8 * RTK_STRIDE) < min(nref, 8u) + 1u) __builtin_amdgcn_s_sleep(1);
+            while (ld_wt(rtk + 8 * RTK_STRIDE) < min(nref, 8u) + 1u) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t_spin > SPIN_LIMIT_TICKS) {
+                    if (tid == 0) atomicOr(&st->error, 1024u);
+                    break;
+                }
+            }
         } else {
             for (;;) {
                 uint32_t c = tid < 8 ? ld_wt(rtk + tid * RTK_STRIDE) : 0u;
@@ -4300,16 +4311,28 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 for (int off = 4; off >= 1; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off);
                 if ((uint32_t)__shfl((int)c, 0) >= nref) break;
                 __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t_spin > SPIN_LIMIT_TICKS) {
+                    if (tid == 0) atomicOr(&st->error, 1024u);
+                    break;
+                }
             }
         }
     }
     __syncthreads();
     if (N.prof && tid == 0) {
         sel_tick(st, 10, &pt);
-        if (N.cs) {  // the last refresh workgroup's prefix: start, end (from this launch's t0)
-            const unsigned long long t0 = st->sel_t0;
-            atomicAdd(&st->sel_prof[6], __hip_atomic_load(&st->sel_prof_pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t0);
-            atomicAdd(&st->sel_prof[11], __hip_atomic_load(&st->sel_prof_pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t0);
+        const unsigned long long t0 = st->sel_t0;
+        // every refresh workgroup has arrived: the latest one's finish (from this launch's t0)
+        const unsigned long long tr = __hip_atomic_load(&st->sel_tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tr >= t0) { atomicAdd(&st->sel_prof[12], tr - t0); atomicAdd(&st->sel_prof[13], 1ull); }
+        if (N.cs && pfx) {  // the last refresh workgroup's prefix of this launch: start, end (from t0)
+            const unsigned long long pq = __hip_atomic_load(&st->sel_prof_pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long pp = __hip_atomic_load(&st->sel_prof_pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (pq >= t0 && pp >= pq) {  // (stamps of an earlier launch are older than t0)
+                atomicAdd(&st->sel_prof[6], pq - t0);
+                atomicAdd(&st->sel_prof[11], pp - t0);
+                atomicAdd(&st->sel_prof[14], 1ull);
+            }
         }
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
@@ -4399,14 +4422,23 @@ constexpr uint32_t PH_SLOTS = 16384;
 constexpr int PH_PROBES = 8;
 constexpr int PH_U = 4;  // 16-B vectors per lane in flight
 constexpr uint32_t PH_EMPTY = 0xFFFFFFFFu;  // (65535, 65535): two holes, never a pair
+// Dense form (a stream of bytes, t = 0): the pairs of two ASCII tokens (both < 128; ~95 % of C4's byte
+// pairs) are counted in PH_DENSE direct u32 bins (64 KiB of LDS, index a << 7 | b: no key, no probe,
+// one non-returning LDS add), the others in an LDS hash of PH_SLOTS / 2 keys. A 16-B vector whose eight
+// tokens and successor are all ASCII takes eight adds and nothing else: the hashed form spends ~30 VALU
+// instructions per pair on the key, its home, the 2-slot read and the compares, which bounded it
+// (2.2 TB/s at C4 t = 0), not the LDS atomics.
+constexpr uint32_t PH_DENSE = 128 * 128;
 // home pair of slots of a key: the even slot its hash picks and the next one (one 8-B LDS read; a
 // 4-slot group by 16-B reads was measured slower: 1.10 vs 0.92 ms at C4 t = 0)
-__device__ inline uint32_t ph_home(uint32_t key) { return ((key * 0x9E3779B1u) >> (32 - 14)) & ~1u; }
+template <uint32_t SLOTS>
+__device__ inline uint32_t ph_home(uint32_t key) { return ((key * 0x9E3779B1u) >> (32 - __builtin_ctz(SLOTS))) & ~1u; }
 // a key missing from its home pair: linear probing from the home pair (insert at the first empty slot),
 // else the global table's id and a global atomic
+template <uint32_t SLOTS>
 __device__ inline void ph_count(uint32_t *s_key, uint32_t *s_cnt, const Tables &T, uint32_t *recount, DevState *st,
                                 uint32_t key) {
-    uint32_t h = ph_home(key);
+    uint32_t h = ph_home<SLOTS>(key);
 #pragma unroll 1
     for (int q = 0; q < PH_PROBES; q++) {
         const uint32_t k = __hip_atomic_load(&s_key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4415,17 +4447,21 @@ __device__ inline void ph_count(uint32_t *s_key, uint32_t *s_cnt, const Tables &
             const uint32_t old = atomicCAS(&s_key[h], PH_EMPTY, key);
             if (old == PH_EMPTY || old == key) { atomicAdd(&s_cnt[h], 1u); return; }
         }
-        h = (h + 1) & (PH_SLOTS - 1);
+        h = (h + 1) & (SLOTS - 1);
     }
     const uint32_t id = ht_find(T, key);
     if (id == NO_ID) { atomicAdd(&st->mismatches, 1u); return; }
     atomicAdd(&recount[id], 1u);
 }
+template <bool DENSE>
 __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__restrict__ tok, int64_t n, int32_t next_tok,
                                                               Tables T, uint32_t *__restrict__ recount, DevState *st) {
+    constexpr uint32_t SLOTS = DENSE ? PH_SLOTS / 2 : PH_SLOTS;
     extern __shared__ __attribute__((aligned(16))) uint32_t ph_lds[];
-    uint32_t *s_key = ph_lds, *s_cnt = ph_lds + PH_SLOTS;
-    for (uint32_t i = threadIdx.x; i < PH_SLOTS; i += PH_THREADS) { s_key[i] = PH_EMPTY; s_cnt[i] = 0; }
+    uint32_t *s_dense = ph_lds, *s_key = ph_lds + (DENSE ? PH_DENSE : 0), *s_cnt = s_key + SLOTS;
+    for (uint32_t i = threadIdx.x; i < SLOTS; i += PH_THREADS) { s_key[i] = PH_EMPTY; s_cnt[i] = 0; }
+    if (DENSE)
+        for (uint32_t i = threadIdx.x; i < PH_DENSE; i += PH_THREADS) s_dense[i] = 0;
     __syncthreads();
     const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
     const int64_t nvec = (n + 7) / 8;
@@ -4454,8 +4490,16 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
             const int64_t p8 = vi * 8 + 8;
             if (p8 >= n) nx = p8 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY;
             if (vi >= nvec) continue;
+            if (DENSE && p8 < n && (((v[u].x | v[u].y | v[u].z | v[u].w) & 0xFF80FF80u) | (nx & 0xFFFFFF80u)) == 0) {
+                // eight ASCII pairs: direct bins (the common vector; no key, no probe)
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t a = tok_at(v[u], k), b = k < 7 ? tok_at(v[u], k + 1) : nx;
+                    atomicAdd(&s_dense[(a << 7) | b], 1u);
+                }
+                continue;
+            }
             // the 8 pairs' first probes are issued together (one LDS round trip for the common hit), then
-            // hits take a non-returning LDS add and misses walk the probe chain
             // hits take a non-returning LDS add; the misses of the vector's 8 pairs are taken together
             // after them (one divergent slow path per vector, not one per pair: at 64 lanes some lane
             // nearly always misses)
@@ -4466,7 +4510,11 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
                 const int64_t p = vi * 8 + k;
                 const uint32_t b = k < 7 ? (p + 1 < n ? tok_at(v[u], k + 1) : (p + 1 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY)) : nx;
                 key[k] = p < n && b != PH_EMPTY ? pair_key(tok_at(v[u], k), b) : PH_EMPTY;
-                h[k] = ph_home(key[k]);
+                if (DENSE && key[k] != PH_EMPTY && (key[k] & 0xFF80FF80u) == 0) {  // an ASCII pair of a mixed vector
+                    atomicAdd(&s_dense[((key[k] & 0x7Fu) << 7) | (key[k] >> 16)], 1u);
+                    key[k] = PH_EMPTY;
+                }
+                h[k] = ph_home<SLOTS>(key[k]);
             }
             // (a plain LDS read: a slot's key only ever goes from empty to its final value, and a stale
             // empty read just sends the pair to the probing path, which re-reads with atomics)
@@ -4487,12 +4535,20 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
 #pragma unroll
                 for (int j = 1; j < 8; j++)
                     if (k == j) kk = key[j];
-                ph_count(s_key, s_cnt, T, recount, st, kk);
+                ph_count<SLOTS>(s_key, s_cnt, T, recount, st, kk);
             }
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < PH_SLOTS; i += PH_THREADS) {
+    if (DENSE)
+        for (uint32_t i = threadIdx.x; i < PH_DENSE; i += PH_THREADS) {
+            const uint32_t c = s_dense[i];
+            if (!c) continue;
+            const uint32_t id = ht_find(T, pair_key(i >> 7, i & 127u));
+            if (id == NO_ID) { atomicAdd(&st->mismatches, c); continue; }
+            atomicAdd(&recount[id], c);
+        }
+    for (uint32_t i = threadIdx.x; i < SLOTS; i += PH_THREADS) {
         const uint32_t k = s_key[i];
         if (k == PH_EMPTY) continue;
         const uint32_t id = ht_find(T, k);

@@ -81,7 +81,9 @@ struct DevState {
     uint32_t scan_mode;      // last pair scan: 0 streamed the token stream, 1 walked an occurrence list
     // option sel_prof: zbpe_select_next phase times (wall_clock64 ticks, summed over merges)
     unsigned long long sel_t0, sel_ta, sel_tr;  // start; latest argmax / refresh block finish
-    unsigned long long sel_prof[12];  // [8] tie decisions, [9] their carries, [10] refresh wait, [6]/[11] prefix start/end
+    // [0..4] last-block phases, [5] argmax blocks done, [7] last-block calls, [8] tie decisions, [9] their carries,
+    // [10] refresh wait, [12] latest refresh block done (at decisions, [13] samples), [6]/[11] prefix start/end ([14] samples)
+    unsigned long long sel_prof[16];
     unsigned long long sel_prof_pq, sel_prof_pp;  // refresh_prefix start / end stamps of the current launch
     // option sel_prof, whole merge pipeline (batch mode): probe stamps of the current launches and the
     // sums they fold into (Engine::train prints them): scan (list form) LDS clear / walk / flush done and
