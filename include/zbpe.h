@@ -147,7 +147,8 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * first-occurrence emulation and cross-check the GPU cluster test), "exact_ties_from" / "exact_ties_to"
  * (the same for merge indices k in [from, to) only; the other merges stay device-resident), "compact_den" (compact when
  * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..7: unroll, load kind, phase-2 form;
- * see engine.hip kScanVariants), "scan_batch" (stream form, variants with cross-tile candidate batching:
+ * see engine.hip kScanVariants), "dense_hist" (0/1: the full pair histogram of a byte stream counts ASCII pairs in direct LDS bins),
+ * "scan_batch" (stream form, variants with cross-tile candidate batching:
  * 0 off, 1 for sparse pairs, 2 always), "hot_target" (ids kept by the argmax hot list),
  * "block_skip" (0/1: stream only the 8192-slot blocks that hold the pair's rarer token),
  * "trace" (0/1: record per-merge timings, see zbpe_trace), "merge_batch" (merges enqueued per host
@@ -214,6 +215,11 @@ zbpe_status zbpe_merge_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_
  * that returned at once (its batch had halted before it). Lets a rocprofv3 per-dispatch trace (PMC
  * counters) be matched to merges. Copies up to `cap` entries; *n = entries recorded. */
 zbpe_status zbpe_scan_log(zbpe_ctx *ctx, int32_t *out, size_t cap, size_t *n);
+
+/* Diagnostic: one row {merge token X, arena_rep} per stream compaction of the last train (X: the merge it
+ * preceded; arena_rep: the replicated occurrence-arena fill it was decided on). Sharded ranks must agree
+ * on every row (compactions are decided on replicated quantities). Copies up to cap_rows rows of 2 u32. */
+zbpe_status zbpe_compaction_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_t *n_rows);
 
 /* Host-only diagnostic (no device work): the Zig 0.13 pair-map iteration order emulation used by
  * the exact tie fallback. Given every live pair's first-occurrence position, key (first |

@@ -52,8 +52,9 @@ def train_worker(rank, world, port, q, case):
         for k, v in case.get("options", {}).items():
             e.set_option(k, v)
         e.upload(text)
+        del text
         m, c, st = e.train_resident(case["vocab"])
-        q.put((rank, m.tolist(), c.tolist(), st.as_dict()))
+        q.put((rank, m.tolist(), c.tolist(), st.as_dict(), e.compaction_log().tolist()))
         e.close()
         dist.barrier()
         dist.destroy_process_group()

@@ -155,3 +155,33 @@ def test_sharded_corpus_over_4GiB(tmp_path):
     t = np.concatenate([np.load(tmp_path / "tok0.npy"), np.load(tmp_path / "tok1.npy")])  # after merge 1
     r1 = O.step(t)
     assert (r1.pair, r1.count) == ((m[1][0], m[1][1]), c[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(1100)
+def test_sharded_c4_world2_vs_golden():
+    """C4 itself (1 GiB, vocab 32000) sharded over 2 ranks that share the GPU (host collectives): every merge and
+    count equals the C4 golden (the fast oracle's full run when committed, else the literal oracle's prefix);
+    the run crosses the replication hand-over (sharded merges, then one gather, then replicas), and both ranks
+    compact at the same merges on the same replicated arena fill."""
+    import json
+    import os
+
+    from helpers import GOLDEN
+
+    full = os.path.join(GOLDEN, "large_c4_words_utf8_1GiB_v32000.json")
+    path = full if os.path.exists(full) else os.path.join(GOLDEN, "large_c4_words_utf8_1GiB_v32000_prefix.json")
+    with open(path) as f:
+        g = json.load(f)
+    case = dict(kind="words_utf8", seed=0x5EED0004, n=1 << 30, vocab=32000)
+    out = run(train_worker, 2, case, timeout=1000)
+    K = g["n_merges"]
+    for r in (0, 1):
+        _, m, c, st, clog = out[r]
+        assert len(m) == 32000 - 256
+        assert m[:K] == g["merges"] and c[:K] == g["counts"], f"rank {r}"
+        assert st["replications"] == 1 and 0 < st["sharded_merges"] < len(m), f"rank {r}"
+    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
+    assert out[0][3]["sharded_merges"] == out[1][3]["sharded_merges"]
+    assert out[0][4] == out[1][4] and len(out[0][4]) >= 2  # compactions: same merges, same replicated arena fill
+    assert out[0][3]["final_tokens"] == g["len_after"][-1] if g["complete"] else True

@@ -245,6 +245,15 @@ zbpe_status zbpe_scan_log(zbpe_ctx *ctx, int32_t *out, size_t cap, size_t *n) {
     return ZBPE_OK;
 }
 
+zbpe_status zbpe_compaction_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_t *n_rows) {
+    if (!ctx || !n_rows || (!rows && cap_rows)) return ZBPE_INVALID_ARGUMENT;
+    const auto &l = ctx->eng.compact_log;
+    *n_rows = l.size() / 2;
+    const size_t k = std::min(cap_rows, *n_rows);
+    if (k) memcpy(rows, l.data(), k * 2 * sizeof(uint32_t));
+    return ZBPE_OK;
+}
+
 zbpe_status zbpe_zig_order_winner(const uint32_t *first_pos, const uint32_t *keys, const uint32_t *counts, size_t n,
                                   uint32_t top, int call_after_last_insert, uint32_t *winner) {
     if ((!first_pos || !keys || !counts) && n) return ZBPE_INVALID_ARGUMENT;

@@ -289,6 +289,8 @@ bool Engine::holes_over() const {
 }
 
 zbpe_status Engine::compact_train(uint32_t X) {
+    compact_log.push_back(X);  // (h_st: the state as of the last sync; every caller synced since its last merge)
+    compact_log.push_back(h_st->arena_rep);
     HIP_OK(hipEventRecord(ev[3], stream));
     CHECK(compact());
     // sharded: on replicated quantities (every rank compacts here, at the same merge)
@@ -1016,6 +1018,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     run.verbose = verbose;
     run.vocab = vocab_size;
     trace.clear();
+    compact_log.clear();
     scan_log.clear();
     std::fill(h_log.begin(), h_log.end(), MergeLog{});
     uint32_t X = 256;

@@ -154,6 +154,7 @@ struct Engine {
     bool trace_on = false;
     std::vector<float> trace;
     std::vector<int32_t> scan_log;  // per pair-scan launch of the last train (zbpe_scan_log)
+    std::vector<uint32_t> compact_log;  // per training compaction: merge X, arena_rep (zbpe_compaction_log)
     // encode: merges applied per launch pair (option "encode_batch"; 1 = one merge at a time)
     uint32_t enc_batch = 32;
     uint64_t enc_batches = 0;       // launch pairs of the last encode
