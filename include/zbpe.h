@@ -147,7 +147,7 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * first-occurrence emulation and cross-check the GPU cluster test), "exact_ties_from" / "exact_ties_to"
  * (the same for merge indices k in [from, to) only; the other merges stay device-resident), "compact_den" (compact when
  * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..7: unroll, load kind, phase-2 form;
- * see engine.hip kScanVariants), "dense_hist" (0/1: the full pair histogram of a byte stream counts ASCII pairs in direct LDS bins),
+ * see engine.hip kScanVariants), "dense_hist" (0/1: the full pair histogram of a byte stream counts every byte pair in a fixed 16-bit LDS bin),
  * "scan_batch" (stream form, variants with cross-tile candidate batching:
  * 0 off, 1 for sparse pairs, 2 always), "hot_target" (ids kept by the argmax hot list),
  * "block_skip" (0/1: stream only the 8192-slot blocks that hold the pair's rarer token),

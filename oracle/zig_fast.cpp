@@ -449,6 +449,8 @@ struct Trainer {
     std::vector<uint8_t> pdirty;
     std::vector<uint32_t> dirty;
     std::vector<uint64_t> heap;   /* (count << 32 | id), max-heap, lazily invalidated */
+    /* analysis hook (tools/batch_potential.cpp): called with the winner before each merge is applied */
+    void (*pre_apply)(Trainer &, uint32_t k, uint32_t win_id, uint32_t T, const std::vector<uint32_t> &tied) = nullptr;
 
     ~Trainer() {
         if (arena) munmap(arena, arena_cap * sizeof(uint32_t));
@@ -792,6 +794,7 @@ struct Trainer {
             out_counts[k] = T;
             out_ties[k] = (uint32_t)tied.size();
             out_distinct[k] = (uint32_t)D;
+            if (pre_apply) pre_apply(*this, k, win_id, T, tied);
             double a0 = now();
             apply(win_id, (uint16_t)cur, k);
             t_apply += now() - a0;

@@ -459,3 +459,31 @@ def test_list_ranges_on_c2_bit_exact():
         m, c, st = e.train(synth_text(gg), gg["vocab_size"])
         assert m.tolist() == gg["merges"] and c.tolist() == gg["counts"]
         e.close()
+
+
+@pytest.mark.parametrize("kind", ["abac", "c4_slice", "utf8", "sharded_tail"])
+def test_pair_hist_bytes_exact(kind):
+    """The full pair histogram of a byte stream (zbpe_pair_hist_bytes: every byte pair in a fixed 16-bit LDS
+    bin, overflow accounted from the adds' return values) equals the incremental table at t = 0 (verify_counts
+    after training zero merges) and the hashed form's result. 'abac' repeated puts ~100 K adds of (a,b) and
+    (a,c) -- the two halves of ONE word -- into every workgroup: both halves wrap, and the low half's carry
+    is taken back while the high half is being added to."""
+    if kind == "abac":
+        text = b"abac" * (24 << 20)
+    elif kind == "c4_slice":
+        text = zbpe.synth_corpus("words_utf8", 0x5EED0004, 96 << 20, threads=16)
+    elif kind == "utf8":
+        text = bytes(range(256)) * 4096 + zbpe.synth_corpus("uniform", 5, 1 << 20)
+    else:
+        text = b"ab" * 1000 + b"x"  # an odd length: the last vector's tail pairs
+    e = zbpe.Engine(0)
+    try:
+        e.upload(text)
+        for dense in (1, 0):
+            e.set_option("dense_hist", dense)
+            e.train_resident(256)
+            assert e.verify_counts() == 0, dense
+            r = e.bench_recount(1)
+            assert r["mismatches"] == 0 and r["tokens"] == len(text)
+    finally:
+        e.close()

@@ -120,9 +120,8 @@ zbpe_status Engine::init(int dev) {
     // the initial byte-pair histogram keeps 128 KiB of bins in LDS
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_count_byte_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4));
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_pres_build, hipFuncAttributeMaxDynamicSharedMemorySize, PRES_MAX_VP * 4));
-    HIP_OK(hipFuncSetAttribute((const void *)zbpe_pair_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, PH_SLOTS * 8));
-    HIP_OK(hipFuncSetAttribute((const void *)zbpe_pair_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               PH_DENSE * 4 + PH_SLOTS / 2 * 8));
+    HIP_OK(hipFuncSetAttribute((const void *)zbpe_pair_hist, hipFuncAttributeMaxDynamicSharedMemorySize, PH_SLOTS * 8));
+    HIP_OK(hipFuncSetAttribute((const void *)zbpe_pair_hist_bytes, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4));
     CHECK(set_scan_variant(0));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dev));
@@ -1559,13 +1558,13 @@ zbpe_status Engine::recount_check(uint64_t *mismatches, uint32_t *first_bad_key)
 // the full pair histogram (zbpe_pair_hist) of the compacted stream in the spare buffer into d_recount
 zbpe_status Engine::launch_pair_hist(uint64_t total) {
     const int32_t next_tok = dist() && halo.nright > 0 ? (int32_t)halo_right(halo, 0) : -1;  // the pair leaving the shard
-    // a stream of bytes (no merge yet on this context): the dense form for its ASCII pairs
-    if (run.merges == 0 && dense_hist)
-        zbpe_pair_hist<true><<<std::max(1, num_cus), PH_THREADS, PH_DENSE * 4 + PH_SLOTS / 2 * 8, stream>>>(
-            d_tok[cur ^ 1], (int64_t)total, next_tok, T, d_recount, d_st);
+    // a stream of bytes (no merge yet on this context): every byte pair in a fixed 16-bit LDS bin
+    if (run.merges == 0 && dense_hist && (next_tok < 256))  // (next_tok: a byte or -1)
+        zbpe_pair_hist_bytes<<<std::max(1, num_cus), PH_THREADS, 32768 * 4, stream>>>(d_tok[cur ^ 1], (int64_t)total, next_tok, T,
+                                                                                       d_recount, d_st);
     else
-        zbpe_pair_hist<false><<<std::max(1, num_cus), PH_THREADS, PH_SLOTS * 8, stream>>>(d_tok[cur ^ 1], (int64_t)total, next_tok,
-                                                                                        T, d_recount, d_st);
+        zbpe_pair_hist<<<std::max(1, num_cus), PH_THREADS, PH_SLOTS * 8, stream>>>(d_tok[cur ^ 1], (int64_t)total, next_tok, T,
+                                                                                    d_recount, d_st);
     LAUNCH_OK();
     return ZBPE_OK;
 }

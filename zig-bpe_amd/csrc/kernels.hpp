@@ -4422,23 +4422,14 @@ constexpr uint32_t PH_SLOTS = 16384;
 constexpr int PH_PROBES = 8;
 constexpr int PH_U = 4;  // 16-B vectors per lane in flight
 constexpr uint32_t PH_EMPTY = 0xFFFFFFFFu;  // (65535, 65535): two holes, never a pair
-// Dense form (a stream of bytes, t = 0): the pairs of two ASCII tokens (both < 128; ~95 % of C4's byte
-// pairs) are counted in PH_DENSE direct u32 bins (64 KiB of LDS, index a << 7 | b: no key, no probe,
-// one non-returning LDS add), the others in an LDS hash of PH_SLOTS / 2 keys. A 16-B vector whose eight
-// tokens and successor are all ASCII takes eight adds and nothing else: the hashed form spends ~30 VALU
-// instructions per pair on the key, its home, the 2-slot read and the compares, which bounded it
-// (2.2 TB/s at C4 t = 0), not the LDS atomics.
-constexpr uint32_t PH_DENSE = 128 * 128;
 // home pair of slots of a key: the even slot its hash picks and the next one (one 8-B LDS read; a
 // 4-slot group by 16-B reads was measured slower: 1.10 vs 0.92 ms at C4 t = 0)
-template <uint32_t SLOTS>
-__device__ inline uint32_t ph_home(uint32_t key) { return ((key * 0x9E3779B1u) >> (32 - __builtin_ctz(SLOTS))) & ~1u; }
+__device__ inline uint32_t ph_home(uint32_t key) { return ((key * 0x9E3779B1u) >> (32 - 14)) & ~1u; }
 // a key missing from its home pair: linear probing from the home pair (insert at the first empty slot),
 // else the global table's id and a global atomic
-template <uint32_t SLOTS>
 __device__ inline void ph_count(uint32_t *s_key, uint32_t *s_cnt, const Tables &T, uint32_t *recount, DevState *st,
                                 uint32_t key) {
-    uint32_t h = ph_home<SLOTS>(key);
+    uint32_t h = ph_home(key);
 #pragma unroll 1
     for (int q = 0; q < PH_PROBES; q++) {
         const uint32_t k = __hip_atomic_load(&s_key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4447,21 +4438,17 @@ __device__ inline void ph_count(uint32_t *s_key, uint32_t *s_cnt, const Tables &
             const uint32_t old = atomicCAS(&s_key[h], PH_EMPTY, key);
             if (old == PH_EMPTY || old == key) { atomicAdd(&s_cnt[h], 1u); return; }
         }
-        h = (h + 1) & (SLOTS - 1);
+        h = (h + 1) & (PH_SLOTS - 1);
     }
     const uint32_t id = ht_find(T, key);
     if (id == NO_ID) { atomicAdd(&st->mismatches, 1u); return; }
     atomicAdd(&recount[id], 1u);
 }
-template <bool DENSE>
 __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__restrict__ tok, int64_t n, int32_t next_tok,
                                                               Tables T, uint32_t *__restrict__ recount, DevState *st) {
-    constexpr uint32_t SLOTS = DENSE ? PH_SLOTS / 2 : PH_SLOTS;
     extern __shared__ __attribute__((aligned(16))) uint32_t ph_lds[];
-    uint32_t *s_dense = ph_lds, *s_key = ph_lds + (DENSE ? PH_DENSE : 0), *s_cnt = s_key + SLOTS;
-    for (uint32_t i = threadIdx.x; i < SLOTS; i += PH_THREADS) { s_key[i] = PH_EMPTY; s_cnt[i] = 0; }
-    if (DENSE)
-        for (uint32_t i = threadIdx.x; i < PH_DENSE; i += PH_THREADS) s_dense[i] = 0;
+    uint32_t *s_key = ph_lds, *s_cnt = ph_lds + PH_SLOTS;
+    for (uint32_t i = threadIdx.x; i < PH_SLOTS; i += PH_THREADS) { s_key[i] = PH_EMPTY; s_cnt[i] = 0; }
     __syncthreads();
     const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
     const int64_t nvec = (n + 7) / 8;
@@ -4490,15 +4477,6 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
             const int64_t p8 = vi * 8 + 8;
             if (p8 >= n) nx = p8 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY;
             if (vi >= nvec) continue;
-            if (DENSE && p8 < n && (((v[u].x | v[u].y | v[u].z | v[u].w) & 0xFF80FF80u) | (nx & 0xFFFFFF80u)) == 0) {
-                // eight ASCII pairs: direct bins (the common vector; no key, no probe)
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t a = tok_at(v[u], k), b = k < 7 ? tok_at(v[u], k + 1) : nx;
-                    atomicAdd(&s_dense[(a << 7) | b], 1u);
-                }
-                continue;
-            }
             // the 8 pairs' first probes are issued together (one LDS round trip for the common hit), then
             // hits take a non-returning LDS add; the misses of the vector's 8 pairs are taken together
             // after them (one divergent slow path per vector, not one per pair: at 64 lanes some lane
@@ -4510,11 +4488,7 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
                 const int64_t p = vi * 8 + k;
                 const uint32_t b = k < 7 ? (p + 1 < n ? tok_at(v[u], k + 1) : (p + 1 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY)) : nx;
                 key[k] = p < n && b != PH_EMPTY ? pair_key(tok_at(v[u], k), b) : PH_EMPTY;
-                if (DENSE && key[k] != PH_EMPTY && (key[k] & 0xFF80FF80u) == 0) {  // an ASCII pair of a mixed vector
-                    atomicAdd(&s_dense[((key[k] & 0x7Fu) << 7) | (key[k] >> 16)], 1u);
-                    key[k] = PH_EMPTY;
-                }
-                h[k] = ph_home<SLOTS>(key[k]);
+                h[k] = ph_home(key[k]);
             }
             // (a plain LDS read: a slot's key only ever goes from empty to its final value, and a stale
             // empty read just sends the pair to the probing path, which re-reads with atomics)
@@ -4535,25 +4509,132 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
 #pragma unroll
                 for (int j = 1; j < 8; j++)
                     if (k == j) kk = key[j];
-                ph_count<SLOTS>(s_key, s_cnt, T, recount, st, kk);
+                ph_count(s_key, s_cnt, T, recount, st, kk);
             }
         }
     }
     __syncthreads();
-    if (DENSE)
-        for (uint32_t i = threadIdx.x; i < PH_DENSE; i += PH_THREADS) {
-            const uint32_t c = s_dense[i];
-            if (!c) continue;
-            const uint32_t id = ht_find(T, pair_key(i >> 7, i & 127u));
-            if (id == NO_ID) { atomicAdd(&st->mismatches, c); continue; }
-            atomicAdd(&recount[id], c);
-        }
-    for (uint32_t i = threadIdx.x; i < SLOTS; i += PH_THREADS) {
+    for (uint32_t i = threadIdx.x; i < PH_SLOTS; i += PH_THREADS) {
         const uint32_t k = s_key[i];
         if (k == PH_EMPTY) continue;
         const uint32_t id = ht_find(T, k);
         if (id == NO_ID) { atomicAdd(&st->mismatches, s_cnt[i]); continue; }
         atomicAdd(&recount[id], s_cnt[i]);
+    }
+}
+
+// The full pair histogram of a stream of BYTES (t = 0: every token < 256): all 65,536 byte
+// pairs in 16-bit LDS bins, two to a word (128 KiB), so a pair is a fixed bin -- no key, no hash, no
+// probe, no compare, no branch. The hashed form above spends most of its ~2,500-instruction tile on
+// exactly those (2.2 TB/s at C4 t = 0, instruction-bound); here a pair is a byte permute, a few bit
+// operations and one returning LDS add.
+//   Bin of (a, b): word (a << 7) | ((b >> 1) ^ (a & 127)) -- the row rotated by a so that text's
+//   successors (letters, space) spread over the LDS banks -- half b & 1 (low: +1, high: +0x10000).
+// A bin can pass 65,535 within a workgroup (C4's hottest pair: ~71 K per workgroup), so overflow is
+// accounted exactly, race-free, from the value each add returns (adds on one word are linearisable):
+//   - a low-half add that returns low == 0xFFFF wrapped the low bin: +65,536 to that pair's global count,
+//     and the carry it put into the high half is taken back by an LDS subtract;
+//   - an add (or the carry of a low add) that carries out of bit 31 wrapped the high bin: +65,536 to the
+//     high pair; a take-back subtract that borrows out of bit 31 undoes one such carry: -65,536.
+// Then a word's final halves are each pair's count mod 65,536 and the events add the multiples (a bin
+// with events always has real adds, so the pairs they name exist). Events are rare (one per 65,536 adds
+// of a bin) and taken in a divergent branch behind one ballot per vector.
+__device__ inline uint32_t phb_word(uint32_t ab) { return (ab >> 1) ^ ((ab >> 8) & 127u); }  // ab = a << 8 | b
+__device__ inline uint32_t phb_pair(uint32_t w, uint32_t half) {  // (a, b) of word w, half -> pair key
+    const uint32_t a = w >> 7, b = (((w & 127u) ^ (a & 127u)) << 1) | half;
+    return pair_key(a, b);
+}
+__device__ inline void phb_global(const Tables &T, uint32_t *recount, DevState *st, uint32_t key, uint32_t add) {
+    const uint32_t id = ht_find(T, key);
+    if (id == NO_ID) { atomicAdd(&st->mismatches, 1u); return; }
+    atomicAdd(&recount[id], add);
+}
+// one pair (ab = a << 8 | b) into its bin; the overflow events in the divergent branch
+__device__ inline void phb_add_events(uint32_t *bins, const Tables &T, uint32_t *recount, DevState *st, uint32_t ab,
+                                      uint32_t old) {
+    const uint32_t w = phb_word(ab), half = ab & 1u, inc = half ? 0x10000u : 1u;
+    if (!half && (old & 0xFFFFu) == 0xFFFFu) {  // the low bin wrapped: count it, take its carry back
+        phb_global(T, recount, st, phb_pair(w, 0), 0x10000u);
+        const uint32_t o2 = atomicSub(&bins[w], 0x10000u);
+        if (o2 < 0x10000u) phb_global(T, recount, st, phb_pair(w, 1), 0u - 0x10000u);  // the take-back borrowed
+    }
+    if (old + inc < old) phb_global(T, recount, st, phb_pair(w, 1), 0x10000u);  // carry out of bit 31: high wrapped
+}
+__global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist_bytes(const uint16_t *__restrict__ tok, int64_t n, int32_t next_tok,
+                                                                    Tables T, uint32_t *__restrict__ recount, DevState *st) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t bins[];  // 32,768 words: 65,536 16-bit bins
+    for (uint32_t i = threadIdx.x; i < 32768u; i += PH_THREADS) bins[i] = 0;
+    __syncthreads();
+    const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
+    const int64_t nvec = (n + 7) / 8;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (PH_THREADS / 64) + (threadIdx.x >> 6);
+    const int64_t waves = (int64_t)gridDim.x * (PH_THREADS / 64);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    for (int64_t tile = wave * PH_U * 64; tile < nvec; tile += waves * PH_U * 64) {
+        uint4 v[PH_U];
+#pragma unroll
+        for (int u = 0; u < PH_U; u++) {
+            const int64_t vi = tile + u * 64 + lane;
+            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(tv + (vi < nvec ? vi : 0)));
+            v[u] = vi < nvec ? make_uint4(y.x, y.y, y.z, y.w) : make_uint4(0, 0, 0, 0);
+        }
+        const int64_t p_last = (tile + PH_U * 64) * 8;
+        const uint32_t after_tile = lane == 63 && p_last < n ? (uint32_t)tok[p_last] : PH_EMPTY;
+#pragma unroll
+        for (int u = 0; u < PH_U; u++) {
+            const int64_t vi = tile + u * 64 + lane;
+            uint32_t nx = (uint32_t)__shfl_down((int)(v[u].x & 0xFFFFu), 1);
+            const uint32_t row0 = u + 1 < PH_U ? (uint32_t)__shfl((int)(v[u + 1 < PH_U ? u + 1 : u].x & 0xFFFFu), 0) : after_tile;
+            if (lane == 63) nx = row0;
+            const int64_t p8 = vi * 8 + 8;
+            if (p8 >= n) nx = p8 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY;
+            if (vi >= nvec) continue;
+            uint32_t ab[8], old[8];
+            if (p8 < n) {
+                // ab = a << 8 | b by one byte permute per pair: a pair inside a word (t0, t1) takes bytes
+                // {2, 0} of it, a pair across words (t1 of w, t0 of the next) bytes {4, 2} of (next : w)
+                const uint32_t w[5] = {v[u].x, v[u].y, v[u].z, v[u].w, nx};
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    ab[k] = (k & 1) ? __builtin_amdgcn_perm(w[k / 2 + 1], w[k / 2], 0x0C0C0204u)
+                                    : __builtin_amdgcn_perm(w[k / 2], w[k / 2], 0x0C0C0002u);
+            } else {  // the stream's last vector: pairs past the end go to no bin
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int64_t p = vi * 8 + k;
+                    const uint32_t b = k < 7 ? (p + 1 < n ? tok_at(v[u], k + 1) : (p + 1 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY)) : nx;
+                    ab[k] = p < n && b != PH_EMPTY ? (tok_at(v[u], k) << 8) | b : PH_EMPTY;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                old[k] = ab[k] != PH_EMPTY ? atomicAdd(&bins[phb_word(ab[k])], (ab[k] & 1u) ? 0x10000u : 1u) : 0u;
+            uint32_t ev = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t inc = (ab[k] & 1u) ? 0x10000u : 1u;
+                const bool e = ab[k] != PH_EMPTY && (((old[k] & 0xFFFFu) == 0xFFFFu && inc == 1u) || old[k] + inc < old[k]);
+                ev |= e ? 1u << k : 0u;
+            }
+            if (__builtin_expect(ev != 0, 0)) {
+                while (ev) {
+                    const int k = __builtin_ctz(ev);
+                    ev &= ev - 1;
+                    uint32_t a0 = ab[0], o0 = old[0];
+#pragma unroll
+                    for (int j = 1; j < 8; j++)
+                        if (k == j) { a0 = ab[j]; o0 = old[j]; }
+                    phb_add_events(bins, T, recount, st, a0, o0);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 32768u; i += PH_THREADS) {
+        const uint32_t x = bins[i];
+        if (x & 0xFFFFu) phb_global(T, recount, st, phb_pair(i, 0), x & 0xFFFFu);
+        if (x >> 16) phb_global(T, recount, st, phb_pair(i, 1), x >> 16);
     }
 }
 
