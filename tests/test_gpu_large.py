@@ -147,6 +147,30 @@ def test_c4_prefix_vs_oracle_golden(c4):
     assert len(tok) == ln and O.fnv64(tok) == int(fnv, 16)
 
 
+C4_FULL = "large_c4_words_utf8_1GiB_v32000.json"
+
+
+def test_c4_full_sequence_vs_oracle_golden(c4):
+    """all 31,744 C4 merges and counts equal the full golden (oracle/zig_fast.cpp: exact incremental counts, every
+    one of the ~20,000 tied merges decided by a literal Zig-map replay; it agrees with the literal oracle's
+    prefix, tests/test_oracle_fast.py), with the same tied merges; the final stream's length and FNV-64, and the
+    device stream at checkpoints spread over the run"""
+    if not os.path.exists(os.path.join(GOLDEN, C4_FULL)):
+        pytest.skip("full C4 golden not committed")
+    g = large_golden(C4_FULL)
+    assert g["complete"] and g["n_merges"] == 31744 and g["tie_replays"]["mismatches"] == 0
+    check_vs_golden(c4, g, 31744)
+    assert c4.stats.tie_iterations == sum(t > 1 for t in g["ties"])
+    k, ln, fnv = g["fnv64_after"][-1]
+    assert k == 31744 and c4.final_len == ln and c4.final_fnv == int(fnv, 16)
+    cps = {k: (ln, h) for k, ln, h in g["fnv64_after"]}
+    for k in (2048, 8192, 16384, 24576, 30720):
+        ln, h = cps[k]
+        _, _, st = c4.e.train_resident(256 + k)
+        tok = c4.e.tokens()
+        assert len(tok) == ln and O.fnv64(tok) == int(h, 16), k
+
+
 def test_c4_late_ties_exact_window(c4):
     """>= 50 consecutive late C4 tie decisions (merges 25,000-25,069) taken by both the device's
     cluster test and the exact Zig-map emulation (first occurrences of all ~4e7 live pairs); a

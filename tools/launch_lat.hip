@@ -103,6 +103,44 @@ __global__ void barrier_k(unsigned *count, unsigned *gen, int iters, unsigned *e
         if (!grid_sync(count, gen, gridDim.x, err)) return;
 }
 
+// GPU-side kernel boundary: kernel A spins `spin` ticks, may dirty `dirty` words per block with plain
+// stores, and its last block to finish stamps the end (atomicMax); kernel B's first block stamps its start
+// (atomicMin). A is long enough for the host to run ahead, so B is queued when A ends.
+__global__ void bnd_a(unsigned long long *t, uint32_t *junk, int dirty, long long spin) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < spin) __builtin_amdgcn_s_sleep(1);
+    for (int k = 0; k < dirty; k++) junk[((size_t)blockIdx.x * dirty + k) * blockDim.x + threadIdx.x] = k;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&t[0], (unsigned long long)wall_clock64());
+}
+__global__ void bnd_b(unsigned long long *t) {
+    if (threadIdx.x == 0) atomicMin(&t[1], (unsigned long long)wall_clock64());
+}
+// the same hand-off inside one launch: blocks [0, na) spin and arrive on a counter (after their stores
+// drain), blocks [na, ...) wait for all arrivals (sc1 polls) and stamp
+__global__ void bnd_fused(unsigned long long *t, uint32_t *junk, int dirty, long long spin, uint32_t na, uint32_t *ctr) {
+    if (blockIdx.x < na) {
+        const long long t0 = wall_clock64();
+        while (wall_clock64() - t0 < spin) __builtin_amdgcn_s_sleep(1);
+        for (int k = 0; k < dirty; k++)
+            __hip_atomic_store(&junk[((size_t)blockIdx.x * dirty + k) * blockDim.x + threadIdx.x], (uint32_t)k, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            atomicMax(&t[0], (unsigned long long)wall_clock64());
+            __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    if (threadIdx.x == 0) {
+        const long long t0 = wall_clock64();
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < na && wall_clock64() - t0 < 5000000)
+            __builtin_amdgcn_s_sleep(1);
+        atomicMin(&t[1], (unsigned long long)wall_clock64());
+    }
+}
+
 int main() {
     hipStream_t s;
     CK(hipStreamCreate(&s));
@@ -210,6 +248,39 @@ int main() {
         CK(hipEventElapsedTime(&ms, e0, e1));
         printf("{\"test\": \"lds_atomic_chain\", \"ns_per_atomic\": %.1f}\n", ms * 1e6 / steps);
         CK(hipFree(a));
+    }
+    {  // GPU-side boundary between dependent kernels, and the in-launch hand-off
+        unsigned long long *t;
+        uint32_t *junk, *ctr;
+        CK(hipMalloc(&t, 16));
+        CK(hipMalloc(&junk, (size_t)64 << 20));
+        CK(hipMalloc(&ctr, 4));
+        for (int fused = 0; fused < 2; fused++)
+            for (int ga : {8, 64, 256})
+                for (int gb : {8, 256})
+                    for (int dirty : {0, 16}) {
+                        double sum = 0;
+                        const int reps = 50;
+                        for (int r = 0; r < reps; r++) {
+                            unsigned long long h[2] = {0, ~0ull};
+                            CK(hipMemcpyAsync(t, h, 16, hipMemcpyHostToDevice, s));
+                            CK(hipMemsetAsync(ctr, 0, 4, s));
+                            if (fused) {
+                                bnd_fused<<<ga + gb, 256, 0, s>>>(t, junk, dirty, 2000, ga, ctr);
+                            } else {
+                                bnd_a<<<ga, 256, 0, s>>>(t, junk, dirty, 2000);
+                                bnd_b<<<gb, 256, 0, s>>>(t);
+                            }
+                            CK(hipMemcpyAsync(h, t, 16, hipMemcpyDeviceToHost, s));
+                            CK(hipStreamSynchronize(s));
+                            if (r) sum += (double)(h[1] - h[0]) * 0.01;  // 100 MHz ticks -> us
+                        }
+                        printf("{\"test\": \"boundary\", \"form\": \"%s\", \"grid_a\": %d, \"grid_b\": %d, \"dirty_KB_per_block\": %d, \"us_end_to_start\": %.3f}\n",
+                               fused ? "in-launch counter" : "kernel boundary", ga, gb, dirty * 1, sum / (reps - 1));
+                    }
+        CK(hipFree(t));
+        CK(hipFree(junk));
+        CK(hipFree(ctr));
     }
     // grid barrier: all blocks resident (grid <= CUs)
     unsigned *cnt, *gen, *err;

@@ -1105,6 +1105,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                         "(%llu samples; all from the first argmax block's start)\n", P[8],
                 P[3] * us / nd, P[10] * us / nd, P[9] * us / nd, P[4] * us / nd, P[12] * us / nr, P[13], P[6] * us / np,
                 P[11] * us / np, P[14]);
+        fprintf(stderr, "sel_prof: refresh workgroups: %llu, average duration %.2f us (start to its summaries stored)\n", P[16],
+                P[15] * us / std::max(1.0, (double)P[16]));
         static const char *bucket[3] = {"merges < 7936", "merges 7936-19743", "merges >= 19744"};
         for (int k = 0; k < 3; k++) {
             const unsigned long long *Q = h_st->pipe_prof[k];
@@ -1242,7 +1244,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
                        dist() ? world : 1, (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
                        scan_plan && lists_on ? 1 : 0};
-            zbpe_select_next<<<sel + (C ? nsb : 0), NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hot_cap, C ? nsb : 0u, sel,
+            const uint32_t nref = C ? (refresh_wgs ? std::min<uint32_t>(nsb, refresh_wgs) : nsb) : 0u;
+            zbpe_select_next<<<sel + nref, NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hot_cap, nref, sel,
                                                                                  d_tok[cur], slots, T, d_partial, left, X, N);
             LAUNCH_OK();
         } else {

@@ -3931,9 +3931,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                                                                  NextArgs N) {
     // blocks [0, nref) refresh the home super-blocks (the longest role: dispatched first, one
     // workgroup per CU at this kernel's VGPR count), blocks [nref, nref + sel_blocks) run the argmax
-    const uint32_t nref = nref_arg;  // == N.V.C ? N.V.nsb : 0
+    const uint32_t nref = nref_arg;  // N.V.C ? min(N.V.nsb, refresh_wgs) : 0
     const uint32_t tid = threadIdx.x;
     if (blockIdx.x < nref) {
+        const unsigned long long t_ref0 = N.prof ? wall_clock64() : 0ull;
         // refresh role, off the argmax's ticket: the last argmax block reduces, rolls and starts
         // merge X+1 while these blocks work, and waits for their arrivals only before a tie
         // decision. They run even after a halt (a halted batch dirties no blocks; a refresh is
@@ -3948,9 +3949,19 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // critical path: the argmax grid is sized by the hot list alone; nothing in this launch reads
         // [0, 2X) -- the roll reads the tail words past it)
         for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
-        refresh_super(T, blockIdx.x, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), true,
-                      home_dirty_bits(T, blockIdx.x));
-        if (N.prof && tid == 0) atomicMax(&st->sel_tr, (unsigned long long)wall_clock64());
+        // nref may be below the super-block count (option refresh_wgs): a smaller grid ends sooner -- a kernel
+        // boundary after 256 workgroups costs ~3.7 us, after 64 ~1.6 (tools/launch_lat.hip, boundary rows)
+        for (uint32_t sb = blockIdx.x; sb < N.V.nsb; sb += nref) {
+            refresh_super(T, sb, N.V.C, N.V.nb, const_cast<Summ *>(N.V.summ), const_cast<Summ *>(N.V.sup), true,
+                          home_dirty_bits(T, sb));
+            if (nref < N.V.nsb) __syncthreads();  // (refresh_super's LDS summaries are reused by the next one)
+        }
+        if (N.prof && tid == 0) {
+            const unsigned long long t_ref1 = wall_clock64();
+            atomicMax(&st->sel_tr, t_ref1);
+            atomicAdd(&st->sel_prof[15], t_ref1 - t_ref0);
+            atomicAdd(&st->sel_prof[16], 1ull);
+        }
         __shared__ uint32_t s_rlast;
         uint32_t *rtk = N.rtk + (X & 1) * RTK_SET;
         if (!pfx) {
