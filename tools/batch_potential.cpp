@@ -114,7 +114,7 @@ int main(int argc, char **argv) {
     t.pre_apply = hook;
     if (t.run(nullptr) != 0) { fprintf(stderr, "oracle run failed\n"); return 2; }
     const uint32_t m = t.merges_done;
-    for (int rule = 0; rule < 2; rule++) {
+    for (int rule = 0; rule < 3; rule++) {  // 2: exact, but only rounds whose leader's tie set has exactly two pairs
         uint64_t rounds = 0, merges = 0;
         std::map<int, uint64_t> sizes;
         uint32_t k = from;
@@ -123,7 +123,7 @@ int main(int argc, char **argv) {
             std::vector<uint32_t> members{k};
             uint32_t j = k + 1;
             size_t next_home = 1;  // conservative: the leader's tied pairs in home order
-            while ((int)members.size() < K && j < m && !lead.self && lead.ties > 1) {
+            while ((int)members.size() < (rule == 2 ? 2 : K) && j < m && !lead.self && lead.ties > 1 && (rule != 2 || lead.ties == 2)) {
                 const MergeInfo &c = g_info[j];
                 if (c.self || c.T != lead.T || c.cap != lead.cap) break;
                 bool was_tied = std::find(lead.tied_keys_by_home.begin(), lead.tied_keys_by_home.end(), c.key) != lead.tied_keys_by_home.end();
@@ -132,7 +132,7 @@ int main(int argc, char **argv) {
                 for (uint32_t i : members) {
                     const MergeInfo &mi = g_info[i];
                     if (mi.max_new >= lead.T) ok = false;
-                    if (rule == 0 && touches(mi, c)) ok = false;
+                    if (rule != 1 && touches(mi, c)) ok = false;
                     if (rule == 1 && token_clash(mi, c)) ok = false;
                 }
                 if (rule == 1) {
@@ -148,7 +148,7 @@ int main(int argc, char **argv) {
             sizes[(int)members.size()]++;
             k += (uint32_t)members.size();
         }
-        printf("%s rule, K=%d, merges %u..%u: %llu merges in %llu rounds = %.3f merges/round; sizes:", rule ? "conservative" : "exact", K,
+        printf("%s rule, K=%d, merges %u..%u: %llu merges in %llu rounds = %.3f merges/round; sizes:", rule == 2 ? "exact-two-tied" : rule ? "conservative" : "exact", rule == 2 ? 2 : K,
                from, m, (unsigned long long)merges, (unsigned long long)rounds, (double)merges / rounds);
         for (auto &x : sizes) printf(" %d:%llu", x.first, (unsigned long long)x.second);
         printf("\n");

@@ -30,6 +30,10 @@ __global__ void lds_k(int *p) {
     if (p && l[(threadIdx.x + 1) & 255] == 999999u) p[0] = 1;
 }
 
+__global__ void stride_init_k(uint32_t *next, uint64_t n, uint64_t stride) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        next[i] = (uint32_t)((i + stride) % n);
+}
 __global__ void chase_k(const uint32_t *next, int steps, uint32_t *out) {
     uint32_t i = 0;
     for (int s = 0; s < steps; s++) i = __builtin_nontemporal_load(&next[i]);
@@ -199,6 +203,26 @@ int main() {
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&ms, e0, e1));
         printf("{\"test\": \"chase\", \"bytes\": %zu, \"ns_per_load\": %.1f}\n", bytes, ms * 1e6 / steps);
+        CK(hipFree(d));
+        CK(hipFree(o));
+    }
+    // pointer chase with a page-sized stride over large buffers: every step touches another 2 MiB page, so
+    // the latency includes a GPU TLB miss once the pages outnumber what the TLBs hold
+    for (size_t bytes : {(size_t)64 << 20, (size_t)512 << 20, (size_t)2 << 30, (size_t)8 << 30}) {
+        const uint64_t n = bytes / 4, stride = ((2u << 20) * 37 + 64) / 4;
+        uint32_t *d, *o;
+        if (hipMalloc(&d, bytes) != hipSuccess) { printf("{\"test\": \"chase_pages\", \"bytes\": %zu, \"error\": \"alloc\"}\n", bytes); continue; }
+        CK(hipMalloc(&o, 4));
+        stride_init_k<<<4096, 256, 0, s>>>(d, n, stride);
+        const int steps = 20000;
+        chase_k<<<1, 1, 0, s>>>(d, steps, o);
+        CK(hipEventRecord(e0, s));
+        chase_k<<<1, 1, 0, s>>>(d, steps, o);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"test\": \"chase_pages\", \"bytes\": %zu, \"stride_bytes\": %llu, \"ns_per_load\": %.1f}\n", bytes,
+               (unsigned long long)stride * 4, ms * 1e6 / steps);
         CK(hipFree(d));
         CK(hipFree(o));
     }

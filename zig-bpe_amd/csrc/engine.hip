@@ -1107,6 +1107,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                 P[11] * us / np, P[14]);
         fprintf(stderr, "sel_prof: refresh workgroups: %llu, average duration %.2f us (start to its summaries stored)\n", P[16],
                 P[15] * us / std::max(1.0, (double)P[16]));
+        fprintf(stderr, "sel_prof: argmax block 0 (from its start): hot counts in %.2f us, block max %.2f us\n", P[17] * us / calls,
+                P[18] * us / calls);
         static const char *bucket[3] = {"merges < 7936", "merges 7936-19743", "merges >= 19744"};
         for (int k = 0; k < 3; k++) {
             const unsigned long long *Q = h_st->pipe_prof[k];
@@ -1242,9 +1244,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
-                       dist() ? world : 1, (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
-                       scan_plan && lists_on ? 1 : 0};
-            const uint32_t nref = C ? (refresh_wgs ? std::min<uint32_t>(nsb, refresh_wgs) : nsb) : 0u;
+                       dist() ? world : 1, (int)sel_prof, tie_trust ? nullptr : cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
+                       scan_plan && lists_on ? 1 : 0, tie_trust ? 1 : 0};
+            const uint32_t nref = C && !tie_trust ? (refresh_wgs ? std::min<uint32_t>(nsb, refresh_wgs) : nsb) : 0u;
             zbpe_select_next<<<sel + nref, NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hot_cap, nref, sel,
                                                                                  d_tok[cur], slots, T, d_partial, left, X, N);
             LAUNCH_OK();

@@ -3737,8 +3737,10 @@ template <int NT = DECIDE_THREADS>
 __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
-                                   uint32_t plan_gen = 0) {
+                                   uint32_t plan_gen = 0, bool trust = false) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
+    // trust (option tie_trust, a TIMING EXPERIMENT only, never a default): the smallest home wins with no
+    // cluster or wrap test -- what a decision costs without the home summaries
     // plan (NT >= 256): wave 3 finds the smallest home's key itself and loads its scan plan during the
     // carries; the commit below stores it with cur_key
     __shared__ uint32_t s_plan[6];
@@ -3767,8 +3769,10 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
             hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
         }
         const uint32_t h1 = (uint32_t)(m1 >> 32);
-        const int64_t f = !len ? -1 : cs ? wave_first_free(V, h1, wave_carry_from_super(V, cs, h1)) : wave_free_from(V, h1);
+        const int64_t f = !len ? -1 : trust ? (int64_t)V.C : cs ? wave_first_free(V, h1, wave_carry_from_super(V, cs, h1)) : wave_free_from(V, h1);
         if (lane == 0) { s_free = f; s_m1 = m1; s_m2 = m2; s_hmax = hmax; }
+    } else if (trust) {
+        if (w == 1 && lane == 0) { s_c0 = 0; s_last = -2; }
     } else if (cs) {  // carry into slot 0 and the wrap test's last free slot: precomputed (refresh_prefix)
         if (w == 1 && lane == 0) {
             s_c0 = (int32_t)ld_wt(cs);
@@ -3789,7 +3793,7 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
         if (lane == 0) plan_compute(plan, (uint32_t)m1, s_plan);
     }
     __syncthreads();
-    if (!ws && !cs) {  // a map of at most 4096 slots: the last free slot needs the carry into slot 0
+    if (!ws && !cs && !trust) {  // a map of at most 4096 slots: the last free slot needs the carry into slot 0
         if (w == 2) {
             const int64_t lf = s_c0 > 0 ? wave_last_free(V, 0, V.C, s_c0) : -2;
             if (lane == 0) s_last = lf;
@@ -3803,7 +3807,7 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
     uint32_t verdict = total > len ? 1u : 0u;
     const int64_t s = s_free;  // first free slot at or after h1
     if (s < 0) verdict = 1;     // the run of h1 wraps (or is absurdly long)
-    if (m2 != ~0ull && s > (int64_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
+    if (!trust && m2 != ~0ull && s > (int64_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
     const long long lf = s_c0 > 0 ? s_last : -2;  // -2: no run wraps past slot C-1
     if (lf != -2 && (lf < 0 || (long long)hmax >= lf + 1)) verdict = 1;  // a tied pair may have wrapped
     st->tie_verdict = verdict;
@@ -3878,6 +3882,7 @@ struct NextArgs {
     const uint32_t *dir_row, *dir;
     uint32_t dir_w, gen;
     int plan;
+    int trust;            // option tie_trust (timing experiment): no refresh workgroups, no cluster test
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -4076,6 +4081,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
 #pragma unroll
         for (int u = 0; u < SEL_U; u++)
             if (cs[u] >= theta && cs[u]) r = max_combine(r, MaxRec{cs[u], 1u, ids[u]});
+        if (N.prof && bx == 0 && tid == 0) atomicAdd(&st->sel_prof[17], wall_clock64() - st->sel_t0);  // thread 0's counts in
         const bool one_step = SEL_U * G >= nh;  // (every entry was in the first step)
         for (uint32_t i0 = i00 + SEL_U * G; i0 < nh; i0 += SEL_U * G) {
 #pragma unroll
@@ -4092,6 +4098,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
         if (tid == 0) s_nc = 0;
         R = block_max(r, sm);
+        if (N.prof && bx == 0 && tid == 0) atomicAdd(&st->sel_prof[18], wall_clock64() - st->sel_t0);
         // the block's keys at its max (from the registers when the thread's entries fit one step)
         if (R.cnt && r.cnt == R.cnt) {
             if (one_step && SEL_U * G >= nh) {
@@ -4347,7 +4354,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
-                              plan_on, plan, N.gen);
+                              plan_on, plan, N.gen, N.trust != 0);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }
@@ -4536,9 +4543,9 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
 
 // The full pair histogram of a stream of BYTES (t = 0: every token < 256): all 65,536 byte
 // pairs in 16-bit LDS bins, two to a word (128 KiB), so a pair is a fixed bin -- no key, no hash, no
-// probe, no compare, no branch. The hashed form above spends most of its ~2,500-instruction tile on
-// exactly those (2.2 TB/s at C4 t = 0, instruction-bound); here a pair is a byte permute, a few bit
-// operations and one returning LDS add.
+// probe, no compare. The hashed form above spends most of its ~2,500-instruction tile on exactly those
+// (2.2 TB/s at C4 t = 0, instruction-bound); here a pair is a byte permute, three bit operations and one
+// LDS add.
 //   Bin of (a, b): word (a << 7) | ((b >> 1) ^ (a & 127)) -- the row rotated by a so that text's
 //   successors (letters, space) spread over the LDS banks -- half b & 1 (low: +1, high: +0x10000).
 // A bin can pass 65,535 within a workgroup (C4's hottest pair: ~71 K per workgroup), so overflow is
@@ -4547,9 +4554,12 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
 //     and the carry it put into the high half is taken back by an LDS subtract;
 //   - an add (or the carry of a low add) that carries out of bit 31 wrapped the high bin: +65,536 to the
 //     high pair; a take-back subtract that borrows out of bit 31 undoes one such carry: -65,536.
-// Then a word's final halves are each pair's count mod 65,536 and the events add the multiples (a bin
-// with events always has real adds, so the pairs they name exist). Events are rare (one per 65,536 adds
-// of a bin) and taken in a divergent branch behind one ballot per vector.
+// Then a word's final halves are each pair's count mod 65,536 and the events add the multiples (a bin with
+// events always has real adds, so the pairs they name exist). Events are rare (one per 65,536 adds of a
+// bin) and taken in a divergent branch behind one test per vector. (Spilling every half past 32,768 after
+// each 32,768-pair pass instead -- non-returning adds, no event test -- was slower: 892 vs 642 us at C4
+// t = 0, the pass barriers keep the waves from hiding each other's load latency.)
+constexpr uint32_t PHB_WORDS = 32768;
 __device__ inline uint32_t phb_word(uint32_t ab) { return (ab >> 1) ^ ((ab >> 8) & 127u); }  // ab = a << 8 | b
 __device__ inline uint32_t phb_pair(uint32_t w, uint32_t half) {  // (a, b) of word w, half -> pair key
     const uint32_t a = w >> 7, b = (((w & 127u) ^ (a & 127u)) << 1) | half;
@@ -4560,9 +4570,8 @@ __device__ inline void phb_global(const Tables &T, uint32_t *recount, DevState *
     if (id == NO_ID) { atomicAdd(&st->mismatches, 1u); return; }
     atomicAdd(&recount[id], add);
 }
-// one pair (ab = a << 8 | b) into its bin; the overflow events in the divergent branch
-__device__ inline void phb_add_events(uint32_t *bins, const Tables &T, uint32_t *recount, DevState *st, uint32_t ab,
-                                      uint32_t old) {
+// an add to pair ab returned `old`: its overflow events (divergent, rare)
+__device__ inline void phb_events(uint32_t *bins, const Tables &T, uint32_t *recount, DevState *st, uint32_t ab, uint32_t old) {
     const uint32_t w = phb_word(ab), half = ab & 1u, inc = half ? 0x10000u : 1u;
     if (!half && (old & 0xFFFFu) == 0xFFFFu) {  // the low bin wrapped: count it, take its carry back
         phb_global(T, recount, st, phb_pair(w, 0), 0x10000u);
@@ -4571,78 +4580,75 @@ __device__ inline void phb_add_events(uint32_t *bins, const Tables &T, uint32_t 
     }
     if (old + inc < old) phb_global(T, recount, st, phb_pair(w, 1), 0x10000u);  // carry out of bit 31: high wrapped
 }
+__device__ inline uint32_t phb_add(uint32_t *bins, uint32_t ab) {  // the pair's add; returns the word's old value
+    return atomicAdd(&bins[phb_word(ab)], (ab & 1u) ? 0x10000u : 1u);
+}
+__device__ inline bool phb_event(uint32_t ab, uint32_t old) {  // did this add wrap a half?
+    const uint32_t inc = (ab & 1u) ? 0x10000u : 1u, nw = old + inc;
+    return nw < old || (inc == 1u && (nw & 0xFFFFu) == 0u);
+}
 __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist_bytes(const uint16_t *__restrict__ tok, int64_t n, int32_t next_tok,
                                                                     Tables T, uint32_t *__restrict__ recount, DevState *st) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t bins[];  // 32,768 words: 65,536 16-bit bins
-    for (uint32_t i = threadIdx.x; i < 32768u; i += PH_THREADS) bins[i] = 0;
+    extern __shared__ __attribute__((aligned(16))) uint32_t bins[];  // PHB_WORDS words: 65,536 16-bit bins
+    for (uint32_t i = threadIdx.x; i < PHB_WORDS; i += PH_THREADS) bins[i] = 0;
     __syncthreads();
+    // vectors whose eight pairs all have their successor inside the stream (the loop below, no edge tests);
+    // the pairs of the stream's last vector or two (successor next_tok or none) are counted at the end
+    const int64_t nfull = n >= 1 ? (n - 1) / 8 : 0, nvec = (n + 7) / 8;
     const uint4 *tv = reinterpret_cast<const uint4 *>(tok);
-    const int64_t nvec = (n + 7) / 8;
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * (PH_THREADS / 64) + (threadIdx.x >> 6);
     const int64_t waves = (int64_t)gridDim.x * (PH_THREADS / 64);
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    for (int64_t tile = wave * PH_U * 64; tile < nvec; tile += waves * PH_U * 64) {
+    for (int64_t tile = wave * PH_U * 64; tile < nfull; tile += waves * PH_U * 64) {
         uint4 v[PH_U];
 #pragma unroll
         for (int u = 0; u < PH_U; u++) {
+            // (loaded up to the stream's end: the last full vector's successor is the next one's first token)
             const int64_t vi = tile + u * 64 + lane;
             const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(tv + (vi < nvec ? vi : 0)));
-            v[u] = vi < nvec ? make_uint4(y.x, y.y, y.z, y.w) : make_uint4(0, 0, 0, 0);
+            v[u] = make_uint4(y.x, y.y, y.z, y.w);
         }
-        const int64_t p_last = (tile + PH_U * 64) * 8;
-        const uint32_t after_tile = lane == 63 && p_last < n ? (uint32_t)tok[p_last] : PH_EMPTY;
+        const int64_t p_last = (tile + PH_U * 64) * 8;  // the token after the tile
+        const uint32_t after_tile = lane == 63 && p_last < n ? (uint32_t)tok[p_last] : 0u;
 #pragma unroll
         for (int u = 0; u < PH_U; u++) {
             const int64_t vi = tile + u * 64 + lane;
-            uint32_t nx = (uint32_t)__shfl_down((int)(v[u].x & 0xFFFFu), 1);
-            const uint32_t row0 = u + 1 < PH_U ? (uint32_t)__shfl((int)(v[u + 1 < PH_U ? u + 1 : u].x & 0xFFFFu), 0) : after_tile;
+            uint32_t nx = (uint32_t)__shfl_down((int)v[u].x, 1);
+            const uint32_t row0 = u + 1 < PH_U ? (uint32_t)__shfl((int)v[u + 1 < PH_U ? u + 1 : u].x, 0) : after_tile;
             if (lane == 63) nx = row0;
-            const int64_t p8 = vi * 8 + 8;
-            if (p8 >= n) nx = p8 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY;
-            if (vi >= nvec) continue;
+            if (vi >= nfull) continue;
+            // ab = a << 8 | b by one byte permute per pair: a pair inside a word (t0, t1) takes bytes {2, 0}
+            // of it, a pair across words (t1 of w, t0 of the next) bytes {4, 2} of (next : w)
+            const uint32_t w[5] = {v[u].x, v[u].y, v[u].z, v[u].w, nx};
             uint32_t ab[8], old[8];
-            if (p8 < n) {
-                // ab = a << 8 | b by one byte permute per pair: a pair inside a word (t0, t1) takes bytes
-                // {2, 0} of it, a pair across words (t1 of w, t0 of the next) bytes {4, 2} of (next : w)
-                const uint32_t w[5] = {v[u].x, v[u].y, v[u].z, v[u].w, nx};
-#pragma unroll
-                for (int k = 0; k < 8; k++)
-                    ab[k] = (k & 1) ? __builtin_amdgcn_perm(w[k / 2 + 1], w[k / 2], 0x0C0C0204u)
-                                    : __builtin_amdgcn_perm(w[k / 2], w[k / 2], 0x0C0C0002u);
-            } else {  // the stream's last vector: pairs past the end go to no bin
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const int64_t p = vi * 8 + k;
-                    const uint32_t b = k < 7 ? (p + 1 < n ? tok_at(v[u], k + 1) : (p + 1 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY)) : nx;
-                    ab[k] = p < n && b != PH_EMPTY ? (tok_at(v[u], k) << 8) | b : PH_EMPTY;
-                }
-            }
 #pragma unroll
             for (int k = 0; k < 8; k++)
-                old[k] = ab[k] != PH_EMPTY ? atomicAdd(&bins[phb_word(ab[k])], (ab[k] & 1u) ? 0x10000u : 1u) : 0u;
-            uint32_t ev = 0;
+                ab[k] = (k & 1) ? __builtin_amdgcn_perm(w[k / 2 + 1], w[k / 2], 0x0C0C0204u)
+                                : __builtin_amdgcn_perm(w[k / 2], w[k / 2], 0x0C0C0002u);
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t inc = (ab[k] & 1u) ? 0x10000u : 1u;
-                const bool e = ab[k] != PH_EMPTY && (((old[k] & 0xFFFFu) == 0xFFFFu && inc == 1u) || old[k] + inc < old[k]);
-                ev |= e ? 1u << k : 0u;
-            }
-            if (__builtin_expect(ev != 0, 0)) {
-                while (ev) {
-                    const int k = __builtin_ctz(ev);
-                    ev &= ev - 1;
-                    uint32_t a0 = ab[0], o0 = old[0];
+            for (int k = 0; k < 8; k++) old[k] = phb_add(bins, ab[k]);
+            bool ev = false;
 #pragma unroll
-                    for (int j = 1; j < 8; j++)
-                        if (k == j) { a0 = ab[j]; o0 = old[j]; }
-                    phb_add_events(bins, T, recount, st, a0, o0);
-                }
+            for (int k = 0; k < 8; k++) ev |= phb_event(ab[k], old[k]);
+            if (__builtin_expect(ev, 0)) {
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (phb_event(ab[k], old[k])) phb_events(bins, T, recount, st, ab[k], old[k]);
             }
         }
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // pairs starting in vectors [nfull, ...): successor next_tok or none
+        for (int64_t p = nfull * 8; p < n; p++) {
+            const int32_t b = p + 1 < n ? (int32_t)tok[p + 1] : next_tok;
+            if (b < 0) continue;
+            const uint32_t ab = ((uint32_t)tok[p] << 8) | (uint32_t)b;
+            const uint32_t old = phb_add(bins, ab);
+            if (phb_event(ab, old)) phb_events(bins, T, recount, st, ab, old);
+        }
+    }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < 32768u; i += PH_THREADS) {
+    for (uint32_t i = threadIdx.x; i < PHB_WORDS; i += PH_THREADS) {
         const uint32_t x = bins[i];
         if (x & 0xFFFFu) phb_global(T, recount, st, phb_pair(i, 0), x & 0xFFFFu);
         if (x >> 16) phb_global(T, recount, st, phb_pair(i, 1), x >> 16);

@@ -83,7 +83,7 @@ struct DevState {
     unsigned long long sel_t0, sel_ta, sel_tr;  // start; latest argmax / refresh block finish
     // [0..4] last-block phases, [5] argmax blocks done, [7] last-block calls, [8] tie decisions, [9] their carries,
     // [10] refresh wait, [12] latest refresh block done (at decisions, [13] samples), [6]/[11] prefix start/end ([14] samples)
-    unsigned long long sel_prof[18];  // [15]/[16]: summed refresh-workgroup durations / their count
+    unsigned long long sel_prof[20];  // [15]/[16]: summed refresh-workgroup durations / their count; [17]/[18] argmax: counts in / block max (last argmax block)
     unsigned long long sel_prof_pq, sel_prof_pp;  // refresh_prefix start / end stamps of the current launch
     // option sel_prof, whole merge pipeline (batch mode): probe stamps of the current launches and the
     // sums they fold into (Engine::train prints them): scan (list form) LDS clear / walk / flush done and
