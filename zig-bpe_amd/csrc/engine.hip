@@ -55,7 +55,7 @@ Engine::~Engine() { release(); }
 void Engine::release() {
     auto f = [](void *p) { if (p) (void)hipFree(p); };
     f(d_text); f(d_tok[0]); f(d_tok[1]);
-    f(T.ht); f(T.id_key); f(T.id_cnt);
+    f(T.ht); f(T.id_key); f(T.id_cnt); f(T.hpos); f(T.hcnt);
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_cs); f(d_rtk); f(d_sizes);
@@ -204,25 +204,26 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     size_t ht_cap_new = 1;
     while (ht_cap_new < 2 * id_cap_new || ht_cap_new < 64) ht_cap_new <<= 1;  // >= 8 buckets of 8
     Tables N{};
-    N.hot = T.hot; N.hot_cap = T.hot_cap; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
+    N.hot = T.hot; N.hot_cap = T.hot_cap; N.hcnt = T.hcnt; N.home_cnt = T.home_cnt; N.home_mask = T.home_mask;
     N.home_dirty = T.home_dirty;
     N.tok_cnt = T.tok_cnt; N.lst_off = T.lst_off; N.lst_len = T.lst_len;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
     if (hipMalloc(&N.ht, ht_cap_new * 8) != hipSuccess || hipMalloc(&N.id_key, id_cap_new * 4) != hipSuccess ||
-        hipMalloc(&N.id_cnt, id_cap_new * 4) != hipSuccess) {
+        hipMalloc(&N.id_cnt, id_cap_new * 4) != hipSuccess || hipMalloc(&N.hpos, id_cap_new * 4) != hipSuccess) {
         (void)hipGetLastError();
-        for (void *p : {(void *)N.ht, (void *)N.id_key, (void *)N.id_cnt}) if (p) (void)hipFree(p);
+        for (void *p : {(void *)N.ht, (void *)N.id_key, (void *)N.id_cnt, (void *)N.hpos}) if (p) (void)hipFree(p);
         return fail(ZBPE_OUT_OF_MEMORY, "pair table allocation (%zu ids) failed", id_cap_new);
     }
     HIP_OK(hipMemsetAsync(N.ht, 0xFF, ht_cap_new * 8, stream));
+    HIP_OK(hipMemsetAsync(N.hpos, 0xFF, id_cap_new * 4, stream));  // no id listed (the hot list is rebuilt)
     if (T.id_key) {  // rebuild from the old tables
         uint32_t old_n = h_st->num_ids;
         HIP_OK(hipMemsetAsync(&d_st->num_ids, 0, 4, stream));
         zbpe_rebuild<<<std::min<uint32_t>(2048, (old_n + 255) / 256 + 1), 256, 0, stream>>>(T.id_key, T.id_cnt, old_n, N, d_st);
         LAUNCH_OK();
         HIP_OK(hipStreamSynchronize(stream));
-        (void)hipFree(T.ht); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt);
+        (void)hipFree(T.ht); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt); (void)hipFree(T.hpos);
         stats_rebuilds++;
     }
     T = N;
@@ -496,10 +497,16 @@ zbpe_status Engine::rebuild_hot() {
         theta = count_bin_lo(b);
     }
     const size_t need = std::max<size_t>(4 * hot_target, 2 * cum + 4096);
+    if (T.hot) {  // the current list's ids unlisted (Tables::hpos) before the list is rebuilt
+        zbpe_hot_clear<<<64, 256, 0, stream>>>(T, d_st);
+        LAUNCH_OK();
+    }
     if (!T.hot || hot_cap_alloc < need) {
         if (T.hot) (void)hipFree(T.hot);
+        if (T.hcnt) (void)hipFree(T.hcnt);
         T.hot = nullptr;
-        if (hipMalloc(&T.hot, need * 8) != hipSuccess) {
+        T.hcnt = nullptr;
+        if (hipMalloc(&T.hot, need * 8) != hipSuccess || hipMalloc(&T.hcnt, need * 4) != hipSuccess) {
             (void)hipGetLastError();
             hot_cap_alloc = 0;
             return fail(ZBPE_OUT_OF_MEMORY, "hot list allocation (%zu ids) failed", need);
@@ -949,10 +956,14 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     lists_on = false;
     list_streak = false;
     if (!T.id_key || T.id_cap < (1u << 20)) {
-        if (T.id_key) { (void)hipFree(T.ht); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt); T.ht = nullptr; T.id_key = T.id_cnt = nullptr; }
+        if (T.id_key) {
+            (void)hipFree(T.ht); (void)hipFree(T.id_key); (void)hipFree(T.id_cnt); (void)hipFree(T.hpos);
+            T.ht = nullptr; T.id_key = T.id_cnt = T.hpos = nullptr;
+        }
         CHECK(alloc_tables(1u << 20));
     } else {
         HIP_OK(hipMemsetAsync(T.ht, 0xFF, ((size_t)T.ht_mask + 1) * 8, stream));
+        HIP_OK(hipMemsetAsync(T.hpos, 0xFF, (size_t)T.id_cap * 4, stream));  // ids restart at 0
     }
     HIP_OK(hipMemsetAsync(d_st, 0, sizeof(DevState), stream));
     {
@@ -1247,7 +1258,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                        dist() ? world : 1, (int)sel_prof, tie_trust ? nullptr : cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
                        scan_plan && lists_on ? 1 : 0, tie_trust ? 1 : 0};
             const uint32_t nref = C && !tie_trust ? (refresh_wgs ? std::min<uint32_t>(nsb, refresh_wgs) : nsb) : 0u;
-            zbpe_select_next<<<sel + nref, NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hot_cap, nref, sel,
+            zbpe_select_next<<<sel + nref, NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hcnt, T.hot_cap, nref, sel,
                                                                                  d_tok[cur], slots, T, d_partial, left, X, N);
             LAUNCH_OK();
         } else {

@@ -142,6 +142,21 @@ __device__ inline uint32_t wave_append(uint32_t *counter, bool flag) {
     return flag ? base + (uint32_t)__popcll(below) : ~0u;
 }
 __device__ inline unsigned long long hot_entry(uint32_t key, uint32_t id) { return ((unsigned long long)key << 32) | id; }
+// hot-list slot j <- (key, id, count), or (j past the capacity: dropped) the id unlisted
+__device__ inline void hot_put(const Tables &T, uint32_t j, uint32_t id, uint32_t key, uint32_t count) {
+    if (j < T.hot_cap) {
+        T.hot[j] = hot_entry(key, id);
+        T.hcnt[j] = count;
+        T.hpos[id] = j;
+    } else {
+        T.hpos[id] = NO_ID;
+    }
+}
+// a listed id's count fell by d: its hot-list copy too
+__device__ inline void hot_sub(const Tables &T, uint32_t id, uint32_t d) {
+    const uint32_t j = T.hpos[id];
+    if (j != NO_ID) atomicSub(&T.hcnt[j], d);
+}
 __device__ inline void pair_new(const Tables &T, DevState *st, uint32_t key, uint32_t count) {
     uint32_t id = atomicAdd(&st->num_ids, 1u);
     if (id >= T.id_cap) { atomicOr(&st->error, 1u); return; }
@@ -150,14 +165,13 @@ __device__ inline void pair_new(const Tables &T, DevState *st, uint32_t key, uin
     ht_insert_new(T, key, id);
     atomicAdd(&st->live, 1);
     home_add(T, st, key, true);
-    if (count >= st->theta) {
-        uint32_t j = atomicAdd(&st->hot_len, 1u);
-        if (j < T.hot_cap) T.hot[j] = hot_entry(key, id);
-    }
+    if (count >= st->theta) hot_put(T, atomicAdd(&st->hot_len, 1u), id, key, count);
+    else T.hpos[id] = NO_ID;
 }
 __device__ inline void pair_dec(const Tables &T, DevState *st, uint32_t key, uint32_t d) {
     uint32_t id = ht_find(T, key);
     if (id == NO_ID) { atomicOr(&st->error, 4u); return; }
+    hot_sub(T, id, d);
     uint32_t old = atomicSub(&T.id_cnt[id], d);
     if (old < d) atomicOr(&st->error, 2u);
     if (old == d) {
@@ -2208,6 +2222,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
             const uint32_t top_id = ht_find(T, top_key);
             if (top_id == NO_ID) atomicOr(&st->error, 4u);
             else {
+                hot_sub(T, top_id, occ);
                 const uint32_t old = atomicSub(&T.id_cnt[top_id], occ);
                 if (old < occ) atomicOr(&st->error, 2u);
                 if (old == occ) { live_delta--; home_add(T, st, top_key, false); }
@@ -2270,9 +2285,9 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
         stamp(10);
         const uint32_t base = s_base, hbase = s_hbase;
         for (uint32_t j = tid; j < s_nhot; j += UPD_THREADS)
-            if (hbase + j < T.hot_cap && base + s_hot[j] < T.id_cap) {
+            if (base + s_hot[j] < T.id_cap) {
                 const uint32_t i = s_hot[j];
-                T.hot[hbase + j] = hot_entry(g == 1 ? pair_key(s_t[i], X) : pair_key(X, s_t[i]), base + i);
+                hot_put(T, hbase + j, base + i, g == 1 ? pair_key(s_t[i], X) : pair_key(X, s_t[i]), s_c[i]);
             }
     }
     int live_delta = 0;
@@ -2283,6 +2298,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
             const uint32_t id = ht_find(T, key);
             if (id == NO_ID) atomicOr(&st->error, 4u);
             else {
+                hot_sub(T, id, c);
                 const uint32_t old = atomicSub(&T.id_cnt[id], c);
                 if (old < c) atomicOr(&st->error, 2u);
                 if (old == c) { live_delta--; home_add(T, st, key, false); }
@@ -2294,6 +2310,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
             else {
                 T.id_key[id] = key;
                 T.id_cnt[id] = c;
+                if (c < theta) T.hpos[id] = NO_ID;  // (a listed one's slot was set by hot_put above)
                 home_add(T, st, key, true);
                 if (i == tid) ht_insert_loaded(T, key, id, pre);
                 else ht_insert_new(T, key, id);
@@ -2875,14 +2892,23 @@ __global__ void __launch_bounds__(256) zbpe_count_hist(Tables T, const DevState 
     for (int i = threadIdx.x; i < COUNT_BINS; i += 256)
         if (h[i]) atomicAdd(&hist[i], h[i]);
 }
+// before a rebuild: the ids of the current list unlisted (their hpos back to NO_ID)
+__global__ void __launch_bounds__(256) zbpe_hot_clear(Tables T, const DevState *st) {
+    const uint32_t n = min(st->hot_len, T.hot_cap);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const uint32_t id = (uint32_t)T.hot[i];
+        if (id < T.id_cap) T.hpos[id] = NO_ID;
+    }
+}
 __global__ void __launch_bounds__(256) zbpe_hot_build(Tables T, DevState *st) {
     const uint32_t n = min(st->num_ids, T.id_cap), theta = st->theta;
     const uint32_t stride = gridDim.x * 256;
     for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~63u); i0 < n; i0 += stride) {  // wave-uniform trip count
         const uint32_t i = i0 + (threadIdx.x & 63);
-        const bool take = i < n && T.id_cnt[i] >= theta;
+        const uint32_t c = i < n ? T.id_cnt[i] : 0u;
+        const bool take = i < n && c >= theta;
         const uint32_t j = wave_append(&st->hot_len, take);
-        if (take && j < T.hot_cap) T.hot[j] = hot_entry(T.id_key[i], i);
+        if (take) hot_put(T, j, i, T.id_key[i], c);
     }
 }
 // Fused select: argmax over the hot list, the final reduction by the last block to finish
@@ -3930,6 +3956,7 @@ __device__ inline MaxRec block_max(MaxRec r, MaxRec *sm) {
 // state, the hot list and its capacity, the role split (nref = the refresh workgroups), the argmax grid
 // and the stream's tail -- so those loads issue at entry, before any kernarg round trip.
 __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st, const unsigned long long *__restrict__ hot,
+                                                                 const uint32_t *__restrict__ hcnt,
                                                                  uint32_t hot_cap, uint32_t nref_arg, uint32_t sel_blocks,
                                                                  const uint16_t *__restrict__ tok, int64_t n, Tables T,
                                                                  MaxRec *__restrict__ partial, uint32_t *delta, uint32_t X,
@@ -3995,6 +4022,9 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     unsigned long long e0[SEL_U];
 #pragma unroll
     for (int u = 0; u < SEL_U; u++) e0[u] = i00 + u * G < hot_cap ? hot[i00 + u * G] : (unsigned long long)NO_ID;
+    uint32_t c0[SEL_U];  // their counts (Tables::hcnt), in the same round trip
+#pragma unroll
+    for (int u = 0; u < SEL_U; u++) c0[u] = i00 + u * G < hot_cap ? hcnt[i00 + u * G] : 0u;  // (a leading argument: preloaded)
     const bool lp_wave = bx == 0 && tid >= 64 && tid < 128 && N.world == 1;
     const uint32_t t_tail = lp_wave && n - 1 - (int64_t)(tid - 64) >= 0 ? tok[n - 1 - (int64_t)(tid - 64)] : HOLE;
     const StateHead H0 = load_head(st);
@@ -4042,7 +4072,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
             ks[u] = (uint32_t)(e >> 32);  // the key rides along: the block's keys at its max come from registers
         }
 #pragma unroll
-        for (int u = 0; u < SEL_U; u++) cs[u] = ids[u] != NO_ID ? T.id_cnt[ids[u]] : 0u;
+        for (int u = 0; u < SEL_U; u++) cs[u] = ids[u] != NO_ID ? c0[u] : 0u;
         if (lp_wave) {
             // wave 1 of block 0: the count of the stream's last pair (a tie needs it: Zig map capacity).
             // The pair id of the last lookup (state head) is checked and its count loaded with the hot
@@ -4091,7 +4121,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 ks[u] = (uint32_t)(e >> 32);  // the key rides along: the block's keys at its max come from registers
             }
 #pragma unroll
-            for (int u = 0; u < SEL_U; u++) cs[u] = ids[u] != NO_ID ? T.id_cnt[ids[u]] : 0u;
+            for (int u = 0; u < SEL_U; u++) cs[u] = ids[u] != NO_ID ? T.hcnt[i0 + u * G] : 0u;
 #pragma unroll
             for (int u = 0; u < SEL_U; u++)
                 if (cs[u] >= theta && cs[u]) r = max_combine(r, MaxRec{cs[u], 1u, ids[u]});
@@ -4112,8 +4142,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
             } else {
                 for (uint32_t i = bx * NEXT_THREADS + tid; i < nh; i += G) {
                     const unsigned long long e = T.hot[i];
-                    const uint32_t id = (uint32_t)e;
-                    if (T.id_cnt[id] == R.cnt) {
+                    if (T.hcnt[i] == R.cnt) {
                         const uint32_t j = atomicAdd(&s_nc, 1u);
                         if (j < NEXT_CAND) s_key[j] = (uint32_t)(e >> 32);
                     }
