@@ -14,7 +14,7 @@
 //                 member i is followed by first_j or preceded by second_j), and member j's key is the next
 //                 home slot among the leader's tied pairs.
 // Build: g++ -O3 -std=c++17 -pthread -o /tmp/batch_potential tools/batch_potential.cpp
-// Run:   /tmp/batch_potential corpus.bin vocab [K] [from_merge]
+// Run:   /tmp/batch_potential corpus.bin vocab [K] [from_merge] [tied_winners.txt]
 #include "../oracle/zig_fast.cpp"
 
 #include <map>
@@ -31,8 +31,11 @@ struct MergeInfo {
     std::map<uint32_t, uint32_t> left, right; // neighbour token histograms
 };
 std::vector<MergeInfo> g_info;
+uint32_t g_from = 0;  // merges before it are not recorded (their footprints would not fit in memory at C4)
 
 void hook(Trainer &t, uint32_t k, uint32_t win, uint32_t T, const std::vector<uint32_t> &tied) {
+    if (g_info.size() <= k) g_info.resize(k + 1);
+    if (k < g_from) return;
     MergeInfo m;
     m.key = t.pkey[win];
     m.T = T;
@@ -91,8 +94,16 @@ int main(int argc, char **argv) {
     const uint32_t vocab = atoi(argv[2]);
     const int K = argc > 3 ? atoi(argv[3]) : 4;
     const uint32_t from = argc > 4 ? atoi(argv[4]) : 0;
+    g_from = from;
     Log log;
     std::vector<Override> ov;
+    // optional: the tied merges' winners from a verified golden ("k key" lines), taken without a replay
+    if (argc > 5) {
+        FILE *o = fopen(argv[5], "r");
+        unsigned k, key;
+        while (o && fscanf(o, "%u %u", &k, &key) == 2) ov.push_back(Override{k, key});
+        if (o) fclose(o);
+    }
     Trainer t;
     t.text = text.data();
     t.n = n;
@@ -112,6 +123,7 @@ int main(int argc, char **argv) {
     t.out_distinct = dist.data();
     t.out_len_after = lens.data();
     t.pre_apply = hook;
+    t.no_replay = !ov.empty();
     if (t.run(nullptr) != 0) { fprintf(stderr, "oracle run failed\n"); return 2; }
     const uint32_t m = t.merges_done;
     for (int rule = 0; rule < 3; rule++) {  // 2: exact, but only rounds whose leader's tie set has exactly two pairs
