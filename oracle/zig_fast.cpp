@@ -449,6 +449,7 @@ struct Trainer {
     std::vector<uint8_t> pdirty;
     std::vector<uint32_t> dirty;
     std::vector<uint64_t> heap;   /* (count << 32 | id), max-heap, lazily invalidated */
+    bool no_replay = false; /* analysis tools: a forced winner (override) is taken without a replay */
     /* analysis hook (tools/batch_potential.cpp): called with the winner before each merge is applied */
     void (*pre_apply)(Trainer &, uint32_t k, uint32_t win_id, uint32_t T, const std::vector<uint32_t> &tied) = nullptr;
 
@@ -754,7 +755,9 @@ struct Trainer {
                 while (ov < overrides->size() && (*overrides)[ov].k < k) ov++;
                 bool forced = ov < overrides->size() && (*overrides)[ov].k == k;
                 uint32_t win_key;
-                if (D <= sync_limit || !pool) {
+                if (forced && no_replay) {  // (analysis tools only: decisions taken from a verified golden)
+                    win_key = (*overrides)[ov].key;
+                } else if (D <= sync_limit || !pool) {
                     double a0 = now();
                     std::shared_ptr<const Snap> sn = snapshot();
                     double a1 = now();

@@ -1118,8 +1118,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                 P[11] * us / np, P[14]);
         fprintf(stderr, "sel_prof: refresh workgroups: %llu, average duration %.2f us (start to its summaries stored)\n", P[16],
                 P[15] * us / std::max(1.0, (double)P[16]));
-        fprintf(stderr, "sel_prof: argmax block 0 (from its start): hot counts in %.2f us, block max %.2f us\n", P[17] * us / calls,
-                P[18] * us / calls);
+        fprintf(stderr, "sel_prof: argmax block 0 (from its start): hot counts in %.2f us, block max %.2f us; hot list %.0f ids on average\n",
+                P[17] * us / calls, P[18] * us / calls, P[19] / calls);
         static const char *bucket[3] = {"merges < 7936", "merges 7936-19743", "merges >= 19744"};
         for (int k = 0; k < 3; k++) {
             const unsigned long long *Q = h_st->pipe_prof[k];

@@ -4111,7 +4111,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
 #pragma unroll
         for (int u = 0; u < SEL_U; u++)
             if (cs[u] >= theta && cs[u]) r = max_combine(r, MaxRec{cs[u], 1u, ids[u]});
-        if (N.prof && bx == 0 && tid == 0) atomicAdd(&st->sel_prof[17], wall_clock64() - st->sel_t0);  // thread 0's counts in
+        if (N.prof && bx == 0 && tid == 0) {
+            atomicAdd(&st->sel_prof[17], wall_clock64() - st->sel_t0);  // thread 0's counts in
+            atomicAdd(&st->sel_prof[19], (unsigned long long)nh);        // the hot list's length
+        }
         const bool one_step = SEL_U * G >= nh;  // (every entry was in the first step)
         for (uint32_t i0 = i00 + SEL_U * G; i0 < nh; i0 += SEL_U * G) {
 #pragma unroll
