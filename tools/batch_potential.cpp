@@ -32,6 +32,21 @@ struct MergeInfo {
 };
 std::vector<MergeInfo> g_info;
 uint32_t g_from = 0;  // merges before it are not recorded (their footprints would not fit in memory at C4)
+bool g_stream = false;  // pair rule only: keep just the previous merge (no footprint history)
+
+// Pair rounds as the device can decide them (streaming, greedy): merge k-1 leads, merge k joins when k-1 was
+// tied and not self, k's key is the tied pair with the 2nd-smallest home (strictly between the 1st and 3rd),
+// k-1's new pairs stay below the top count, capacity is unchanged and no occurrence of k touches k-1's
+// footprint (the scan can test that exactly from two neighbours on each side).
+struct PairStats {
+    uint64_t leaders = 0, paired = 0, not_tied = 0, self = 0, not_second = 0, same_home = 0, new_top = 0, cap = 0,
+             touch = 0, wrong = 0, merges = 0;
+    std::map<uint32_t, uint64_t> by_band;  // merges paired per 4096-merge band
+} g_pair;
+MergeInfo g_prev;
+bool g_prev_valid = false, g_prev_member2 = false;
+
+void pair_rule(uint32_t k, const MergeInfo &m);
 
 void hook(Trainer &t, uint32_t k, uint32_t win, uint32_t T, const std::vector<uint32_t> &tied) {
     if (g_info.size() <= k) g_info.resize(k + 1);
@@ -65,6 +80,7 @@ void hook(Trainer &t, uint32_t k, uint32_t win, uint32_t T, const std::vector<ui
     }
     for (auto &x : m.left) m.max_new = std::max(m.max_new, x.second);
     for (auto &x : m.right) m.max_new = std::max(m.max_new, x.second);
+    if (g_stream) { pair_rule(k, m); g_prev = std::move(m); g_prev_valid = true; return; }
     if (g_info.size() <= k) g_info.resize(k + 1);
     g_info[k] = std::move(m);
 }
@@ -78,6 +94,27 @@ bool token_clash(const MergeInfo &i, const MergeInfo &j) {
     const uint32_t c = j.key & 0xFFFF, d = j.key >> 16;
     auto has = [](const std::map<uint32_t, uint32_t> &h, uint32_t t) { auto it = h.find(t); return it != h.end() && it->second; };
     return has(i.right, c) || has(i.left, d);
+}
+void pair_rule(uint32_t k, const MergeInfo &m) {
+    g_pair.merges++;
+    if (!g_prev_valid || g_prev_member2) { g_prev_member2 = false; g_pair.leaders++; return; }
+    const MergeInfo &l = g_prev;
+    auto fail = [&](uint64_t &c) { c++; g_pair.leaders++; g_prev_member2 = false; };
+    if (l.ties < 2) return fail(g_pair.not_tied);
+    if (l.self || m.self) return fail(g_pair.self);
+    if (l.tied_keys_by_home.size() < 2 || l.tied_keys_by_home[1] != m.key) {
+        // the device would predict tied_keys_by_home[1]; it is only wrong if the checks below pass
+        return fail(g_pair.not_second);
+    }
+    auto home = [&](uint32_t key) { return zig_hash(key) & (l.cap - 1); };
+    const auto &tk = l.tied_keys_by_home;
+    if (home(tk[0]) == home(tk[1]) || (tk.size() > 2 && home(tk[1]) == home(tk[2]))) return fail(g_pair.same_home);
+    if (l.max_new >= l.T || m.T != l.T) return fail(g_pair.new_top);
+    if (m.cap != l.cap) return fail(g_pair.cap);
+    if (touches(l, m)) return fail(g_pair.touch);
+    g_pair.paired++;
+    g_pair.by_band[k / 4096]++;
+    g_prev_member2 = true;
 }
 }  // namespace
 
@@ -95,6 +132,7 @@ int main(int argc, char **argv) {
     const int K = argc > 3 ? atoi(argv[3]) : 4;
     const uint32_t from = argc > 4 ? atoi(argv[4]) : 0;
     g_from = from;
+    g_stream = K == 2 && getenv("PAIR_STREAM");
     Log log;
     std::vector<Override> ov;
     // optional: the tied merges' winners from a verified golden ("k key" lines), taken without a replay
@@ -126,6 +164,19 @@ int main(int argc, char **argv) {
     t.no_replay = !ov.empty();
     if (t.run(nullptr) != 0) { fprintf(stderr, "oracle run failed\n"); return 2; }
     const uint32_t m = t.merges_done;
+    if (g_stream) {
+        const PairStats &P = g_pair;
+        printf("device pair rule, merges %u..%u: %llu merges in %llu rounds = %.3f merges/round\n", from, m,
+               (unsigned long long)(P.merges), (unsigned long long)P.leaders, (double)P.merges / P.leaders);
+        printf("  leader not paired because: not tied %llu, self %llu, next merge not the 2nd home %llu, equal homes %llu, "
+               "new pair at the top count %llu, capacity %llu, footprints touch %llu\n",
+               (unsigned long long)P.not_tied, (unsigned long long)P.self, (unsigned long long)P.not_second,
+               (unsigned long long)P.same_home, (unsigned long long)P.new_top, (unsigned long long)P.cap, (unsigned long long)P.touch);
+        printf("  paired merges per 4096-merge band:");
+        for (auto &x : P.by_band) printf(" %u:%llu", x.first * 4096, (unsigned long long)x.second);
+        printf("\n");
+        return 0;
+    }
     for (int rule = 0; rule < 3; rule++) {  // 2: exact, but only rounds whose leader's tie set has exactly two pairs
         uint64_t rounds = 0, merges = 0;
         std::map<int, uint64_t> sizes;

@@ -1120,6 +1120,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                 P[15] * us / std::max(1.0, (double)P[16]));
         fprintf(stderr, "sel_prof: argmax block 0 (from its start): hot counts in %.2f us, block max %.2f us; hot list %.0f ids on average\n",
                 P[17] * us / calls, P[18] * us / calls, P[19] / calls);
+        fprintf(stderr, "sel_prof: pair selects %llu, average %.2f us from the first argmax block's start to their commit\n", P[20],
+                P[21] * us / std::max(1.0, (double)P[20]));
         static const char *bucket[3] = {"merges < 7936", "merges 7936-19743", "merges >= 19744"};
         for (int k = 0; k < 3; k++) {
             const unsigned long long *Q = h_st->pipe_prof[k];
@@ -1138,6 +1140,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     stats.total_s = now_s() - t_start;
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
     stats.distinct_pairs = (uint64_t)std::max(h_st->live, 0);
+    stats.pair_selects = h_st->pr_hits;
     stats.pair_ids = h_st->num_ids;
     trained = true;
     if (out_stats) *out_stats = stats;
@@ -1256,7 +1259,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
                        dist() ? world : 1, (int)sel_prof, tie_trust ? nullptr : cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
-                       scan_plan && lists_on ? 1 : 0, tie_trust ? 1 : 0};
+                       scan_plan && lists_on ? 1 : 0, tie_trust ? 1 : 0, lp_lazy, pair_select};
             const uint32_t nref = C && !tie_trust ? (refresh_wgs ? std::min<uint32_t>(nsb, refresh_wgs) : nsb) : 0u;
             zbpe_select_next<<<sel + nref, NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hcnt, T.hot_cap, nref, sel,
                                                                                  d_tok[cur], slots, T, d_partial, left, X, N);

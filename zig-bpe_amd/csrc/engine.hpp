@@ -146,6 +146,8 @@ struct Engine {
     int list_grid = 0;          // scan grid after such a batch (option "list_grid"; 0 = the full grid)
     int list_mode = 1;          // 0: never build lists, 1: once pair counts are small against the stream
     uint32_t refresh_wgs = 256;   // option "refresh_wgs": home-refresh workgroups of zbpe_select_next (0: one per super-block)
+    int pair_select = 1;        // option "pair_select": a tied merge's decision qualifies the next merge's winner (DevState::pr_*)
+    int lp_lazy = 1;            // option "lp_lazy": the select looks the stream's last pair up only when a tie's capacity needs it
     int tie_trust = 0;          // option "tie_trust": TIMING EXPERIMENT ONLY -- ties taken by smallest home, unverified
     int dense_hist = 1;         // option "dense_hist": the full pair histogram of a byte stream counts every byte pair in a fixed 16-bit LDS bin
     uint32_t list_ratio = 96;   // training: list scan when list length * ratio < stream slots

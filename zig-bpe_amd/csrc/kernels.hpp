@@ -2200,7 +2200,10 @@ __host__ __device__ inline uint32_t update_per(uint32_t X) {
 __device__ inline void update_block(const Tables &T, DevState *st, const uint32_t *__restrict__ left,
                                     const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
                                     uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per,
-                                    const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta, int prof = 0) {
+                                    const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta, int prof = 0,
+                                    uint32_t top_count = 0, uint32_t pr_key = NO_ID) {
+    // pr_key != NO_ID: merge X+1 has a pair-select candidate (DevState::pr_key): count the new pairs, the
+    // tied pairs decremented (old count == top_count) and flag what rules the candidate out
     // option sel_prof: the latest stamp of each phase over the update blocks (st->pp_t[8..11])
     const auto stamp = [&](int k) {
         if (prof && threadIdx.x == 0) atomicMax(&st->pp_t[k], (unsigned long long)wall_clock64());
@@ -2216,6 +2219,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
         int live_delta = 0;
         const uint32_t xx = tail[0];
         if (tid == 0 && xx) pair_dec(T, st, pair_key(b, a), xx);
+        if (tid == 0 && xx && pr_key != NO_ID) atomicOr(&st->pr_dt, 1u << 18);
         if (tid == 1 && xx) pair_new(T, st, pair_key(X, X), xx);
         if (tid == 2) {
             const uint32_t occ = tail[1];
@@ -2279,6 +2283,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
             if (nh) hb = atomicAdd(&st->hot_len, nh);
             s_base = atomicAdd(&st->num_ids, n);
             atomicAdd(&st->live, (int)n);
+            if (pr_key != NO_ID) atomicAdd(&st->pr_births, n);
             s_hbase = hb;
         }
         __syncthreads();
@@ -2302,10 +2307,13 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 const uint32_t old = atomicSub(&T.id_cnt[id], c);
                 if (old < c) atomicOr(&st->error, 2u);
                 if (old == c) { live_delta--; home_add(T, st, key, false); }
+                // (a pair's first decrement sees its count before the merge: each tied pair counts once)
+                if (pr_key != NO_ID && old == top_count) atomicAdd(&st->pr_dt, key == pr_key ? 0x10001u : 1u);
             }
         } else {
             const uint32_t id = s_base + i;
             const uint32_t key = g == 1 ? pair_key(t, X) : pair_key(X, t);
+            if (pr_key != NO_ID && c >= top_count) atomicOr(&st->pr_dt, 1u << 17);
             if (id >= T.id_cap) atomicOr(&st->error, 1u);
             else {
                 T.id_key[id] = key;
@@ -2368,6 +2376,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     const uint32_t per = update_per(Xp);
     if (blockIdx.x >= apply_blocks) update_preload(left, left + Xp, Xp, blockIdx.x - apply_blocks, per, dv);
     const StateHead H = load_head(st);  // (with the deltas: one round trip)
+    const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key;  // (same round trip)
     const uint32_t theta = H.theta;
     if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the list scan's stamps
         const unsigned long long now = wall_clock64();
@@ -2435,7 +2444,8 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     }
     const uint32_t ublk = blockIdx.x - apply_blocks;
     if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) atomicOr(&st->error, 64u);  // occurrences != count
-    update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof);
+    update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof, H.top_count,
+                 R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID);
     if (R.prof) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
@@ -2940,10 +2950,12 @@ __device__ inline void roll_preload(const DevState *st, const uint32_t *delta, u
                         : lane == RI_HOT_LEN ? &st->hot_len : &st->lastpair_count;
     __builtin_amdgcn_global_load_lds(w, (__attribute__((address_space(3))) void *)s_pre, 4, 0, 0);
 }
+__device__ inline uint64_t dev_zig_cap_for(uint64_t D);
+__device__ inline bool dev_zig_at_max_load(uint64_t cap, uint64_t D);
 __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, const uint16_t *tok, int64_t n,
                                      uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world,
                                      uint32_t key_hint = NO_ID, uint32_t lastpair_hint = NO_ID, FinishOut *fo = nullptr,
-                                     const uint32_t *pre = nullptr, bool defer_key = false);
+                                     const uint32_t *pre = nullptr, bool defer_key = false, bool lazy_lp = false);
 __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState *st, MaxRec *__restrict__ partial,
                                                               const uint16_t *__restrict__ tok, int64_t n, uint32_t *delta,
                                                               uint32_t X, int roll, const Boundary *__restrict__ bnd, int world) {
@@ -2991,7 +3003,7 @@ __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_select(Tables T, DevState
 __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, const uint16_t *tok, int64_t n,
                                      uint32_t *delta, uint32_t X, int roll, const Boundary *bnd, int world,
                                      uint32_t key_hint, uint32_t lastpair_hint, FinishOut *fo, const uint32_t *pre,
-                                     bool defer_key) {
+                                     bool defer_key, bool lazy_lp) {
     {
         // every state word the roll reads, loaded together before the first store (the stores
         // below may alias them as far as the compiler knows, which would serialise each load), or
@@ -3021,7 +3033,9 @@ __device__ inline void select_finish(const Tables &T, DevState *st, MaxRec q, co
         if (top_key != NO_ID) st->top_key = top_key;
         if (q.ties > 1 && lastpair_hint != NO_ID) {
             st->lastpair_count = lastpair = lastpair_hint;
-        } else if (q.ties > 1) {
+        } else if (q.ties > 1 && !(lazy_lp && !dev_zig_at_max_load(dev_zig_cap_for((uint64_t)max(live, 0)), (uint64_t)max(live, 0)))) {
+            // (lazy_lp: only when the capacity depends on it -- D exactly at a max load; else the stale
+            // count gives the same capacity, here and in the host's resolve_tie, which reads the same D)
             uint32_t lt[2];  // last live token of the whole stream, then the one before
             int got = 0;
             if (world > 1) {
@@ -3103,11 +3117,17 @@ __device__ inline uint32_t home_at(const uint32_t *hc, uint32_t s) { return (hc[
 
 __device__ inline bool tie_skip(const DevState *st, int dyn) { return dyn && (st->halt || !st->tie_on); }
 // Zig map final capacity for D live pairs (zig_order.hpp zig_final_capacity, on the device)
+// Closed form, no loop and no division (a 64-bit division by 100 per doubling was ~1 us of one thread on
+// a tied merge's critical path): floor(cap * 80 / 100) >= D  <=>  4 cap >= 5 D, so cap is the smallest power
+// of two >= max(8, ceil(5 D / 4)); the max load equals D exactly iff 4 cap - 5 D < 5.
+__device__ inline uint64_t dev_zig_cap_for(uint64_t D) {
+    const uint64_t m = (5 * D + 3) / 4;
+    return m <= 8 ? 8ull : 1ull << (64 - __builtin_clzll(m - 1));
+}
+__device__ inline bool dev_zig_at_max_load(uint64_t cap, uint64_t D) { return 4 * cap - 5 * D < 5; }
 __device__ inline uint64_t dev_zig_final_capacity(uint64_t D, bool call_after) {
-    uint64_t cap = 8;
-    while (cap * 80 / 100 < D) cap *= 2;
-    if (cap * 80 / 100 == D && call_after) cap *= 2;
-    return cap;
+    const uint64_t cap = dev_zig_cap_for(D);
+    return call_after && dev_zig_at_max_load(cap, D) ? 2 * cap : cap;
 }
 // Batch mode, start of merge X: can the device run this merge by itself? Every block of the first
 // kernel of the merge evaluates the same predicate on the (read-only here) selection state; block 0
@@ -3751,6 +3771,62 @@ __device__ inline void plan_store(DevState *st, uint32_t x1, uint32_t key, uint3
     st->plan_key = key;
     st->plan_x = x1;
 }
+// Pair selects (DevState::pr_*): the three smallest entries of the tied-key list (home << 32 | key, unique)
+// and the largest home, by one wave
+__device__ inline void min3_insert(uint64_t &m1, uint64_t &m2, uint64_t &m3, uint64_t e) {
+    if (e < m1) { m3 = m2; m2 = m1; m1 = e; }
+    else if (e < m2) { m3 = m2; m2 = e; }
+    else if (e < m3) m3 = e;
+}
+__device__ inline void wave_min3(const uint64_t *list, uint32_t len, uint64_t &m1, uint64_t &m2, uint64_t &m3, uint32_t &hmax) {
+    const uint32_t lane = threadIdx.x & 63;
+    m1 = m2 = m3 = ~0ull;
+    hmax = 0;
+    for (uint32_t i = lane; i < len; i += 64) {
+        const uint64_t e = list[i];
+        min3_insert(m1, m2, m3, e);
+        hmax = max(hmax, (uint32_t)(e >> 32));
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t b1 = __shfl_xor(m1, off), b2 = __shfl_xor(m2, off), b3 = __shfl_xor(m3, off);
+        min3_insert(m1, m2, m3, b1);
+        min3_insert(m1, m2, m3, b2);
+        min3_insert(m1, m2, m3, b3);
+        hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
+    }
+}
+// keys whose home lies in the 4096-slot blocks covering [x, y) (0 <= x < y <= C, C >= one super-block):
+// block summaries for the partial super-blocks at the two ends, super-block summaries between (one wave,
+// one round trip; write-through loads). A summary's q is homes - slots.
+__device__ inline int64_t wave_homes_cover(const HomeView &V, uint32_t x, uint32_t y) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t bx = x / SUMM_SLOTS, by = (y - 1) / SUMM_SLOTS, sx = bx / SUPER_BLOCKS, sy = by / SUPER_BLOCKS;
+    int64_t h = 0;
+    if (sx == sy) {
+        const uint32_t b = bx + lane;
+        if (b <= by) h += (int64_t)ld_wt(V.summ + b).q + SUMM_SLOTS;
+    } else {
+        const uint32_t b1 = bx + lane, b2 = sy * SUPER_BLOCKS + lane;
+        if (b1 < (sx + 1) * SUPER_BLOCKS) h += (int64_t)ld_wt(V.summ + b1).q + SUMM_SLOTS;
+        if (b2 <= by) h += (int64_t)ld_wt(V.summ + b2).q + SUMM_SLOTS;
+        // the super-blocks between: up to 8 per lane with every load issued before the first use (a loop
+        // with a run-time trip count waited for each load in turn); past 512 of them (C > 2^27) a loop
+        constexpr int SB_U = 8;
+        Summ sv[SB_U];
+#pragma unroll
+        for (int j = 0; j < SB_U; j++) {
+            const uint32_t k = sx + 1 + lane + 64u * j;
+            sv[j] = k < sy ? ld_wt(V.sup + k) : Summ{-(SUMM_SLOTS * SUPER_BLOCKS), 0};
+        }
+#pragma unroll
+        for (int j = 0; j < SB_U; j++) h += (int64_t)sv[j].q + (int64_t)SUMM_SLOTS * SUPER_BLOCKS;
+        for (uint32_t k = sx + 1 + lane + 64u * SB_U; k < sy; k += 64) h += (int64_t)ld_wt(V.sup + k).q + (int64_t)SUMM_SLOTS * SUPER_BLOCKS;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) h += __shfl_xor(h, off);
+    return h;
+}
 __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uint64_t b2) {
     const uint64_t a1 = m1, a2 = m2;
     m1 = min(a1, b1);
@@ -3763,7 +3839,7 @@ template <int NT = DECIDE_THREADS>
 __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
-                                   uint32_t plan_gen = 0, bool trust = false) {
+                                   uint32_t plan_gen = 0, bool trust = false, uint32_t pair_x = 0) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
     // trust (option tie_trust, a TIMING EXPERIMENT only, never a default): the smallest home wins with no
     // cluster or wrap test -- what a decision costs without the home summaries
@@ -3811,6 +3887,27 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
         const int64_t lf = wave_last_free(V, ws, V.C, wave_carry_into(V, ws));
         if (lane == 0) s_last = lf;
     }
+    // pair_x (merge X+1 = pair_x, NT >= 512, precomputed carries): waves 4-7 bound the free slots that keep
+    // the second-smallest home's key first once this merge's new pairs are placed: F(h2, h3), the free slots
+    // between its home and the third-smallest home (its run ends before h3), and F(hmax, C), after the largest
+    // tied home (no tied key's run wraps). A range [x, y) has at least (y - x) - homes(x..y) - carry(x) free
+    // slots (the keys in it came from homes in it or were carried in), homes over-counted by whole blocks.
+    __shared__ int64_t s_pr[4];
+    __shared__ uint32_t s_pr_h3;
+    const bool pair_on = NT >= 512 && pair_x && cs && !trust && len >= 3 && V.C >= (uint32_t)(SUMM_SLOTS * SUPER_BLOCKS);
+    if (pair_on && w >= 4 && w < 8) {
+        uint64_t p1, p2, p3;
+        uint32_t hmx;
+        wave_min3(list, len, p1, p2, p3, hmx);
+        const uint32_t h2 = (uint32_t)(p2 >> 32), h3 = (uint32_t)(p3 >> 32);
+        int64_t r = 0;
+        if (w == 4) r = wave_carry_from_super(V, cs, h2);
+        else if (w == 5) r = h3 > h2 ? wave_homes_cover(V, h2, h3) : (int64_t)1 << 40;
+        else if (w == 6) r = wave_carry_from_super(V, cs, hmx);
+        else r = wave_homes_cover(V, hmx, V.C);
+        if (lane == 0) s_pr[w - 4] = r;
+        if (w == 5 && lane == 0) s_pr_h3 = h3;
+    }
     if (NT >= 256 && plan_on && w == 3 && len) {
         uint64_t m1 = ~0ull;
         for (uint32_t i = lane; i < len; i += 64) m1 = min(m1, list[i]);
@@ -3851,6 +3948,25 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
             st->cur_key = key;
             log[st->cur_x - 256] = MergeLog{key, st->top_count, (uint32_t)st->live_tokens, st->tie_count};
             if (NT >= 256 && plan_on && len) plan_store(st, st->cur_x, key, plan_gen, s_plan);
+            // merge X+1's pair-select candidate: the second-smallest home's key (not a self pair)
+            const uint32_t k2 = (uint32_t)m2;
+            if (NT >= 512 && pair_x && cs && !trust && m2 != ~0ull && (k2 & 0xFFFF) != (k2 >> 16) && total == len &&
+                (len == 2 || pair_on)) {
+                uint32_t slack = 0xFFFFFFFFu;  // two tied pairs: the candidate is the only one left
+                if (len >= 3) {  // (waves 4-7 reduced the same list: h2 = m2's home, h3, hmax)
+                    const uint32_t h2 = (uint32_t)(m2 >> 32);
+                    const int64_t f23 = (int64_t)s_pr_h3 - (int64_t)h2 - s_pr[1] - s_pr[0];
+                    const int64_t fe = (int64_t)V.C - (int64_t)hmax - s_pr[3] - s_pr[2];
+                    const int64_t f = min(f23, fe);
+                    slack = f <= 0 ? 0u : (uint32_t)min(f, (int64_t)0xFFFFFFFEll);
+                }
+                st->pr_births = 0;
+                st->pr_dt = 0;
+                st->pr_key = k2;
+                st->pr_ties = total;
+                st->pr_slack = slack;
+                st->pr_x = pair_x;
+            }
         }
     }
 }
@@ -3909,6 +4025,11 @@ struct NextArgs {
     uint32_t dir_w, gen;
     int plan;
     int trust;            // option tie_trust (timing experiment): no refresh workgroups, no cluster test
+    // option lp_lazy: the stream's last pair count (the Zig map's final grow) is looked up by the last block
+    // only for a tie whose capacity depends on it, not by argmax wave 1 at every merge (its dependent loads
+    // held the argmax block's max behind them)
+    int lp_lazy;
+    int pair;             // option pair_select (DevState::pr_*)
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -4025,9 +4146,17 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     uint32_t c0[SEL_U];  // their counts (Tables::hcnt), in the same round trip
 #pragma unroll
     for (int u = 0; u < SEL_U; u++) c0[u] = i00 + u * G < hot_cap ? hcnt[i00 + u * G] : 0u;  // (a leading argument: preloaded)
-    const bool lp_wave = bx == 0 && tid >= 64 && tid < 128 && N.world == 1;
+    const bool lp_wave = bx == 0 && tid >= 64 && tid < 128 && N.world == 1 && !N.lp_lazy;
     const uint32_t t_tail = lp_wave && n - 1 - (int64_t)(tid - 64) >= 0 ? tok[n - 1 - (int64_t)(tid - 64)] : HOLE;
     const StateHead H0 = load_head(st);
+    // pair select: merge X+1's candidate from merge X's tie decision and what merge X's replace counted (in
+    // the head's round trip)
+    PairHead P0{};
+    int32_t live0 = 0;
+    if (N.pair) {
+        P0 = *reinterpret_cast<const PairHead *>(&st->pr_x);
+        live0 = st->live;
+    }
     if (H0.halt) return;
     __shared__ MaxRec sm[NEXT_THREADS / WAVE];
     __shared__ uint32_t s_flag, s_nc, s_h, s_tie, s_len, s_ntb, s_ovf;
@@ -4049,6 +4178,58 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 st->pp_t[k] = 0;
             }
             st->pp_t[5] = st->pp_t[6] = 0;
+        }
+    }
+    // ---- pair select: merge X+1 is the candidate that merge X's decision named, with no argmax and no
+    // decision, when (a) merge X's replace decremented neither it nor made adjacent occurrences (it still
+    // has the top count T; every other count only fell), (b) no new pair reached T (the tied set is the old
+    // one minus merge X, minus the tied pairs merge X decremented), (c) the new pairs are fewer than the
+    // free slots the decision counted (the candidate's run still ends before the next tied home, and no
+    // tied run wraps: it is the first tied key in slot order) and (d) the Zig capacity is the same and not
+    // at a max load (the stream's last pair is not needed). Then the Zig order is the one the decision saw.
+    if (N.pair && P0.x == N.B.X && N.B.X < N.x_end) {
+        const uint32_t dT = P0.dt & 0xFFFFu, kc = P0.key;
+        const uint64_t D1 = (uint64_t)max(live0, 0);
+        const bool light = (P0.dt >> 16) == 0 && P0.births < P0.slack && dT + 1 < P0.ties && N.V.C &&
+                           dev_zig_cap_for(D1) == N.V.C && !dev_zig_at_max_load(N.V.C, D1) && (kc & 0xFFFF) != (kc >> 16);
+        if (light) {
+            if (bx != 0) return;
+            __shared__ uint32_t s_lh, s_lplan[6];
+            const PlanCtx lplan{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, X, H0.arena_top, H0.rec_count};
+            const bool lplan_on = N.plan && T.lst_off && H0.lists_valid;
+            if (lplan_on && tid == 64) plan_compute(lplan, kc, s_lplan);
+            // the next launch's refresh counts (as the full path's last block)
+            if (tid < 9) st_wt(N.rtk + ((X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // roll_preload's LDS words (wave 0) landed
+            __syncthreads();
+            if (tid == 0) {
+                st_wt(&st->ref_noprefix, X);  // no decision here: the last refresh workgroup may skip the carries
+                const MaxRec Q{H0.top_count, P0.ties - 1u - dT, 0u};
+                FinishOut fo;
+                select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, kc, NO_ID, &fo, s_pre, false, true);
+                bool tie;
+                const uint32_t h = merge_begin_eval_v(T, fo, N.B, &tie);
+                if (!h && tie) {  // (the decision's commit, with its winner)
+                    st->cur_x = N.B.X;
+                    st->tie_on = 0;
+                    st->cur_key = kc;
+                    N.B.log[N.B.X - 256] = MergeLog{kc, fo.top_count, (uint32_t)fo.live_tokens, fo.tie_count};
+                } else {
+                    merge_begin_commit_v(st, N.B, h, tie, fo);
+                }
+                st->pr_x = 0;
+                st->pr_hits = P0.hits + 1;
+                s_lh = h;
+            }
+            __syncthreads();
+            if (lplan_on && tid == 64 && !s_lh) plan_store(st, N.B.X, kc, N.gen, s_lplan);
+            if (N.prof && tid == 0) {
+                const unsigned long long now = wall_clock64();
+                st->pp_t[7] = now;
+                atomicAdd(&st->sel_prof[20], 1ull);
+                atomicAdd(&st->sel_prof[21], now - st->sel_t0);
+            }
+            return;
         }
     }
     // one argmax workgroup (a short hot list): it is the last one by construction -- no ticket, no
@@ -4183,7 +4364,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     // ---- the last block: argmax, roll of merge X -------------------------------------------------
     // the stream's last pair count (block 0 stored it write-through): in flight with the partials
-    const uint32_t lastpair_wt = tid == 0 && N.world == 1 ? (single ? s_lastpair : ld_wt(N.lastpair)) : NO_ID;
+    const uint32_t lastpair_wt = tid == 0 && N.world == 1 && !N.lp_lazy ? (single ? s_lastpair : ld_wt(N.lastpair)) : NO_ID;
     MaxRec Q = R;
     if (single) {  // (s_nc, s_key from the argmax above; the barrier after it published them)
         if (tid == 0) {
@@ -4226,7 +4407,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     if (tid == 0) {
         FinishOut fo;
         select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, Q.ties == 1 && Q.cnt ? s_key[0] : NO_ID,
-                      lastpair_wt, &fo, s_pre, Q.ties > 1);
+                      lastpair_wt, &fo, s_pre, Q.ties > 1, N.lp_lazy != 0);
         s_h = HALT_DONE;
         s_tie = 0;
         if (N.B.X < N.x_end) {
@@ -4386,7 +4567,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
-                              plan_on, plan, N.gen, N.trust != 0);
+                              plan_on, plan, N.gen, N.trust != 0, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }

@@ -83,7 +83,7 @@ struct DevState {
     unsigned long long sel_t0, sel_ta, sel_tr;  // start; latest argmax / refresh block finish
     // [0..4] last-block phases, [5] argmax blocks done, [7] last-block calls, [8] tie decisions, [9] their carries,
     // [10] refresh wait, [12] latest refresh block done (at decisions, [13] samples), [6]/[11] prefix start/end ([14] samples)
-    unsigned long long sel_prof[20];  // [15]/[16]: summed refresh-workgroup durations / their count; [17]/[18] argmax: counts in / block max (last argmax block)
+    unsigned long long sel_prof[24];  // [15]/[16]: summed refresh-workgroup durations / their count; [17]/[18] argmax: counts in / block max (last argmax block); [20]/[21] pair selects / their time
     unsigned long long sel_prof_pq, sel_prof_pp;  // refresh_prefix start / end stamps of the current launch
     // option sel_prof, whole merge pipeline (batch mode): probe stamps of the current launches and the
     // sums they fold into (Engine::train prints them): scan (list form) LDS clear / walk / flush done and
@@ -93,7 +93,20 @@ struct DevState {
     // zbpe_select_next of merge X whose merge X+1 is not tied (its last argmax block stores X): the
     // last refresh workgroup skips the decision's carries (zeroed with the state at each train)
     uint32_t ref_noprefix;
+    // Pair selects (option pair_select, zbpe_select_next): the tie decision of merge X names the tied key of
+    // the second-smallest home as merge X+1's candidate (pr_key, pr_x = X+1) with a lower bound on the free
+    // Zig-map slots that keep it first (pr_slack); merge X's replace counts its new pairs (pr_births) and, in
+    // pr_dt, the tied pairs it decremented (low 16 bits) with flags above them (bit 16 the candidate was
+    // decremented, bit 17 a new pair reached the top count, bit 18 adjacent occurrences); the select of merge
+    // X then starts merge X+1 with the candidate and no argmax or decision when every condition holds
+    // (pr_hits counts those). One 32-B group, loaded in one round trip (PairHead).
+    alignas(32) uint32_t pr_x;
+    uint32_t pr_key, pr_slack, pr_ties, pr_births, pr_dt, pr_hits, pr_pad;
 };
+struct PairHead {
+    uint32_t x, key, slack, ties, births, dt, hits, pad;
+};
+static_assert(sizeof(PairHead) == 32, "pair head: 8 words");
 // DevState's hot header as one value (StateHead load_head(st))
 struct StateHead {
     uint32_t halt, cur_key, arena_top, lists_valid, lists_x, top_count, theta, hot_len, rec_count;

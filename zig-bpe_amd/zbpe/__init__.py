@@ -140,6 +140,7 @@ class Stats(ctypes.Structure):
         ("sharded_merges", ctypes.c_uint64),
         ("tie_crosschecks", ctypes.c_uint64),
         ("generate_tokens_s", ctypes.c_double),
+        ("pair_selects", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
