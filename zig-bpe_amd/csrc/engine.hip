@@ -1229,11 +1229,14 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 2], stream));
         CHECK(comm_sum(left, 2ull * X + 2));
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 3], stream));
+        const int pair_blk = fused_select && pair_select && !tie_trust && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS ? 1 : 0;
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
-                      1, dist() ? d_halo : nullptr, 1, (int)sel_prof};
+                      1, dist() ? d_halo : nullptr, 1, (int)sel_prof, pair_blk, d_summ, d_sup, (uint32_t)C, nb, nsb, cs,
+                      A.dir_row, A.dir, A.dir_w, layout_gen, scan_plan && lists_on ? 1 : 0};
         if (!replace_split) {
-            zbpe_replace<<<ab + update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
-        } else {  // profiling: apply and count update as two launches
+            zbpe_replace<<<ab + update_blocks(X, update_per(X)) + pair_blk, 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
+        } else {  // profiling: apply and count update as two launches (no pair-select bound)
+            R.pair_blk = 0;
             zbpe_replace<<<ab, 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
             R.apply_blocks = 0;
             zbpe_replace<<<update_blocks(X, update_per(X)), 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
@@ -1259,7 +1262,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
                        dist() ? world : 1, (int)sel_prof, tie_trust ? nullptr : cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
-                       scan_plan && lists_on ? 1 : 0, tie_trust ? 1 : 0, lp_lazy, pair_select};
+                       scan_plan && lists_on ? 1 : 0, tie_trust ? 1 : 0, lp_lazy, pair_select, pair_refresh ? 0 : 1, pair_m3w};
             const uint32_t nref = C && !tie_trust ? (refresh_wgs ? std::min<uint32_t>(nsb, refresh_wgs) : nsb) : 0u;
             zbpe_select_next<<<sel + nref, NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hcnt, T.hot_cap, nref, sel,
                                                                                  d_tok[cur], slots, T, d_partial, left, X, N);

@@ -2353,7 +2353,20 @@ struct ReplaceArgs {
     const Halo *dhalo;
     int rec_arena;      // records at rec + st->arena_top (ScanArgs::rec_arena)
     int prof;           // option sel_prof: probe stamps (st->pp_t)
+    // pair selects: the last workgroup of the grid computes merge X+1's candidate bound (pair_slack_block)
+    int pair_blk;
+    const Summ *summ, *sup;  // the home view of the decision (HomeView: summ, sup, C, nb, nsb)
+    uint32_t C, nb, nsb;
+    const uint32_t *cs;
+    const uint32_t *dir_row, *dir;  // the candidate's scan plan (ScanArgs::dir_row, dir, dir_w)
+    uint32_t dir_w, gen;
+    int plan;
 };
+// pair selects: merge X+1's candidate bound, by the replace's extra workgroup (defined with the home views below)
+__device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Summ *sup, uint32_t C, uint32_t nb,
+                                        uint32_t nsb, const uint32_t *cs, uint32_t X, const uint32_t *lst_off,
+                                        const uint32_t *lst_len, const uint32_t *dir_row, const uint32_t *dir,
+                                        uint32_t dir_w, uint32_t lists_x, bool plan_on, uint32_t gen);
 // this thread's deltas of an update block, loaded before anything that waits on the state (they do
 // not depend on the merged pair: group and range follow from the block index)
 __device__ inline void update_preload(const uint32_t *left, const uint32_t *right, uint32_t X, uint32_t ublk, uint32_t per,
@@ -2394,6 +2407,11 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     }
     if (R.dyn) {
         if (H.halt) return;
+        if (R.pair_blk && blockIdx.x == gridDim.x - 1) {
+            pair_slack_block(st, R.summ, R.sup, R.C, R.nb, R.nsb, R.cs, R.X, T.lst_off, T.lst_len, R.dir_row, R.dir, R.dir_w,
+                             H.lists_x, R.plan && T.lst_off && H.lists_valid, R.gen);
+            return;
+        }
         R.top_key = H.cur_key;
         R.a = R.top_key & 0xFFFF;
         R.b = R.top_key >> 16;
@@ -3772,11 +3790,13 @@ __device__ inline void plan_store(DevState *st, uint32_t x1, uint32_t key, uint3
     st->plan_x = x1;
 }
 // Pair selects (DevState::pr_*): the three smallest entries of the tied-key list (home << 32 | key, unique)
-// and the largest home, by one wave
-__device__ inline void min3_insert(uint64_t &m1, uint64_t &m2, uint64_t &m3, uint64_t e) {
-    if (e < m1) { m3 = m2; m2 = m1; m1 = e; }
-    else if (e < m2) { m3 = m2; m2 = e; }
-    else if (e < m3) m3 = e;
+// and the largest home, by one wave. Branch-free: the three smallest of two sorted triples a, b are
+// min(a1, b1), min(max(a1, b1), a2, b2) and min(a3, b3, max(a2, b1), max(a1, b2)) (an if-chain per insert
+// diverged across the lanes and cost ~3 us on the decision's critical path)
+__device__ inline void min3_merge(uint64_t &a1, uint64_t &a2, uint64_t &a3, uint64_t b1, uint64_t b2, uint64_t b3) {
+    const uint64_t r1 = min(a1, b1), r2 = min(max(a1, b1), min(a2, b2));
+    const uint64_t r3 = min(min(a3, b3), min(max(a2, b1), max(a1, b2)));
+    a1 = r1; a2 = r2; a3 = r3;
 }
 __device__ inline void wave_min3(const uint64_t *list, uint32_t len, uint64_t &m1, uint64_t &m2, uint64_t &m3, uint32_t &hmax) {
     const uint32_t lane = threadIdx.x & 63;
@@ -3784,15 +3804,13 @@ __device__ inline void wave_min3(const uint64_t *list, uint32_t len, uint64_t &m
     hmax = 0;
     for (uint32_t i = lane; i < len; i += 64) {
         const uint64_t e = list[i];
-        min3_insert(m1, m2, m3, e);
+        min3_merge(m1, m2, m3, e, ~0ull, ~0ull);
         hmax = max(hmax, (uint32_t)(e >> 32));
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         const uint64_t b1 = __shfl_xor(m1, off), b2 = __shfl_xor(m2, off), b3 = __shfl_xor(m3, off);
-        min3_insert(m1, m2, m3, b1);
-        min3_insert(m1, m2, m3, b2);
-        min3_insert(m1, m2, m3, b3);
+        min3_merge(m1, m2, m3, b1, b2, b3);
         hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
     }
 }
@@ -3827,6 +3845,53 @@ __device__ inline int64_t wave_homes_cover(const HomeView &V, uint32_t x, uint32
     for (int off = 32; off >= 1; off >>= 1) h += __shfl_xor(h, off);
     return h;
 }
+// Pair selects: the bound on the free Zig-map slots that keep merge X+1's candidate first, by one extra
+// workgroup of merge X's replace, from the home summaries the decision saw (only the selects refresh them;
+// the home counts this replace changes are not read). A range [x, y) has at least (y - x) - homes - carry(x)
+// free slots (its keys came from homes in it or were carried in). The ranges start at the block after the
+// candidate's home (free slots there end its run before the third-smallest home h3) and after the largest
+// tied home's block (a free slot there: no tied key's run wraps past slot C-1). Four waves: the carry into
+// each range (the super-block carry cs composed with the block summaries before it) and its homes.
+__device__ inline int32_t wave_carry_block(const HomeView &V, const uint32_t *cs, uint32_t b) {
+    const uint32_t lane = threadIdx.x & 63, sb = b / SUPER_BLOCKS, bi = sb * SUPER_BLOCKS + lane;
+    const Summ bs = bi < b ? ld_wt(V.summ + bi) : Summ{0, 0};
+    const int32_t c_in = (int32_t)ld_wt(cs + sb);
+    const Summ x = wave_reduce_summ(bs);
+    return max(x.m, c_in + x.q);
+}
+__device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Summ *sup, uint32_t C, uint32_t nb,
+                                        uint32_t nsb, const uint32_t *cs, uint32_t X, const uint32_t *lst_off,
+                                        const uint32_t *lst_len, const uint32_t *dir_row, const uint32_t *dir,
+                                        uint32_t dir_w, uint32_t lists_x, bool plan_on, uint32_t gen) {
+    const HomeView V{nullptr, summ, sup, C, nb, nsb};
+    __shared__ int64_t s_r[4];
+    const uint32_t px = st->pr_x, slack = st->pr_slack, h2 = st->pr_h2, h3 = st->pr_h3, hmax = st->pr_hmax, key = st->pr_key;
+    if (px != X + 1) return;
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the candidate's scan plan (its tokens existed before merge X: their lists are the ones the scan of
+    // merge X+1 finds, unless the layout generation changes), by one lane beside the bound
+    if (plan_on && threadIdx.x == 64) {
+        const PlanCtx plan{lst_off, lst_len, dir_row, dir, dir_w, lists_x, NO_ID, 0u, 0u};
+        uint32_t pl[6];
+        plan_compute(plan, key, pl);
+        for (int k = 0; k < 6; k++) st->pr_plan[k] = pl[k];
+        st->pr_plan_gen = gen;
+    }
+    if (slack != 0 || !cs || V.C < (uint32_t)(SUMM_SLOTS * SUPER_BLOCKS)) return;
+    const uint32_t x23 = (h2 / SUMM_SLOTS + 1) * SUMM_SLOTS, xe = (hmax / SUMM_SLOTS + 1) * SUMM_SLOTS;
+    int64_t r = 0;
+    if (w == 0) r = x23 < h3 ? wave_carry_block(V, cs, x23 / SUMM_SLOTS) : 0;
+    else if (w == 1) r = x23 < h3 ? wave_homes_cover(V, x23, h3) : 0;
+    else if (w == 2) r = xe < V.C ? wave_carry_block(V, cs, xe / SUMM_SLOTS) : 0;
+    else if (w == 3) r = xe < V.C ? wave_homes_cover(V, xe, V.C) : 0;
+    if (lane == 0 && w < 4) s_r[w] = r;
+    __syncthreads();
+    if (threadIdx.x) return;
+    const int64_t f23 = x23 < h3 ? (int64_t)h3 - x23 - s_r[1] - s_r[0] : 0;
+    const int64_t fe = xe < V.C ? (int64_t)V.C - xe - s_r[3] - s_r[2] : 0;
+    const int64_t f = min(f23, fe);
+    st->pr_slack = f <= 0 ? 0u : (uint32_t)min(f, (int64_t)0xFFFFFFFEll);
+}
 __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uint64_t b2) {
     const uint64_t a1 = m1, a2 = m2;
     m1 = min(a1, b1);
@@ -3839,7 +3904,7 @@ template <int NT = DECIDE_THREADS>
 __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
-                                   uint32_t plan_gen = 0, bool trust = false, uint32_t pair_x = 0) {
+                                   uint32_t plan_gen = 0, bool trust = false, uint32_t pair_x = 0, bool m3_w4 = false) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
     // trust (option tie_trust, a TIMING EXPERIMENT only, never a default): the smallest home wins with no
     // cluster or wrap test -- what a decision costs without the home summaries
@@ -3856,20 +3921,26 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
     const int w = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t ws = V.C > 4096 ? V.C - 4096 : 0;
+    __shared__ uint64_t s_m3;
     if (w == 0) {
-        uint64_t m1 = ~0ull, m2 = ~0ull;
+        uint64_t m1 = ~0ull, m2 = ~0ull, m3 = ~0ull;
         uint32_t hmax = 0;
-        for (uint32_t i = lane; i < len; i += 64) {
-            const uint64_t e = list[i];
-            if (e < m1) { m2 = m1; m1 = e; } else if (e < m2) m2 = e;
-            hmax = max(hmax, (uint32_t)(e >> 32));
-        }
+        if (NT >= 512 && pair_x && !m3_w4) {
+            wave_min3(list, len, m1, m2, m3, hmax);
+        } else {
+            for (uint32_t i = lane; i < len; i += 64) {
+                const uint64_t e = list[i];
+                if (e < m1) { m2 = m1; m1 = e; } else if (e < m2) m2 = e;
+                hmax = max(hmax, (uint32_t)(e >> 32));
+            }
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const uint64_t b1 = __shfl_xor(m1, off), b2 = __shfl_xor(m2, off);
-            min2_combine(m1, m2, b1, b2);
-            hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
+            for (int off = 32; off >= 1; off >>= 1) {
+                const uint64_t b1 = __shfl_xor(m1, off), b2 = __shfl_xor(m2, off);
+                min2_combine(m1, m2, b1, b2);
+                hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
+            }
         }
+        if (lane == 0 && !(NT >= 512 && pair_x && m3_w4)) s_m3 = m3;
         const uint32_t h1 = (uint32_t)(m1 >> 32);
         const int64_t f = !len ? -1 : trust ? (int64_t)V.C : cs ? wave_first_free(V, h1, wave_carry_from_super(V, cs, h1)) : wave_free_from(V, h1);
         if (lane == 0) { s_free = f; s_m1 = m1; s_m2 = m2; s_hmax = hmax; }
@@ -3887,26 +3958,15 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
         const int64_t lf = wave_last_free(V, ws, V.C, wave_carry_into(V, ws));
         if (lane == 0) s_last = lf;
     }
-    // pair_x (merge X+1 = pair_x, NT >= 512, precomputed carries): waves 4-7 bound the free slots that keep
-    // the second-smallest home's key first once this merge's new pairs are placed: F(h2, h3), the free slots
-    // between its home and the third-smallest home (its run ends before h3), and F(hmax, C), after the largest
-    // tied home (no tied key's run wraps). A range [x, y) has at least (y - x) - homes(x..y) - carry(x) free
-    // slots (the keys in it came from homes in it or were carried in), homes over-counted by whole blocks.
-    __shared__ int64_t s_pr[4];
-    __shared__ uint32_t s_pr_h3;
-    const bool pair_on = NT >= 512 && pair_x && cs && !trust && len >= 3 && V.C >= (uint32_t)(SUMM_SLOTS * SUPER_BLOCKS);
-    if (pair_on && w >= 4 && w < 8) {
+    // pair_x (merge X+1 = pair_x, NT >= 512, precomputed carries): the second-smallest home's key is merge
+    // X+1's candidate; wave 0 also finds the third-smallest home (merge X's replace bounds the free slots
+    // between them and loads the candidate's scan plan: pair_slack_block)
+    const bool pair_on = NT >= 512 && pair_x && cs && !trust && len >= 2;
+    if (NT >= 512 && pair_x && m3_w4 && w == 4) {  // (option pair_m3w: the third-smallest by a wave of its own)
         uint64_t p1, p2, p3;
         uint32_t hmx;
         wave_min3(list, len, p1, p2, p3, hmx);
-        const uint32_t h2 = (uint32_t)(p2 >> 32), h3 = (uint32_t)(p3 >> 32);
-        int64_t r = 0;
-        if (w == 4) r = wave_carry_from_super(V, cs, h2);
-        else if (w == 5) r = h3 > h2 ? wave_homes_cover(V, h2, h3) : (int64_t)1 << 40;
-        else if (w == 6) r = wave_carry_from_super(V, cs, hmx);
-        else r = wave_homes_cover(V, hmx, V.C);
-        if (lane == 0) s_pr[w - 4] = r;
-        if (w == 5 && lane == 0) s_pr_h3 = h3;
+        if (lane == 0) s_m3 = p3;
     }
     if (NT >= 256 && plan_on && w == 3 && len) {
         uint64_t m1 = ~0ull;
@@ -3950,21 +4010,19 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
             if (NT >= 256 && plan_on && len) plan_store(st, st->cur_x, key, plan_gen, s_plan);
             // merge X+1's pair-select candidate: the second-smallest home's key (not a self pair)
             const uint32_t k2 = (uint32_t)m2;
-            if (NT >= 512 && pair_x && cs && !trust && m2 != ~0ull && (k2 & 0xFFFF) != (k2 >> 16) && total == len &&
-                (len == 2 || pair_on)) {
-                uint32_t slack = 0xFFFFFFFFu;  // two tied pairs: the candidate is the only one left
-                if (len >= 3) {  // (waves 4-7 reduced the same list: h2 = m2's home, h3, hmax)
-                    const uint32_t h2 = (uint32_t)(m2 >> 32);
-                    const int64_t f23 = (int64_t)s_pr_h3 - (int64_t)h2 - s_pr[1] - s_pr[0];
-                    const int64_t fe = (int64_t)V.C - (int64_t)hmax - s_pr[3] - s_pr[2];
-                    const int64_t f = min(f23, fe);
-                    slack = f <= 0 ? 0u : (uint32_t)min(f, (int64_t)0xFFFFFFFEll);
-                }
+            if (pair_on && m2 != ~0ull && (k2 & 0xFFFF) != (k2 >> 16) && total == len &&
+                (len == 2 || V.C >= (uint32_t)(SUMM_SLOTS * SUPER_BLOCKS))) {
+                // two tied pairs: the candidate is the only one left (no bound needed); else 0 until merge
+                // X's replace has bounded the free slots (pair_slack_block)
+                st->pr_slack = len == 2 ? 0xFFFFFFFFu : 0u;
+                st->pr_h2 = (uint32_t)(m2 >> 32);
+                st->pr_h3 = len >= 3 ? (uint32_t)(s_m3 >> 32) : 0u;
+                st->pr_hmax = hmax;
+                st->pr_plan_gen = 0xFFFFFFFFu;  // (the replace's extra workgroup loads the plan)
                 st->pr_births = 0;
                 st->pr_dt = 0;
                 st->pr_key = k2;
                 st->pr_ties = total;
-                st->pr_slack = slack;
                 st->pr_x = pair_x;
             }
         }
@@ -4030,6 +4088,8 @@ struct NextArgs {
     // held the argmax block's max behind them)
     int lp_lazy;
     int pair;             // option pair_select (DevState::pr_*)
+    int skip_refresh;     // option pair_refresh 0: a pair select's refresh workgroups leave the dirty blocks to the next launch
+    int m3_w4;            // option pair_m3w: the decision's third-smallest home by wave 4 (else wave 0)
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -4038,6 +4098,16 @@ struct NextArgs {
 // bypass its CU's L1, so no acquire either (MI355X_MICROARCH.md, valid hand-off forms: one lane of
 // each storing workgroup adds to one counter after the workgroup's vmcnt(0) and barrier; the
 // workgroup whose add came last loads after its add has returned, its other waves after a barrier)
+// pair selects: does this launch start merge X+1 with the candidate (the conditions at the light path in
+// zbpe_select_next)? Both roles evaluate it on the same words: the refresh workgroups then leave the dirty
+// home blocks to the next launch, whose decision reads them
+__device__ inline bool pair_light(const NextArgs &N, const PairHead &P0, int32_t live0) {
+    if (!N.pair || P0.x != N.B.X || N.B.X >= N.x_end) return false;
+    const uint32_t dT = P0.dt & 0xFFFFu, kc = P0.key;
+    const uint64_t D1 = (uint64_t)max(live0, 0);
+    return (P0.dt >> 16) == 0 && P0.births < P0.slack && dT + 1 < P0.ties && N.V.C && dev_zig_cap_for(D1) == N.V.C &&
+           !dev_zig_at_max_load(N.V.C, D1) && (kc & 0xFFFF) != (kc >> 16);
+}
 __device__ inline bool block_ticket_last(uint32_t *ticket, uint32_t nblocks, uint32_t *s_flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -4102,6 +4172,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // critical path: the argmax grid is sized by the hot list alone; nothing in this launch reads
         // [0, 2X) -- the roll reads the tail words past it)
         for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
+        if (N.pair && N.skip_refresh) {  // a pair select: no decision in this launch reads the summaries
+            const PairHead P0 = *reinterpret_cast<const PairHead *>(&st->pr_x);
+            if (pair_light(N, P0, st->live)) return;
+        }
         // nref may be below the super-block count (option refresh_wgs): a smaller grid ends sooner -- a kernel
         // boundary after 256 workgroups costs ~3.7 us, after 64 ~1.6 (tools/launch_lat.hip, boundary rows)
         for (uint32_t sb = blockIdx.x; sb < N.V.nsb; sb += nref) {
@@ -4187,17 +4261,21 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     // free slots the decision counted (the candidate's run still ends before the next tied home, and no
     // tied run wraps: it is the first tied key in slot order) and (d) the Zig capacity is the same and not
     // at a max load (the stream's last pair is not needed). Then the Zig order is the one the decision saw.
-    if (N.pair && P0.x == N.B.X && N.B.X < N.x_end) {
+    if (pair_light(N, P0, live0)) {
         const uint32_t dT = P0.dt & 0xFFFFu, kc = P0.key;
-        const uint64_t D1 = (uint64_t)max(live0, 0);
-        const bool light = (P0.dt >> 16) == 0 && P0.births < P0.slack && dT + 1 < P0.ties && N.V.C &&
-                           dev_zig_cap_for(D1) == N.V.C && !dev_zig_at_max_load(N.V.C, D1) && (kc & 0xFFFF) != (kc >> 16);
-        if (light) {
+        {
             if (bx != 0) return;
             __shared__ uint32_t s_lh, s_lplan[6];
             const PlanCtx lplan{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, X, H0.arena_top, H0.rec_count};
             const bool lplan_on = N.plan && T.lst_off && H0.lists_valid;
-            if (lplan_on && tid == 64) plan_compute(lplan, kc, s_lplan);
+            // the candidate's plan, loaded by the decision (its lists have not changed since: the candidate
+            // existed before merge X, whose token's list is the only new one), else loaded here
+            if (lplan_on && tid == 64) {
+                if (P0.plan_gen == N.gen)
+                    for (int k = 0; k < 6; k++) s_lplan[k] = P0.plan[k];
+                else
+                    plan_compute(lplan, kc, s_lplan);
+            }
             // the next launch's refresh counts (as the full path's last block)
             if (tid < 9) st_wt(N.rtk + ((X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // roll_preload's LDS words (wave 0) landed
@@ -4567,7 +4645,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
-                              plan_on, plan, N.gen, N.trust != 0, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u);
+                              plan_on, plan, N.gen, N.trust != 0, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u, N.m3_w4 != 0);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }

@@ -94,19 +94,23 @@ struct DevState {
     // last refresh workgroup skips the decision's carries (zeroed with the state at each train)
     uint32_t ref_noprefix;
     // Pair selects (option pair_select, zbpe_select_next): the tie decision of merge X names the tied key of
-    // the second-smallest home as merge X+1's candidate (pr_key, pr_x = X+1) with a lower bound on the free
-    // Zig-map slots that keep it first (pr_slack); merge X's replace counts its new pairs (pr_births) and, in
+    // the second-smallest home as merge X+1's candidate (pr_key, pr_x = X+1); merge X's replace computes a
+    // lower bound on the free Zig-map slots that keep it first (pr_slack), counts its new pairs (pr_births) and, in
     // pr_dt, the tied pairs it decremented (low 16 bits) with flags above them (bit 16 the candidate was
     // decremented, bit 17 a new pair reached the top count, bit 18 adjacent occurrences); the select of merge
     // X then starts merge X+1 with the candidate and no argmax or decision when every condition holds
-    // (pr_hits counts those). One 32-B group, loaded in one round trip (PairHead).
-    alignas(32) uint32_t pr_x;
-    uint32_t pr_key, pr_slack, pr_ties, pr_births, pr_dt, pr_hits, pr_pad;
+    // (pr_hits counts those). One 64-B group, loaded in one round trip (PairHead),
+    // and the candidate's scan plan (valid for layout generation pr_plan_gen; by the replace's extra workgroup)
+    alignas(64) uint32_t pr_x;
+    uint32_t pr_key, pr_slack, pr_ties, pr_births, pr_dt, pr_hits, pr_plan_gen;
+    uint32_t pr_plan[6], pr_pad[2];
+    uint32_t pr_h2, pr_h3, pr_hmax;  // the decision's tied homes the replace bounds the free slots with
 };
 struct PairHead {
-    uint32_t x, key, slack, ties, births, dt, hits, pad;
+    uint32_t x, key, slack, ties, births, dt, hits, plan_gen;
+    uint32_t plan[6], pad[2];
 };
-static_assert(sizeof(PairHead) == 32, "pair head: 8 words");
+static_assert(sizeof(PairHead) == 64, "pair head: 16 words");
 // DevState's hot header as one value (StateHead load_head(st))
 struct StateHead {
     uint32_t halt, cur_key, arena_top, lists_valid, lists_x, top_count, theta, hot_len, rec_count;
