@@ -2201,7 +2201,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                                     const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
                                     uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per,
                                     const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta, int prof = 0,
-                                    uint32_t top_count = 0, uint32_t pr_key = NO_ID) {
+                                    uint32_t top_count = 0, uint32_t pr_key = NO_ID, uint32_t pr_key2 = NO_ID) {
     // pr_key != NO_ID: merge X+1 has a pair-select candidate (DevState::pr_key): count the new pairs, the
     // tied pairs decremented (old count == top_count) and flag what rules the candidate out
     // option sel_prof: the latest stamp of each phase over the update blocks (st->pp_t[8..11])
@@ -2308,7 +2308,8 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 if (old < c) atomicOr(&st->error, 2u);
                 if (old == c) { live_delta--; home_add(T, st, key, false); }
                 // (a pair's first decrement sees its count before the merge: each tied pair counts once)
-                if (pr_key != NO_ID && old == top_count) atomicAdd(&st->pr_dt, key == pr_key ? 0x10001u : 1u);
+                if (pr_key != NO_ID && old == top_count)
+                    atomicAdd(&st->pr_dt, key == pr_key ? 0x10001u : key == pr_key2 ? 0x80001u : 1u);
             }
         } else {
             const uint32_t id = s_base + i;
@@ -2389,7 +2390,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     const uint32_t per = update_per(Xp);
     if (blockIdx.x >= apply_blocks) update_preload(left, left + Xp, Xp, blockIdx.x - apply_blocks, per, dv);
     const StateHead H = load_head(st);  // (with the deltas: one round trip)
-    const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key;  // (same round trip)
+    const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key, pr_key2 = st->pr_key2;  // (same round trip)
     const uint32_t theta = H.theta;
     if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the list scan's stamps
         const unsigned long long now = wall_clock64();
@@ -2463,7 +2464,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     const uint32_t ublk = blockIdx.x - apply_blocks;
     if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) atomicOr(&st->error, 64u);  // occurrences != count
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof, H.top_count,
-                 R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID);
+                 R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2);
     if (R.prof) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
@@ -3798,6 +3799,31 @@ __device__ inline void min3_merge(uint64_t &a1, uint64_t &a2, uint64_t &a3, uint
     const uint64_t r3 = min(min(a3, b3), min(max(a2, b1), max(a1, b2)));
     a1 = r1; a2 = r2; a3 = r3;
 }
+// the four smallest of two sorted quadruples: r_k = min over i of max(a_i, b_{k-i}) (a_0 = b_0 = -inf)
+__device__ inline void min4_merge(uint64_t (&a)[4], const uint64_t (&b)[4]) {
+    const uint64_t r1 = min(a[0], b[0]);
+    const uint64_t r2 = min(min(a[1], b[1]), max(a[0], b[0]));
+    const uint64_t r3 = min(min(a[2], b[2]), min(max(a[1], b[0]), max(a[0], b[1])));
+    const uint64_t r4 = min(min(a[3], b[3]), min(min(max(a[2], b[0]), max(a[0], b[2])), max(a[1], b[1])));
+    a[0] = r1; a[1] = r2; a[2] = r3; a[3] = r4;
+}
+__device__ inline void wave_min4(const uint64_t *list, uint32_t len, uint64_t (&m)[4], uint32_t &hmax) {
+    const uint32_t lane = threadIdx.x & 63;
+    m[0] = m[1] = m[2] = m[3] = ~0ull;
+    hmax = 0;
+    for (uint32_t i = lane; i < len; i += 64) {
+        const uint64_t e = list[i];
+        const uint64_t b[4] = {e, ~0ull, ~0ull, ~0ull};
+        min4_merge(m, b);
+        hmax = max(hmax, (uint32_t)(e >> 32));
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t b[4] = {__shfl_xor(m[0], off), __shfl_xor(m[1], off), __shfl_xor(m[2], off), __shfl_xor(m[3], off)};
+        min4_merge(m, b);
+        hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
+    }
+}
 __device__ inline void wave_min3(const uint64_t *list, uint32_t len, uint64_t &m1, uint64_t &m2, uint64_t &m3, uint32_t &hmax) {
     const uint32_t lane = threadIdx.x & 63;
     m1 = m2 = m3 = ~0ull;
@@ -3904,7 +3930,8 @@ template <int NT = DECIDE_THREADS>
 __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
-                                   uint32_t plan_gen = 0, bool trust = false, uint32_t pair_x = 0, bool m3_w4 = false) {
+                                   uint32_t plan_gen = 0, bool trust = false, uint32_t pair_x = 0, bool m3_w4 = false,
+                                   bool chain = false) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
     // trust (option tie_trust, a TIMING EXPERIMENT only, never a default): the smallest home wins with no
     // cluster or wrap test -- what a decision costs without the home summaries
@@ -3921,7 +3948,7 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
     const int w = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t ws = V.C > 4096 ? V.C - 4096 : 0;
-    __shared__ uint64_t s_m3;
+    __shared__ uint64_t s_m3, s_m4;
     if (w == 0) {
         uint64_t m1 = ~0ull, m2 = ~0ull, m3 = ~0ull;
         uint32_t hmax = 0;
@@ -3940,7 +3967,7 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
                 hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
             }
         }
-        if (lane == 0 && !(NT >= 512 && pair_x && m3_w4)) s_m3 = m3;
+        if (lane == 0 && !(NT >= 512 && pair_x && m3_w4)) { s_m3 = m3; s_m4 = ~0ull; }
         const uint32_t h1 = (uint32_t)(m1 >> 32);
         const int64_t f = !len ? -1 : trust ? (int64_t)V.C : cs ? wave_first_free(V, h1, wave_carry_from_super(V, cs, h1)) : wave_free_from(V, h1);
         if (lane == 0) { s_free = f; s_m1 = m1; s_m2 = m2; s_hmax = hmax; }
@@ -3962,11 +3989,11 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
     // X+1's candidate; wave 0 also finds the third-smallest home (merge X's replace bounds the free slots
     // between them and loads the candidate's scan plan: pair_slack_block)
     const bool pair_on = NT >= 512 && pair_x && cs && !trust && len >= 2;
-    if (NT >= 512 && pair_x && m3_w4 && w == 4) {  // (option pair_m3w: the third-smallest by a wave of its own)
-        uint64_t p1, p2, p3;
+    if (NT >= 512 && pair_x && m3_w4 && w == 4) {  // (option pair_m3w: the third- and fourth-smallest by a wave of its own)
+        uint64_t q[4];
         uint32_t hmx;
-        wave_min3(list, len, p1, p2, p3, hmx);
-        if (lane == 0) s_m3 = p3;
+        wave_min4(list, len, q, hmx);
+        if (lane == 0) { s_m3 = q[2]; s_m4 = q[3]; }
     }
     if (NT >= 256 && plan_on && w == 3 && len) {
         uint64_t m1 = ~0ull;
@@ -4017,7 +4044,13 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
                 st->pr_slack = len == 2 ? 0xFFFFFFFFu : 0u;
                 st->pr_h2 = (uint32_t)(m2 >> 32);
                 st->pr_h3 = len >= 3 ? (uint32_t)(s_m3 >> 32) : 0u;
+                st->pr_h4 = len >= 4 && s_m4 != ~0ull ? (uint32_t)(s_m4 >> 32) : 0u;
                 st->pr_hmax = hmax;
+                // chain: the third-smallest home's key for merge X+2 (found with the fourth, wave 4)
+                const uint32_t k3 = (uint32_t)s_m3;
+                st->pr_key2 = chain && m3_w4 && len >= 3 && s_m3 != ~0ull && (k3 & 0xFFFF) != (k3 >> 16) &&
+                                      (len == 3 || s_m4 != ~0ull)
+                                  ? k3 : NO_ID;
                 st->pr_plan_gen = 0xFFFFFFFFu;  // (the replace's extra workgroup loads the plan)
                 st->pr_births = 0;
                 st->pr_dt = 0;
@@ -4090,6 +4123,7 @@ struct NextArgs {
     int pair;             // option pair_select (DevState::pr_*)
     int skip_refresh;     // option pair_refresh 0: a pair select's refresh workgroups leave the dirty blocks to the next launch
     int m3_w4;            // option pair_m3w: the decision's third-smallest home by wave 4 (else wave 0)
+    int chain;            // option pair_chain: a pair select names merge X+2's candidate (needs skip_refresh, m3_w4)
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -4105,7 +4139,7 @@ __device__ inline bool pair_light(const NextArgs &N, const PairHead &P0, int32_t
     if (!N.pair || P0.x != N.B.X || N.B.X >= N.x_end) return false;
     const uint32_t dT = P0.dt & 0xFFFFu, kc = P0.key;
     const uint64_t D1 = (uint64_t)max(live0, 0);
-    return (P0.dt >> 16) == 0 && P0.births < P0.slack && dT + 1 < P0.ties && N.V.C && dev_zig_cap_for(D1) == N.V.C &&
+    return ((P0.dt >> 16) & 7u) == 0 && P0.births < P0.slack && dT + 1 < P0.ties && N.V.C && dev_zig_cap_for(D1) == N.V.C &&
            !dev_zig_at_max_load(N.V.C, D1) && (kc & 0xFFFF) != (kc >> 16);
 }
 __device__ inline bool block_ticket_last(uint32_t *ticket, uint32_t nblocks, uint32_t *s_flag) {
@@ -4295,7 +4329,23 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 } else {
                     merge_begin_commit_v(st, N.B, h, tie, fo);
                 }
-                st->pr_x = 0;
+                // chain: merge X+2's candidate is the next tied key by home, once this pair select is committed;
+                // its bound (the free slots between its home and the next, and after the largest, against the
+                // new pairs of both merges) and plan come from merge X+1's replace, whose home summaries are
+                // still the decision's (this launch refreshed none)
+                if (!h && N.skip_refresh && P0.key2 != NO_ID && N.B.X + 1 < N.x_end) {
+                    st->pr_key = P0.key2;
+                    st->pr_key2 = NO_ID;
+                    st->pr_ties = P0.ties - 1u;
+                    st->pr_dt = (P0.dt & 0xFFFFu) | (((P0.dt >> 19) & 1u) << 16);
+                    st->pr_h2 = P0.h3;
+                    st->pr_h3 = P0.h4;
+                    st->pr_slack = P0.ties == 3u ? 0xFFFFFFFFu : 0u;  // (the third was the last tied key)
+                    st->pr_plan_gen = 0xFFFFFFFFu;
+                    st->pr_x = N.B.X + 1;
+                } else {
+                    st->pr_x = 0;
+                }
                 st->pr_hits = P0.hits + 1;
                 s_lh = h;
             }
@@ -4645,7 +4695,8 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
-                              plan_on, plan, N.gen, N.trust != 0, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u, N.m3_w4 != 0);
+                              plan_on, plan, N.gen, N.trust != 0, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u, N.m3_w4 != 0,
+                              N.skip_refresh != 0 && N.chain != 0);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }

@@ -99,18 +99,25 @@ struct DevState {
     // pr_dt, the tied pairs it decremented (low 16 bits) with flags above them (bit 16 the candidate was
     // decremented, bit 17 a new pair reached the top count, bit 18 adjacent occurrences); the select of merge
     // X then starts merge X+1 with the candidate and no argmax or decision when every condition holds
-    // (pr_hits counts those). One 64-B group, loaded in one round trip (PairHead),
+    // (pr_hits counts those). One 128-B group, loaded in one round trip (PairHead),
     // and the candidate's scan plan (valid for layout generation pr_plan_gen; by the replace's extra workgroup)
-    alignas(64) uint32_t pr_x;
+    alignas(128) uint32_t pr_x;
     uint32_t pr_key, pr_slack, pr_ties, pr_births, pr_dt, pr_hits, pr_plan_gen;
-    uint32_t pr_plan[6], pr_pad[2];
-    uint32_t pr_h2, pr_h3, pr_hmax;  // the decision's tied homes the replace bounds the free slots with
+    uint32_t pr_plan[6];
+    // chains (option pair_refresh 0): the third-smallest home's key, candidate of merge X+2 once merge X+1 was a
+    // pair select (bit 19 of pr_dt: decremented); the tied homes the replace bounds the free slots with: the
+    // candidate's and the next one's (pr_h2, pr_h3), the one after (pr_h4) and the largest (pr_hmax)
+    uint32_t pr_key2, pr_pad1;
+    uint32_t pr_h2, pr_h3, pr_h4, pr_hmax;
+    uint32_t pr_pad2[12];
 };
 struct PairHead {
     uint32_t x, key, slack, ties, births, dt, hits, plan_gen;
-    uint32_t plan[6], pad[2];
+    uint32_t plan[6], key2, pad1;
+    uint32_t h2, h3, h4, hmax;
+    uint32_t pad2[12];
 };
-static_assert(sizeof(PairHead) == 64, "pair head: 16 words");
+static_assert(sizeof(PairHead) == 128, "pair head: 32 words");
 // DevState's hot header as one value (StateHead load_head(st))
 struct StateHead {
     uint32_t halt, cur_key, arena_top, lists_valid, lists_x, top_count, theta, hot_len, rec_count;
