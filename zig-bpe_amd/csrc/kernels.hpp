@@ -13,6 +13,9 @@
 
 #include "types.hpp"
 
+#ifndef ZBPE_PAIR_MIN4
+#define ZBPE_PAIR_MIN4 1  // decide_body: the pair-select chain's fourth-smallest home (0: min3 only, no chains past two)
+#endif
 #ifndef ZBPE_LP_CACHE
 #define ZBPE_LP_CACHE 1  // zbpe_select_next: the stream's last pair id cached in the state head (0: looked up every merge)
 #endif
@@ -3843,7 +3846,7 @@ __device__ inline void wave_min3(const uint64_t *list, uint32_t len, uint64_t &m
 // keys whose home lies in the 4096-slot blocks covering [x, y) (0 <= x < y <= C, C >= one super-block):
 // block summaries for the partial super-blocks at the two ends, super-block summaries between (one wave,
 // one round trip; write-through loads). A summary's q is homes - slots.
-__device__ inline int64_t wave_homes_cover(const HomeView &V, uint32_t x, uint32_t y) {
+__device__ __attribute__((always_inline)) inline int64_t wave_homes_cover(const HomeView &V, uint32_t x, uint32_t y) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t bx = x / SUMM_SLOTS, by = (y - 1) / SUMM_SLOTS, sx = bx / SUPER_BLOCKS, sy = by / SUPER_BLOCKS;
     int64_t h = 0;
@@ -3878,7 +3881,7 @@ __device__ inline int64_t wave_homes_cover(const HomeView &V, uint32_t x, uint32
 // candidate's home (free slots there end its run before the third-smallest home h3) and after the largest
 // tied home's block (a free slot there: no tied key's run wraps past slot C-1). Four waves: the carry into
 // each range (the super-block carry cs composed with the block summaries before it) and its homes.
-__device__ inline int32_t wave_carry_block(const HomeView &V, const uint32_t *cs, uint32_t b) {
+__device__ __attribute__((always_inline)) inline int32_t wave_carry_block(const HomeView &V, const uint32_t *cs, uint32_t b) {
     const uint32_t lane = threadIdx.x & 63, sb = b / SUPER_BLOCKS, bi = sb * SUPER_BLOCKS + lane;
     const Summ bs = bi < b ? ld_wt(V.summ + bi) : Summ{0, 0};
     const int32_t c_in = (int32_t)ld_wt(cs + sb);
@@ -3927,7 +3930,7 @@ __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uin
 // shortfall decides nothing). NT threads (>= 192: three waves compute carries). dyn: batch mode
 // (halt / commit).
 template <int NT = DECIDE_THREADS>
-__device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
+__device__ __attribute__((always_inline)) inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
                                    uint32_t plan_gen = 0, bool trust = false, uint32_t pair_x = 0, bool m3_w4 = false,
@@ -3990,10 +3993,17 @@ __device__ inline void decide_body(DevState *st, const uint64_t *list, uint32_t 
     // between them and loads the candidate's scan plan: pair_slack_block)
     const bool pair_on = NT >= 512 && pair_x && cs && !trust && len >= 2;
     if (NT >= 512 && pair_x && m3_w4 && w == 4) {  // (option pair_m3w: the third- and fourth-smallest by a wave of its own)
+#if ZBPE_PAIR_MIN4
         uint64_t q[4];
         uint32_t hmx;
         wave_min4(list, len, q, hmx);
         if (lane == 0) { s_m3 = q[2]; s_m4 = q[3]; }
+#else
+        uint64_t p1, p2, p3;
+        uint32_t hmx;
+        wave_min3(list, len, p1, p2, p3, hmx);
+        if (lane == 0) { s_m3 = p3; s_m4 = ~0ull; }
+#endif
     }
     if (NT >= 256 && plan_on && w == 3 && len) {
         uint64_t m1 = ~0ull;
@@ -4135,12 +4145,13 @@ struct NextArgs {
 // pair selects: does this launch start merge X+1 with the candidate (the conditions at the light path in
 // zbpe_select_next)? Both roles evaluate it on the same words: the refresh workgroups then leave the dirty
 // home blocks to the next launch, whose decision reads them
-__device__ inline bool pair_light(const NextArgs &N, const PairHead &P0, int32_t live0) {
-    if (!N.pair || P0.x != N.B.X || N.B.X >= N.x_end) return false;
+// (scalar arguments: a reference to the kernel's NextArgs made the compiler copy all of it to scratch at entry)
+__device__ inline bool pair_light(int pair, uint32_t x1, uint32_t x_end, uint32_t C, const PairHead &P0, int32_t live0) {
+    if (!pair || P0.x != x1 || x1 >= x_end) return false;
     const uint32_t dT = P0.dt & 0xFFFFu, kc = P0.key;
     const uint64_t D1 = (uint64_t)max(live0, 0);
-    return ((P0.dt >> 16) & 7u) == 0 && P0.births < P0.slack && dT + 1 < P0.ties && N.V.C && dev_zig_cap_for(D1) == N.V.C &&
-           !dev_zig_at_max_load(N.V.C, D1) && (kc & 0xFFFF) != (kc >> 16);
+    return ((P0.dt >> 16) & 7u) == 0 && P0.births < P0.slack && dT + 1 < P0.ties && C && dev_zig_cap_for(D1) == C &&
+           !dev_zig_at_max_load(C, D1) && (kc & 0xFFFF) != (kc >> 16);
 }
 __device__ inline bool block_ticket_last(uint32_t *ticket, uint32_t nblocks, uint32_t *s_flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -4168,7 +4179,7 @@ __device__ inline bool block_ticket_last_x(uint32_t *ctr, uint32_t nblocks, uint
     __syncthreads();
     return *s_flag != 0;
 }
-__device__ inline MaxRec block_max(MaxRec r, MaxRec *sm) {
+__device__ __attribute__((always_inline)) inline MaxRec block_max(MaxRec r, MaxRec *sm) {
     r = wave_max(r);
     if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = r;
     __syncthreads();
@@ -4208,7 +4219,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
         if (N.pair && N.skip_refresh) {  // a pair select: no decision in this launch reads the summaries
             const PairHead P0 = *reinterpret_cast<const PairHead *>(&st->pr_x);
-            if (pair_light(N, P0, st->live)) return;
+            if (pair_light(N.pair, N.B.X, N.x_end, N.V.C, P0, st->live)) return;
         }
         // nref may be below the super-block count (option refresh_wgs): a smaller grid ends sooner -- a kernel
         // boundary after 256 workgroups costs ~3.7 us, after 64 ~1.6 (tools/launch_lat.hip, boundary rows)
@@ -4295,77 +4306,22 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     // free slots the decision counted (the candidate's run still ends before the next tied home, and no
     // tied run wraps: it is the first tied key in slot order) and (d) the Zig capacity is the same and not
     // at a max load (the stream's last pair is not needed). Then the Zig order is the one the decision saw.
-    if (pair_light(N, P0, live0)) {
-        const uint32_t dT = P0.dt & 0xFFFFu, kc = P0.key;
-        {
-            if (bx != 0) return;
-            __shared__ uint32_t s_lh, s_lplan[6];
-            const PlanCtx lplan{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, X, H0.arena_top, H0.rec_count};
-            const bool lplan_on = N.plan && T.lst_off && H0.lists_valid;
-            // the candidate's plan, loaded by the decision (its lists have not changed since: the candidate
-            // existed before merge X, whose token's list is the only new one), else loaded here
-            if (lplan_on && tid == 64) {
-                if (P0.plan_gen == N.gen)
-                    for (int k = 0; k < 6; k++) s_lplan[k] = P0.plan[k];
-                else
-                    plan_compute(lplan, kc, s_lplan);
-            }
-            // the next launch's refresh counts (as the full path's last block)
-            if (tid < 9) st_wt(N.rtk + ((X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // roll_preload's LDS words (wave 0) landed
-            __syncthreads();
-            if (tid == 0) {
-                st_wt(&st->ref_noprefix, X);  // no decision here: the last refresh workgroup may skip the carries
-                const MaxRec Q{H0.top_count, P0.ties - 1u - dT, 0u};
-                FinishOut fo;
-                select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, kc, NO_ID, &fo, s_pre, false, true);
-                bool tie;
-                const uint32_t h = merge_begin_eval_v(T, fo, N.B, &tie);
-                if (!h && tie) {  // (the decision's commit, with its winner)
-                    st->cur_x = N.B.X;
-                    st->tie_on = 0;
-                    st->cur_key = kc;
-                    N.B.log[N.B.X - 256] = MergeLog{kc, fo.top_count, (uint32_t)fo.live_tokens, fo.tie_count};
-                } else {
-                    merge_begin_commit_v(st, N.B, h, tie, fo);
-                }
-                // chain: merge X+2's candidate is the next tied key by home, once this pair select is committed;
-                // its bound (the free slots between its home and the next, and after the largest, against the
-                // new pairs of both merges) and plan come from merge X+1's replace, whose home summaries are
-                // still the decision's (this launch refreshed none)
-                if (!h && N.skip_refresh && P0.key2 != NO_ID && N.B.X + 1 < N.x_end) {
-                    st->pr_key = P0.key2;
-                    st->pr_key2 = NO_ID;
-                    st->pr_ties = P0.ties - 1u;
-                    st->pr_dt = (P0.dt & 0xFFFFu) | (((P0.dt >> 19) & 1u) << 16);
-                    st->pr_h2 = P0.h3;
-                    st->pr_h3 = P0.h4;
-                    st->pr_slack = P0.ties == 3u ? 0xFFFFFFFFu : 0u;  // (the third was the last tied key)
-                    st->pr_plan_gen = 0xFFFFFFFFu;
-                    st->pr_x = N.B.X + 1;
-                } else {
-                    st->pr_x = 0;
-                }
-                st->pr_hits = P0.hits + 1;
-                s_lh = h;
-            }
-            __syncthreads();
-            if (lplan_on && tid == 64 && !s_lh) plan_store(st, N.B.X, kc, N.gen, s_lplan);
-            if (N.prof && tid == 0) {
-                const unsigned long long now = wall_clock64();
-                st->pp_t[7] = now;
-                atomicAdd(&st->sel_prof[20], 1ull);
-                atomicAdd(&st->sel_prof[21], now - st->sel_t0);
-            }
-            return;
-        }
+    // (one roll and begin below serve both: a second inlined copy of them pushed the kernel into spills)
+    const bool light = pair_light(N.pair, N.B.X, N.x_end, N.V.C, P0, live0);
+    if (light && bx != 0) return;
+    // the candidate's words wait in LDS (kept in registers across the argmax and decision code, they pushed
+    // the kernel's scalar registers into spills)
+    __shared__ uint32_t s_p0[5];
+    enum { P0_KEY, P0_TIES, P0_DT, P0_HITS, P0_PGEN };
+    if (light && tid == 0) {
+        s_p0[P0_KEY] = P0.key; s_p0[P0_TIES] = P0.ties; s_p0[P0_DT] = P0.dt; s_p0[P0_HITS] = P0.hits; s_p0[P0_PGEN] = P0.plan_gen;
     }
     // one argmax workgroup (a short hot list): it is the last one by construction -- no ticket, no
     // partials through global memory
-    const bool single = sel_blocks == 1;
+    const bool single = sel_blocks == 1 || light;
     __shared__ uint32_t s_lastpair;
     MaxRec R{0, 0, NO_ID};
-    {
+    if (!light) {
         if (!nref)  // (no refresh workgroups: the argmax ones clear the deltas)
             for (uint32_t t = bx * NEXT_THREADS + tid; t < 2 * X; t += G) delta[t] = 0;
         const uint32_t nh = min(H0.hot_len, T.hot_cap), theta = H0.theta;
@@ -4479,7 +4435,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     // the next launch's refresh count (the launch before this one used it and has ended)
     if (tid < 9) st_wt(N.rtk + ((X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
     unsigned long long pt = 0;
-    if (N.prof && tid == 0) {
+    if (N.prof && tid == 0 && !light) {
         pt = st->sel_t0;
         const unsigned long long ta = __hip_atomic_load(&st->sel_ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long tr = __hip_atomic_load(&st->sel_tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -4492,9 +4448,14 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     // ---- the last block: argmax, roll of merge X -------------------------------------------------
     // the stream's last pair count (block 0 stored it write-through): in flight with the partials
-    const uint32_t lastpair_wt = tid == 0 && N.world == 1 && !N.lp_lazy ? (single ? s_lastpair : ld_wt(N.lastpair)) : NO_ID;
+    const uint32_t lastpair_wt = tid == 0 && N.world == 1 && !N.lp_lazy && !light ? (single ? s_lastpair : ld_wt(N.lastpair)) : NO_ID;
     MaxRec Q = R;
-    if (single) {  // (s_nc, s_key from the argmax above; the barrier after it published them)
+    if (light) {  // the candidate: the top count, the tied set less merge X and the tied pairs merge X decremented
+        if (tid == 0) s_key[0] = s_p0[P0_KEY];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // roll_preload's LDS words (wave 0) landed
+        __syncthreads();
+        Q = MaxRec{H0.top_count, s_p0[P0_TIES] - 1u - (s_p0[P0_DT] & 0xFFFFu), 0u};
+    } else if (single) {  // (s_nc, s_key from the argmax above; the barrier after it published them)
         if (tid == 0) {
             s_pc[0] = R.cnt;
             s_pt[0] = R.cnt ? s_nc : 0u;
@@ -4513,7 +4474,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
         Q = block_max(q, sm);  // (its barriers also publish s_pc / s_pt)
     }
-    if (Q.ties == 1 && Q.cnt) {  // the unique max: its block kept its key
+    if (!light && Q.ties == 1 && Q.cnt) {  // the unique max: its block kept its key
         for (uint32_t b = tid; b < sel_blocks; b += NEXT_THREADS)
             if (s_pc[b] == Q.cnt) s_key[0] = s_pk[b];
     }
@@ -4522,7 +4483,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     // next LDS read wait for it), and stored by it at the launch's end
     constexpr uint32_t KEY_TID = NEXT_THREADS - 64;
     __shared__ uint32_t s_qkey;
-    if (tid == KEY_TID && Q.cnt && Q.ties > 1)
+    if (tid == KEY_TID && Q.cnt && Q.ties > 1 && !light)
         __builtin_amdgcn_global_load_lds(&T.id_key[Q.id], (__attribute__((address_space(3))) void *)&s_qkey, 4, 0, 0);
     __syncthreads();
     // the next merge's scan plan: its list loads (one lane of wave 1) overlap the roll and begin below;
@@ -4530,18 +4491,59 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     __shared__ uint32_t s_plan[6];
     const PlanCtx plan{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, X, H0.arena_top, H0.rec_count};  // (X's list: the roll's lst_off / lst_len, from the same words)
     const bool plan_on = N.plan && T.lst_off && H0.lists_valid;
-    if (plan_on && tid == 64 && Q.ties == 1 && Q.cnt) plan_compute(plan, s_key[0], s_plan);
-    if (N.prof && tid == 0) sel_tick(st, 1, &pt);
+    if (plan_on && tid == 64) {
+        if (light) {  // the candidate's plan, by merge X's replace (pair_slack_block), unless the layout changed since
+            const PairTail &PT = *reinterpret_cast<const PairTail *>(&st->pr_plan[0]);
+            if (s_p0[P0_PGEN] == N.gen)
+                for (int k = 0; k < 6; k++) s_plan[k] = PT.plan[k];
+            else
+                plan_compute(plan, s_key[0], s_plan);
+        } else if (Q.ties == 1 && Q.cnt) {
+            plan_compute(plan, s_key[0], s_plan);
+        }
+    }
+    if (N.prof && tid == 0 && !light) sel_tick(st, 1, &pt);
     if (tid == 0) {
         FinishOut fo;
-        select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, Q.ties == 1 && Q.cnt ? s_key[0] : NO_ID,
-                      lastpair_wt, &fo, s_pre, Q.ties > 1, N.lp_lazy != 0);
+        select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, light || (Q.ties == 1 && Q.cnt) ? s_key[0] : NO_ID,
+                      lastpair_wt, &fo, s_pre, Q.ties > 1 && !light, N.lp_lazy != 0 || light);
         s_h = HALT_DONE;
         s_tie = 0;
         if (N.B.X < N.x_end) {
             bool tie;
             const uint32_t h = merge_begin_eval_v(T, fo, N.B, &tie);
-            merge_begin_commit_v(st, N.B, h, tie, fo);
+            if (light && !h && tie) {  // a pair select: the decision's commit, with its winner
+                st->cur_x = N.B.X;
+                st->tie_on = 0;
+                st->cur_key = s_key[0];
+                N.B.log[N.B.X - 256] = MergeLog{s_key[0], fo.top_count, (uint32_t)fo.live_tokens, fo.tie_count};
+                tie = false;
+            } else {
+                merge_begin_commit_v(st, N.B, h, tie, fo);
+            }
+            if (light) {
+                // chain: merge X+2's candidate is the next tied key by home, once this pair select is committed;
+                // its bound (the free slots between its home and the next, and after the largest, against the
+                // new pairs of both merges) and plan come from merge X+1's replace, whose home summaries are
+                // still the decision's (this launch refreshed none)
+                const PairTail &PT = *reinterpret_cast<const PairTail *>(&st->pr_plan[0]);
+                const uint32_t key2 = PT.key2, h3 = PT.h3, h4 = PT.h4;
+                if (!h && N.skip_refresh && key2 != NO_ID && N.B.X + 1 < N.x_end) {
+                    st->pr_key = key2;
+                    st->pr_key2 = NO_ID;
+                    const uint32_t ties0 = s_p0[P0_TIES], dt0 = s_p0[P0_DT];
+                    st->pr_ties = ties0 - 1u;
+                    st->pr_dt = (dt0 & 0xFFFFu) | (((dt0 >> 19) & 1u) << 16);
+                    st->pr_h2 = h3;
+                    st->pr_h3 = h4;
+                    st->pr_slack = ties0 == 3u ? 0xFFFFFFFFu : 0u;  // (the third was the last tied key)
+                    st->pr_plan_gen = 0xFFFFFFFFu;
+                    st->pr_x = N.B.X + 1;
+                } else {
+                    st->pr_x = 0;
+                }
+                st->pr_hits = s_p0[P0_HITS] + 1;
+            }
             s_h = h;
             s_tie = tie ? 1u : 0u;
         }
@@ -4551,17 +4553,24 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     __syncthreads();
     // merge X+1 needs no tie decision: the last refresh workgroup may skip its carries
     if (tid == 0 && (s_h || !s_tie)) st_wt(&st->ref_noprefix, X);
-    if (N.prof && tid == 0) sel_tick(st, 2, &pt);
+    if (N.prof && tid == 0 && !light) sel_tick(st, 2, &pt);
     // the tied top pair's key, deferred by select_finish (stored on every way out below)
     auto put_key = [&]() {
-        if (tid == KEY_TID && Q.cnt && Q.ties > 1) {
+        if (tid == KEY_TID && Q.cnt && Q.ties > 1 && !light) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             st->top_key = s_qkey;
         }
     };
     if (s_h || !s_tie) {
-        if (plan_on && tid == 64 && !s_h && Q.ties == 1 && Q.cnt) plan_store(st, N.B.X, s_key[0], N.gen, s_plan);
-        if (N.prof && tid == 0) st->pp_t[7] = wall_clock64();
+        if (plan_on && tid == 64 && !s_h && (light || (Q.ties == 1 && Q.cnt))) plan_store(st, N.B.X, s_key[0], N.gen, s_plan);
+        if (N.prof && tid == 0) {
+            const unsigned long long now = wall_clock64();
+            st->pp_t[7] = now;
+            if (light) {
+                atomicAdd(&st->sel_prof[20], 1ull);
+                atomicAdd(&st->sel_prof[21], now - st->sel_t0);
+            }
+        }
         put_key();
         return;
     }

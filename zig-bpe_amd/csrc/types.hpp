@@ -99,7 +99,7 @@ struct DevState {
     // pr_dt, the tied pairs it decremented (low 16 bits) with flags above them (bit 16 the candidate was
     // decremented, bit 17 a new pair reached the top count, bit 18 adjacent occurrences); the select of merge
     // X then starts merge X+1 with the candidate and no argmax or decision when every condition holds
-    // (pr_hits counts those). One 128-B group, loaded in one round trip (PairHead),
+    // (pr_hits counts those). Loaded as PairHead (the test, at kernel entry) and PairTail,
     // and the candidate's scan plan (valid for layout generation pr_plan_gen; by the replace's extra workgroup)
     alignas(128) uint32_t pr_x;
     uint32_t pr_key, pr_slack, pr_ties, pr_births, pr_dt, pr_hits, pr_plan_gen;
@@ -111,13 +111,14 @@ struct DevState {
     uint32_t pr_h2, pr_h3, pr_h4, pr_hmax;
     uint32_t pr_pad2[12];
 };
-struct PairHead {
+struct PairHead {  // what the light test reads (the kernel entry's round trip)
     uint32_t x, key, slack, ties, births, dt, hits, plan_gen;
+};
+struct PairTail {  // what a pair select then reads (plan, chain)
     uint32_t plan[6], key2, pad1;
     uint32_t h2, h3, h4, hmax;
-    uint32_t pad2[12];
 };
-static_assert(sizeof(PairHead) == 128, "pair head: 32 words");
+static_assert(sizeof(PairHead) == 32 && sizeof(PairTail) == 48, "pair head: 8 words, tail: 12");
 // DevState's hot header as one value (StateHead load_head(st))
 struct StateHead {
     uint32_t halt, cur_key, arena_top, lists_valid, lists_x, top_count, theta, hot_len, rec_count;
