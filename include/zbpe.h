@@ -79,13 +79,15 @@ typedef struct zbpe_stats {
     /* merges whose winner the previous merge's tie decision qualified (option "pair_select"): their select
      * skipped the argmax and the Zig-order decision */
     uint64_t pair_selects;
+    /* merges whose scan the previous merge's scan had done beside its own (option "pair_scan") */
+    uint64_t pair_scans;
 } zbpe_stats;
 
 /* Layout version of zbpe_stats. The struct is caller-allocated and has grown across versions: a
  * consumer compares zbpe_stats_size() with the size of the zbpe_stats of the header it was built against
  * before passing a zbpe_stats: the library writes zbpe_stats_size() bytes.
  *   1: up to tie_fallbacks ... list_builds;  2: + replications, phase split, sharded_merges;
- *   3: + tie_crosschecks, generate_tokens_s;  4: + pair_selects. */
+ *   3: + tie_crosschecks, generate_tokens_s;  4: + pair_selects, pair_scans. */
 #define ZBPE_STATS_VERSION 4
 size_t zbpe_stats_size(void);
 

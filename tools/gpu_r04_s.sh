@@ -1,0 +1,10 @@
+# pair scans (option pair_scan: a scan also walks the next merge's candidate): parity with it on, A/B, probes
+set -o pipefail
+mkdir -p gpurun_out
+export ZBPE_TEST_OPTS=""
+timeout -k 10 300 python -u tools/ab_run.py --reps 1 --cfg pair_scan=1 > gpurun_out/r04_ps_smoke.jsonl 2> gpurun_out/ps_smoke.err || exit 1
+: > gpurun_out/r04_ab_pscan.jsonl
+for r in 1 2 3; do
+  timeout -k 10 250 python -u tools/ab_run.py --reps 2 --cfg pair_scan=0 --cfg pair_scan=1 >> gpurun_out/r04_ab_pscan.jsonl 2> gpurun_out/ab_ps.err || exit 2
+done
+timeout -k 10 300 python tools/trace_run.py --opt sel_prof=1 --opt pair_scan=1 > gpurun_out/r04_sel_prof14.txt 2>&1 || exit 3

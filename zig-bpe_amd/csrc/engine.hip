@@ -59,7 +59,8 @@ void Engine::release() {
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_cs); f(d_rtk); f(d_sizes);
-    f(d_enc_cnt); f(d_enc_ctr); f(d_nb); f(d_ord_pos); f(d_ord_ent); f(d_sort_tmp);
+    f(d_enc_cnt); f(d_enc_ctr); f(d_nb); f(d_ord_pos); f(d_ord_ent); f(d_sort_tmp); f(d_spec);
+    d_spec = nullptr;
     f(d_dir); f(d_dir_row); f(d_row_tok); f(d_dir_tmp); f(d_sort_hist);
     d_dir = d_dir_row = d_row_tok = d_sort_hist = nullptr; d_dir_tmp = nullptr;
     dir_cap = dir_row_cap = row_tok_cap = dir_tmp_cap = sort_hist_cap = 0;
@@ -99,6 +100,8 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipMalloc(&d_st, sizeof(DevState)));
     HIP_OK(hipMalloc(&d_delta, 2 * DELTA_WORDS * sizeof(uint32_t)));  // two: merges alternate (delta_of)
     HIP_OK(hipMemset(d_delta, 0, 2 * DELTA_WORDS * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_spec, 2 * DELTA_WORDS * sizeof(uint32_t)));  // pair scans' spare deltas (spec_of)
+    HIP_OK(hipMemset(d_spec, 0, 2 * DELTA_WORDS * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&T.tok_cnt, 65536 * sizeof(int32_t)));
     HIP_OK(hipMalloc(&d_log, 65536 * sizeof(MergeLog)));
@@ -1141,6 +1144,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
     stats.distinct_pairs = (uint64_t)std::max(h_st->live, 0);
     stats.pair_selects = h_st->pr_hits;
+    stats.pair_scans = h_st->sp_hits;
     stats.pair_ids = h_st->num_ids;
     trained = true;
     if (out_stats) *out_stats = stats;
@@ -1184,6 +1188,13 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // the refresh counts of zbpe_select_next: each launch zeroes the next one's, unless this batch
     // does not continue the last one's launches
     if (fused_select && !begun) HIP_OK(hipMemsetAsync(d_rtk, 0, RTK_WORDS * sizeof(uint32_t), stream));
+    // pair scans: a batch that does not continue the last one's launches (host-path merges ran between) starts
+    // from clean spare buffers and slots (the selects keep them clean inside a run of batches)
+    const bool pair_scan_on = pair_scan && pair_select && fused_select && !dist();
+    if (pair_scan_on && !begun) {
+        HIP_OK(hipMemsetAsync(d_spec, 0, 2 * DELTA_WORDS * sizeof(uint32_t), stream));
+        HIP_OK(hipMemsetAsync(&d_st->sp[0], 0, sizeof(d_st->sp), stream));
+    }
     if (dist()) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
     const uint64_t C = home_slots;
     const uint32_t nb = (uint32_t)((C + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
@@ -1223,6 +1234,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                    lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log, nullptr, (int)sel_prof};
         set_list_nb(A);
         A.gen = layout_gen;
+        A.spec_left = pair_scan_on ? spec_of(X + 1) : nullptr;
         // a batch that follows one of list scans only launches a smaller grid (fewer idle workgroups
         // to dispatch); a stream scan still completes on it, only slower
         CHECK(launch_scan(A, list_streak ? list_grid : 0, top0));
@@ -1232,7 +1244,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         const int pair_blk = fused_select && pair_select && !tie_trust && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS ? 1 : 0;
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
                       1, dist() ? d_halo : nullptr, 1, (int)sel_prof, pair_blk, d_summ, d_sup, (uint32_t)C, nb, nsb, cs,
-                      A.dir_row, A.dir, A.dir_w, layout_gen, scan_plan && lists_on ? 1 : 0};
+                      A.dir_row, A.dir, A.dir_w, layout_gen, scan_plan && lists_on ? 1 : 0, pair_scan_on ? spec_of(X) : nullptr};
         if (!replace_split) {
             zbpe_replace<<<ab + update_blocks(X, update_per(X)) + pair_blk, 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
         } else {  // profiling: apply and count update as two launches (no pair-select bound)
@@ -1262,7 +1274,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
                        dist() ? world : 1, (int)sel_prof, tie_trust ? nullptr : cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
-                       scan_plan && lists_on ? 1 : 0, tie_trust ? 1 : 0, lp_lazy, pair_select, pair_refresh ? 0 : 1, pair_m3w, pair_chain};
+                       scan_plan && lists_on ? 1 : 0, tie_trust ? 1 : 0, lp_lazy, pair_select, pair_refresh ? 0 : 1, pair_m3w, pair_chain,
+                       pair_scan_on ? spec_of(X) : nullptr};
             const uint32_t nref = C && !tie_trust ? (refresh_wgs ? std::min<uint32_t>(nsb, refresh_wgs) : nsb) : 0u;
             zbpe_select_next<<<sel + nref, NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hcnt, T.hot_cap, nref, sel,
                                                                                  d_tok[cur], slots, T, d_partial, left, X, N);

@@ -46,6 +46,9 @@ struct Engine {
     // scan merge X + 1 into the other buffer while its own merge's words are still being cleared)
     uint32_t *d_delta = nullptr, *d_hist = nullptr;
     uint32_t *delta_of(uint32_t X) const { return d_delta + (size_t)(X & 1) * DELTA_WORDS; }
+    // pair scans (option pair_scan): merge X's spare delta buffer, filled by the scan of merge X-1 (DevState::sp)
+    uint32_t *d_spec = nullptr;
+    uint32_t *spec_of(uint32_t X) const { return d_spec + (size_t)(X & 1) * DELTA_WORDS; }
 
     // multi-GPU: this rank's shard and its neighbours' boundary tokens
     int rank = 0, world = 1;
@@ -149,6 +152,7 @@ struct Engine {
     int pair_select = 1;        // option "pair_select": a tied merge's decision qualifies the next merge's winner (DevState::pr_*)
     int pair_refresh = 0;       // option "pair_refresh": 1 = a pair select's refresh workgroups still refresh the dirty home blocks
     int pair_m3w = 1;           // option "pair_m3w": the decision's third-smallest tied home by a wave of its own
+    int pair_scan = 0;          // option "pair_scan": a scan also walks the next merge's candidate (DevState::sp)
     int pair_chain = 1;         // option "pair_chain": a pair select names the next merge's candidate too (three merges per decision)
     int lp_lazy = 1;            // option "lp_lazy": the select looks the stream's last pair up only when a tie's capacity needs it
     int tie_trust = 0;          // option "tie_trust": TIMING EXPERIMENT ONLY -- ties taken by smallest home, unverified

@@ -465,6 +465,12 @@ struct ScanArgs {
     uint32_t top_count;
     uint32_t plan_ok;
     uint32_t pl[6];
+    // pair scans (option pair_scan, batch mode): the spare delta buffer of merge X+1's candidate walk
+    // (nullptr: off), and in that walk the merged pair whose occurrences it must not touch (touch_out nullptr:
+    // not such a walk)
+    uint32_t *spec_left;
+    uint32_t touch_key;
+    uint32_t *touch_out;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // batching pays below about one occurrence per 400 slots and costs above it (tools/scan_bands.py:
@@ -492,7 +498,7 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0, const StateHead
     ScanArgs A{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
                A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
                A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb, A0.batch,
-               A0.dir_row, A0.dir, A0.dir_w, A0.gen, H.top_count, 0u, {}};
+               A0.dir_row, A0.dir, A0.dir_w, A0.gen, H.top_count, 0u, {}, A0.spec_left, 0u, nullptr};
     // batch mode: the plan the select stored with this merge's pair, for the current lists
     A.plan_ok = A0.dyn && H.plan_x == A0.X && H.plan_key == pair_key(a, b) && H.plan_gen == A0.gen ? 1u : 0u;
     A.pl[0] = H.plan_la; A.pl[1] = H.plan_lb; A.pl[2] = H.plan_oa; A.pl[3] = H.plan_ob; A.pl[4] = H.plan_r0; A.pl[5] = H.plan_r1;
@@ -714,8 +720,18 @@ __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64
                 if (r_occ) xx++;
                 else H.right((uint16_t)tr);
             }
+            if (hit && A.touch_out) {
+                // pair scan: does this occurrence touch one of the merged pair (ta, tb)'s? Its left neighbour
+                // ends one (L = tb after ta), its right neighbour starts one (R = ta before tb), or it shares a
+                // token with one (a == tb after ta at L, b == ta before tb at R); unknown past the window: yes
+                const uint32_t ta = A.touch_key & 0xFFFFu, tb = A.touch_key >> 16, tl = win(l), tr = win(r);
+                const bool t = (tl == tb && (ll < 0 || win(ll < 0 ? 0 : ll) == ta)) || (tr == ta && (rn >= 14 || win(rn > 13 ? 13 : rn) == tb)) ||
+                               (A.a == tb && tl == ta) || (A.b == ta && tr == tb);
+                if (t) atomicOr(A.touch_out, 1u);
+            }
         } else {
             hit = occ_slow(A, H, p, xx);
+            if (hit && A.touch_out) atomicOr(A.touch_out, 1u);  // (not resolved here: counted as touching)
         }
         if (hit) hits |= 1u << k;
     }
@@ -878,8 +894,11 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
                                                                          ScanLds &S, uint32_t vb, uint32_t vg, bool all = false);
 // one pair scan with resolved arguments: the list form when the shorter token list is short
 // enough, else the stream form
+// (vb, vg: this workgroup among the vg that walk a list; spec: a pair scan's candidate walk, list forms
+// only -- returns whether it walked)
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false, bool BATCH = false>
-__device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S, const StateHead &H) {
+__device__ __attribute__((always_inline)) inline bool scan_dispatch(const ScanArgs &A, ScanLds &S, const StateHead &H,
+                                                                    uint32_t vb, uint32_t vg, bool spec = false) {
     // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
     const uint32_t lists_x = H.lists_x;
     if (A.lists && A.a != A.b && H.lists_valid) {
@@ -905,7 +924,7 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
         // a's list sorted by build-time successor (a long list): by the invariant below, every occurrence
         // is in the range of successor b -- about the pair's count of entries, wherever a's list is
         if (ranged) {
-            if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (vb == 0 && threadIdx.x == 0 && !spec) {
                 A.st->scan_mode = 1;
                 if (A.log) {
                     A.log[A.X - 256].mode = 1;
@@ -915,8 +934,9 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
                 }
                 if (PROF) A.st->pp_t[4] = 1;
             }
-            scan_list_filtered<PROF>(A, false, r0, r1 - r0, S, blockIdx.x, gridDim.x, true);
-            return;
+            if (spec && vb == 0 && threadIdx.x == 0) A.st->sp[A.X & 1].len = r1 - r0;
+            scan_list_filtered<PROF>(A, false, r0, r1 - r0, S, vb, vg, true);
+            return true;
         }
         // Both tokens existed when the lists were built: since then a position's successor (its
         // predecessor) has only ever changed into a token created after the build (a merge at the
@@ -926,7 +946,7 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
         // (coalesced) and gathers the stream only where it matches: ~count gathers, not ~len.
         const bool NB = A.nb && A.a < lists_x && A.b < lists_x;
         if (len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n) {
-            if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (vb == 0 && threadIdx.x == 0 && !spec) {
                 A.st->scan_mode = 1;
                 if (A.log) {
                     A.log[A.X - 256].mode = 1;
@@ -935,13 +955,24 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
                 }
                 if (PROF) A.st->pp_t[4] = 1;
             }
-            if (NB) scan_list_filtered<PROF>(A, by_b, by_b ? ob : oa, len, S, blockIdx.x, gridDim.x);
-            else scan_list_body<PROF>(A, by_b, A.lists + (by_b ? ob : oa), len, S, nullptr, blockIdx.x, gridDim.x);
-            return;
+            if (spec && vb == 0 && threadIdx.x == 0) A.st->sp[A.X & 1].len = len;
+            if (NB) scan_list_filtered<PROF>(A, by_b, by_b ? ob : oa, len, S, vb, vg);
+            else scan_list_body<PROF>(A, by_b, A.lists + (by_b ? ob : oa), len, S, nullptr, vb, vg);
+            return true;
         }
     }
+    if (spec) return false;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
     scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH>(A, S);
+    return true;
+}
+// the scan plan says this merge's scan walks a list (scan_dispatch's test, on the plan's words)
+__device__ inline bool plan_is_list(const ScanArgs &A, const StateHead &H) {
+    if (!A.plan_ok || !A.lists || A.a == A.b || !H.lists_valid) return false;
+    const uint32_t la = A.pl[0], lb = A.pl[1], r0 = A.pl[4];
+    if (A.dir_row && r0 != NO_LIST && A.a < H.lists_x && A.b < H.lists_x) return true;
+    const uint32_t len = lb < la ? lb : la;
+    return len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n;
 }
 // PROF (option sel_prof): the pipeline probes; a separate instantiation, so the production kernel's
 // code and register allocation are untouched by them
@@ -967,7 +998,67 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
     if (A0.dyn && H.halt) return;
     __shared__ ScanLds S;
     const ScanArgs A = scan_args_resolve(A0, H);
-    scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF, BATCH>(A, S, H);
+    if (A0.spec_left) {  // pair scans (option pair_scan; batch mode, one GPU or replicas)
+        DevState *st = A0.st;
+        const SpecHead SP = st->sp[A0.X & 1];  // (written by the last scan for this merge)
+        const uint32_t px = st->pr_x, pk = st->pr_key;
+        if (SP.x == A0.X && SP.key == H.cur_key && SP.gen == A0.gen && SP.touch == 0) {
+            // the last scan walked this merge (merge X-1 touched none of its occurrences, so the walk over
+            // the stream before merge X-1 found what one now would): records in place after merge X-1's,
+            // deltas in the spare buffer (the replace reads them there); hand over the counts
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                st->rec_count = SP.rec;
+                A0.xx_out[0] = SP.xx;
+                A0.occ_out[0] = SP.occ;
+                st->sp_hit = A0.X;
+                st->sp_hits++;
+                st->scan_mode = 1;
+                if (A0.log) {
+                    A0.log[A0.X - 256].mode = 1;
+                    A0.log[A0.X - 256].list_len = SP.len;
+                }
+            }
+            return;
+        }
+        // the candidate of merge X+1 (pr_x, pr_key) is walked beside this merge's list walk, by the grid's
+        // upper half, when both walks are list walks and the arena holds both merges' records
+        const uint32_t half = gridDim.x / 2;
+        const bool spec = px == A0.X + 1 && pk != NO_ID && (pk & 0xFFFFu) != (pk >> 16) && half >= 1 && plan_is_list(A, H) &&
+                          (uint64_t)H.arena_top + 2ull * H.top_count <= (uint64_t)A0.rec_cap;
+        if (spec) {
+            if (blockIdx.x >= half) {
+                ScanArgs B = A;
+                B.a = pk & 0xFFFFu;
+                B.b = pk >> 16;
+                B.left = A0.spec_left;
+                B.right = A0.spec_left + (A0.X + 1);
+                B.X = A0.X + 1;
+                B.rec = A.rec + H.top_count;  // after merge X's records (its count: every occurrence is one)
+                B.rec_cap = A.rec_cap > H.top_count ? A.rec_cap - H.top_count : 0u;
+                SpecHead *sn = &st->sp[(A0.X + 1) & 1];  // (zeroed by the last select)
+                B.rec_ctr = &sn->rec;
+                B.xx_out = &sn->xx;
+                B.occ_out = &sn->occ;
+                B.log = nullptr;
+                B.prof = 0;
+                B.plan_ok = 0;
+                B.pres = nullptr;
+                B.touch_key = H.cur_key;
+                B.touch_out = &sn->touch;
+                const uint32_t vb = blockIdx.x - half;
+                if (scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, false, BATCH>(B, S, H, vb, gridDim.x - half, true) && vb == 0 &&
+                    threadIdx.x == 0) {
+                    sn->key = pk;
+                    sn->gen = A0.gen;
+                    sn->x = A0.X + 1;
+                }
+                return;
+            }
+            scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF, BATCH>(A, S, H, blockIdx.x, half);
+            return;
+        }
+    }
+    scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF, BATCH>(A, S, H, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1012,7 +1103,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) zbpe_encode_scan_batch(ScanArgs 
     const StateHead H = load_head(A0.st);
     A.top_count = H.top_count;
     A.plan_ok = 0;
-    scan_dispatch<4, true, true, true, true>(A, S, H);
+    scan_dispatch<4, true, true, true, true>(A, S, H, blockIdx.x, gridDim.x);
 }
 __global__ void __launch_bounds__(256) zbpe_encode_apply_batch(uint16_t *tok, int64_t n, EncBatch E, const uint32_t *__restrict__ scratch,
                                                                int32_t *cnt, uint32_t *ctr, uint32_t *arena, DevState *st, Tables T) {
@@ -2365,6 +2456,7 @@ struct ReplaceArgs {
     const uint32_t *dir_row, *dir;  // the candidate's scan plan (ScanArgs::dir_row, dir, dir_w)
     uint32_t dir_w, gen;
     int plan;
+    uint32_t *spec_left;  // pair scans: this merge's spare delta buffer (its walk by the last scan; nullptr: off)
 };
 // pair selects: merge X+1's candidate bound, by the replace's extra workgroup (defined with the home views below)
 __device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Summ *sup, uint32_t C, uint32_t nb,
@@ -2389,11 +2481,19 @@ __device__ inline void update_preload(const uint32_t *left, const uint32_t *righ
 // R.apply_blocks; right = left + X), so they issue at entry beside the state head.
 __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t *__restrict__ left, uint32_t Xp, uint32_t apply_blocks,
                                                     ReplaceArgs R, Tables T) {
-    uint32_t dv[UPD_MAX_PER];
+    uint32_t dv[UPD_MAX_PER], dv2[UPD_MAX_PER];
     const uint32_t per = update_per(Xp);
     if (blockIdx.x >= apply_blocks) update_preload(left, left + Xp, Xp, blockIdx.x - apply_blocks, per, dv);
+    // pair scans: the spare buffer's deltas too (which one holds this merge's is in the state)
+    if (R.spec_left && blockIdx.x >= apply_blocks) update_preload(R.spec_left, R.spec_left + Xp, Xp, blockIdx.x - apply_blocks, per, dv2);
     const StateHead H = load_head(st);  // (with the deltas: one round trip)
     const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key, pr_key2 = st->pr_key2;  // (same round trip)
+    if (R.spec_left && st->sp_hit == R.X) {  // this merge's walk was the last scan's candidate walk
+#pragma unroll
+        for (int k = 0; k < UPD_MAX_PER; k++) dv[k] = dv2[k];
+        R.left = R.spec_left;
+        R.right = R.spec_left + Xp;
+    }
     const uint32_t theta = H.theta;
     if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the list scan's stamps
         const unsigned long long now = wall_clock64();
@@ -4134,6 +4234,7 @@ struct NextArgs {
     int skip_refresh;     // option pair_refresh 0: a pair select's refresh workgroups leave the dirty blocks to the next launch
     int m3_w4;            // option pair_m3w: the decision's third-smallest home by wave 4 (else wave 0)
     int chain;            // option pair_chain: a pair select names merge X+2's candidate (needs skip_refresh, m3_w4)
+    uint32_t *spec_clear; // pair scans: merge X's spare delta buffer (nullptr: off)
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -4217,6 +4318,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // critical path: the argmax grid is sized by the hot list alone; nothing in this launch reads
         // [0, 2X) -- the roll reads the tail words past it)
         for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
+        if (N.spec_clear) {  // pair scans: merge X's spare deltas (read by its replace) and the slot merge X+2's walk fills
+            for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) N.spec_clear[t] = 0;
+            if (blockIdx.x == 0 && tid < 8) reinterpret_cast<uint32_t *>(&st->sp[X & 1])[tid] = 0u;
+        }
         if (N.pair && N.skip_refresh) {  // a pair select: no decision in this launch reads the summaries
             const PairHead P0 = *reinterpret_cast<const PairHead *>(&st->pr_x);
             if (pair_light(N.pair, N.B.X, N.x_end, N.V.C, P0, st->live)) return;

@@ -141,6 +141,7 @@ class Stats(ctypes.Structure):
         ("tie_crosschecks", ctypes.c_uint64),
         ("generate_tokens_s", ctypes.c_double),
         ("pair_selects", ctypes.c_uint64),
+        ("pair_scans", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
