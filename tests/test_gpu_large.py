@@ -263,3 +263,52 @@ def test_c3_encode_and_decode(c3):
         t.merges.put(zbpe.CharPair(int(a), int(b)), int(x))
     pre = c3.text[: 1 << 18]
     assert t.decode(c3.e.encode(c3.merges, pre)) == pre  # the API's own decode on a prefix
+
+
+# --- pair selects, chains, pair scans: fewer launches' work, the same merges -------
+PAIR_OPTS = [
+    {"pair_select": 0},
+    {"pair_select": 1, "pair_chain": 0},
+    {"pair_select": 1, "pair_chain": 1},
+    {"pair_select": 1, "pair_refresh": 1},
+    {"pair_select": 1, "pair_chain": 1, "pair_scan": 1},
+]
+
+
+def _train_with(text, vocab, opts):
+    e = zbpe.Engine(0)
+    e.upload(text)
+    for k, v in opts.items():
+        e.set_option(k, v)
+    m, c, st = e.train_resident(vocab)
+    fnv = O.fnv64(e.tokens())
+    mism = e.verify_counts()
+    e.close()
+    return m, c, st, fnv, mism
+
+
+@pytest.mark.parametrize("opts", PAIR_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_c3_pair_options_same_run(c3, opts):
+    """every C3 merge, count and tie count, the final stream and the recount are the same whichever of the
+    pair options is on; the counters say the option did something"""
+    m, c, st, fnv, mism = _train_with(c3.text, c3.vocab, opts)
+    assert np.array_equal(m, c3.merges) and np.array_equal(c, c3.counts)
+    assert st.tie_iterations == c3.stats.tie_iterations
+    assert fnv == c3.final_fnv and mism == 0
+    if opts.get("pair_select", 1):
+        assert st.pair_selects > 0
+    else:
+        assert st.pair_selects == 0
+    if opts.get("pair_scan", 0):
+        assert st.pair_scans > 0
+    else:
+        assert st.pair_scans == 0
+
+
+def test_c4_pair_scans_same_run(c4):
+    """C4 with pair scans on: all 31,744 merges and counts, the tie count, the final stream"""
+    m, c, st, fnv, mism = _train_with(c4.text, c4.vocab, {"pair_scan": 1})
+    assert np.array_equal(m, c4.merges) and np.array_equal(c, c4.counts)
+    assert st.tie_iterations == c4.stats.tie_iterations
+    assert fnv == c4.final_fnv and mism == 0
+    assert st.pair_scans > 1000 and st.pair_selects > 1000

@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export ZBPE_TEST_OPTS=""
-timeout -k 10 300 python -u tools/ab_run.py --reps 1 --cfg pair_scan=1 > gpurun_out/r04_ps_smoke.jsonl 2> gpurun_out/ps_smoke.err || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_large.py -x -v -k "pair" --timeout 500 --timeout-method thread > gpurun_out/pytest_pair_s.log 2>&1 || exit 1
 : > gpurun_out/r04_ab_pscan.jsonl
 for r in 1 2 3; do
   timeout -k 10 250 python -u tools/ab_run.py --reps 2 --cfg pair_scan=0 --cfg pair_scan=1 >> gpurun_out/r04_ab_pscan.jsonl 2> gpurun_out/ab_ps.err || exit 2
