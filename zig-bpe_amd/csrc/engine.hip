@@ -1190,7 +1190,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     if (fused_select && !begun) HIP_OK(hipMemsetAsync(d_rtk, 0, RTK_WORDS * sizeof(uint32_t), stream));
     // pair scans: a batch that does not continue the last one's launches (host-path merges ran between) starts
     // from clean spare buffers and slots (the selects keep them clean inside a run of batches)
-    const bool pair_scan_on = pair_scan && pair_select && fused_select && !dist();
+    const bool pair_scan_on = ZBPE_PAIR_SCAN && pair_scan && pair_select && fused_select && !dist();
     if (pair_scan_on && !begun) {
         HIP_OK(hipMemsetAsync(d_spec, 0, 2 * DELTA_WORDS * sizeof(uint32_t), stream));
         HIP_OK(hipMemsetAsync(&d_st->sp[0], 0, sizeof(d_st->sp), stream));

@@ -13,6 +13,9 @@
 
 #include "types.hpp"
 
+#ifndef ZBPE_PAIR_SCAN
+#define ZBPE_PAIR_SCAN 0  // pair scans compiled in (option pair_scan; 0: the scan, replace and select kernels have no trace of them)
+#endif
 #ifndef ZBPE_PAIR_MIN4
 #define ZBPE_PAIR_MIN4 1  // decide_body: the pair-select chain's fourth-smallest home (0: min3 only, no chains past two)
 #endif
@@ -720,7 +723,7 @@ __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64
                 if (r_occ) xx++;
                 else H.right((uint16_t)tr);
             }
-            if (hit && A.touch_out) {
+            if (ZBPE_PAIR_SCAN && hit && A.touch_out) {
                 // pair scan: does this occurrence touch one of the merged pair (ta, tb)'s? Its left neighbour
                 // ends one (L = tb after ta), its right neighbour starts one (R = ta before tb), or it shares a
                 // token with one (a == tb after ta at L, b == ta before tb at R); unknown past the window: yes
@@ -731,7 +734,7 @@ __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64
             }
         } else {
             hit = occ_slow(A, H, p, xx);
-            if (hit && A.touch_out) atomicOr(A.touch_out, 1u);  // (not resolved here: counted as touching)
+            if (ZBPE_PAIR_SCAN && hit && A.touch_out) atomicOr(A.touch_out, 1u);  // (not resolved here: counted as touching)
         }
         if (hit) hits |= 1u << k;
     }
@@ -998,7 +1001,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
     if (A0.dyn && H.halt) return;
     __shared__ ScanLds S;
     const ScanArgs A = scan_args_resolve(A0, H);
-    if (A0.spec_left) {  // pair scans (option pair_scan; batch mode, one GPU or replicas)
+    if (ZBPE_PAIR_SCAN && A0.spec_left) {  // pair scans (option pair_scan; batch mode, one GPU or replicas)
         DevState *st = A0.st;
         const SpecHead SP = st->sp[A0.X & 1];  // (written by the last scan for this merge)
         const uint32_t px = st->pr_x, pk = st->pr_key;
@@ -2485,10 +2488,10 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     const uint32_t per = update_per(Xp);
     if (blockIdx.x >= apply_blocks) update_preload(left, left + Xp, Xp, blockIdx.x - apply_blocks, per, dv);
     // pair scans: the spare buffer's deltas too (which one holds this merge's is in the state)
-    if (R.spec_left && blockIdx.x >= apply_blocks) update_preload(R.spec_left, R.spec_left + Xp, Xp, blockIdx.x - apply_blocks, per, dv2);
+    if (ZBPE_PAIR_SCAN && R.spec_left && blockIdx.x >= apply_blocks) update_preload(R.spec_left, R.spec_left + Xp, Xp, blockIdx.x - apply_blocks, per, dv2);
     const StateHead H = load_head(st);  // (with the deltas: one round trip)
     const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key, pr_key2 = st->pr_key2;  // (same round trip)
-    if (R.spec_left && st->sp_hit == R.X) {  // this merge's walk was the last scan's candidate walk
+    if (ZBPE_PAIR_SCAN && R.spec_left && st->sp_hit == R.X) {  // this merge's walk was the last scan's candidate walk
 #pragma unroll
         for (int k = 0; k < UPD_MAX_PER; k++) dv[k] = dv2[k];
         R.left = R.spec_left;
@@ -4318,7 +4321,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // critical path: the argmax grid is sized by the hot list alone; nothing in this launch reads
         // [0, 2X) -- the roll reads the tail words past it)
         for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
-        if (N.spec_clear) {  // pair scans: merge X's spare deltas (read by its replace) and the slot merge X+2's walk fills
+        if (ZBPE_PAIR_SCAN && N.spec_clear) {  // pair scans: merge X's spare deltas (read by its replace) and the slot merge X+2's walk fills
             for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) N.spec_clear[t] = 0;
             if (blockIdx.x == 0 && tid < 8) reinterpret_cast<uint32_t *>(&st->sp[X & 1])[tid] = 0u;
         }
