@@ -2298,7 +2298,8 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                                     const uint32_t *__restrict__ right, const uint32_t *__restrict__ tail, uint32_t a,
                                     uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per,
                                     const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta, int prof = 0,
-                                    uint32_t top_count = 0, uint32_t pr_key = NO_ID, uint32_t pr_key2 = NO_ID) {
+                                    uint32_t top_count = 0, uint32_t pr_key = NO_ID, uint32_t pr_key2 = NO_ID,
+                                    uint32_t pr_key3 = NO_ID) {
     // pr_key != NO_ID: merge X+1 has a pair-select candidate (DevState::pr_key): count the new pairs, the
     // tied pairs decremented (old count == top_count) and flag what rules the candidate out
     // option sel_prof: the latest stamp of each phase over the update blocks (st->pp_t[8..11])
@@ -2406,7 +2407,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 if (old == c) { live_delta--; home_add(T, st, key, false); }
                 // (a pair's first decrement sees its count before the merge: each tied pair counts once)
                 if (pr_key != NO_ID && old == top_count)
-                    atomicAdd(&st->pr_dt, key == pr_key ? 0x10001u : key == pr_key2 ? 0x80001u : 1u);
+                    atomicAdd(&st->pr_dt, key == pr_key ? 0x10001u : key == pr_key2 ? 0x80001u : key == pr_key3 ? 0x100001u : 1u);
             }
         } else {
             const uint32_t id = s_base + i;
@@ -2490,7 +2491,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     // pair scans: the spare buffer's deltas too (which one holds this merge's is in the state)
     if (ZBPE_PAIR_SCAN && R.spec_left && blockIdx.x >= apply_blocks) update_preload(R.spec_left, R.spec_left + Xp, Xp, blockIdx.x - apply_blocks, per, dv2);
     const StateHead H = load_head(st);  // (with the deltas: one round trip)
-    const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key, pr_key2 = st->pr_key2;  // (same round trip)
+    const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key, pr_key2 = st->pr_key2, pr_key3 = st->pr_key3;  // (same round trip)
     if (ZBPE_PAIR_SCAN && R.spec_left && st->sp_hit == R.X) {  // this merge's walk was the last scan's candidate walk
 #pragma unroll
         for (int k = 0; k < UPD_MAX_PER; k++) dv[k] = dv2[k];
@@ -2570,7 +2571,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     const uint32_t ublk = blockIdx.x - apply_blocks;
     if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) atomicOr(&st->error, 64u);  // occurrences != count
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof, H.top_count,
-                 R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2);
+                 R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2, pr_key3);
     if (R.prof) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
@@ -3905,28 +3906,40 @@ __device__ inline void min3_merge(uint64_t &a1, uint64_t &a2, uint64_t &a3, uint
     const uint64_t r3 = min(min(a3, b3), min(max(a2, b1), max(a1, b2)));
     a1 = r1; a2 = r2; a3 = r3;
 }
-// the four smallest of two sorted quadruples: r_k = min over i of max(a_i, b_{k-i}) (a_0 = b_0 = -inf)
-__device__ inline void min4_merge(uint64_t (&a)[4], const uint64_t (&b)[4]) {
-    const uint64_t r1 = min(a[0], b[0]);
-    const uint64_t r2 = min(min(a[1], b[1]), max(a[0], b[0]));
-    const uint64_t r3 = min(min(a[2], b[2]), min(max(a[1], b[0]), max(a[0], b[1])));
-    const uint64_t r4 = min(min(a[3], b[3]), min(min(max(a[2], b[0]), max(a[0], b[2])), max(a[1], b[1])));
-    a[0] = r1; a[1] = r2; a[2] = r3; a[3] = r4;
+// the K smallest of two sorted K-tuples: r_k = min over i of max(a_i, b_{k-i}) (a_0 = b_0 = -inf)
+template <int K>
+__device__ inline void minK_merge(uint64_t (&a)[K], const uint64_t (&b)[K]) {
+    uint64_t r[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        uint64_t v = min(a[k], b[k]);
+#pragma unroll
+        for (int i = 0; i < k; i++) v = min(v, max(a[i], b[k - 1 - i]));
+        r[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) a[k] = r[k];
 }
-__device__ inline void wave_min4(const uint64_t *list, uint32_t len, uint64_t (&m)[4], uint32_t &hmax) {
+template <int K>
+__device__ inline void wave_minK(const uint64_t *list, uint32_t len, uint64_t (&m)[K], uint32_t &hmax) {
     const uint32_t lane = threadIdx.x & 63;
-    m[0] = m[1] = m[2] = m[3] = ~0ull;
+#pragma unroll
+    for (int k = 0; k < K; k++) m[k] = ~0ull;
     hmax = 0;
     for (uint32_t i = lane; i < len; i += 64) {
         const uint64_t e = list[i];
-        const uint64_t b[4] = {e, ~0ull, ~0ull, ~0ull};
-        min4_merge(m, b);
+        uint64_t b[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) b[k] = k ? ~0ull : e;
+        minK_merge<K>(m, b);
         hmax = max(hmax, (uint32_t)(e >> 32));
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-        const uint64_t b[4] = {__shfl_xor(m[0], off), __shfl_xor(m[1], off), __shfl_xor(m[2], off), __shfl_xor(m[3], off)};
-        min4_merge(m, b);
+        uint64_t b[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) b[k] = __shfl_xor(m[k], off);
+        minK_merge<K>(m, b);
         hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
     }
 }
@@ -4037,7 +4050,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
                                    uint32_t plan_gen = 0, bool trust = false, uint32_t pair_x = 0, bool m3_w4 = false,
-                                   bool chain = false) {
+                                   bool chain = false, bool chain2 = false) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
     // trust (option tie_trust, a TIMING EXPERIMENT only, never a default): the smallest home wins with no
     // cluster or wrap test -- what a decision costs without the home summaries
@@ -4054,7 +4067,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
     const int w = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t ws = V.C > 4096 ? V.C - 4096 : 0;
-    __shared__ uint64_t s_m3, s_m4;
+    __shared__ uint64_t s_m3, s_m4, s_m5;
     if (w == 0) {
         uint64_t m1 = ~0ull, m2 = ~0ull, m3 = ~0ull;
         uint32_t hmax = 0;
@@ -4073,7 +4086,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                 hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
             }
         }
-        if (lane == 0 && !(NT >= 512 && pair_x && m3_w4)) { s_m3 = m3; s_m4 = ~0ull; }
+        if (lane == 0 && !(NT >= 512 && pair_x && m3_w4)) { s_m3 = m3; s_m4 = ~0ull; s_m5 = ~0ull; }
         const uint32_t h1 = (uint32_t)(m1 >> 32);
         const int64_t f = !len ? -1 : trust ? (int64_t)V.C : cs ? wave_first_free(V, h1, wave_carry_from_super(V, cs, h1)) : wave_free_from(V, h1);
         if (lane == 0) { s_free = f; s_m1 = m1; s_m2 = m2; s_hmax = hmax; }
@@ -4097,15 +4110,15 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
     const bool pair_on = NT >= 512 && pair_x && cs && !trust && len >= 2;
     if (NT >= 512 && pair_x && m3_w4 && w == 4) {  // (option pair_m3w: the third- and fourth-smallest by a wave of its own)
 #if ZBPE_PAIR_MIN4
-        uint64_t q[4];
+        uint64_t q[5];
         uint32_t hmx;
-        wave_min4(list, len, q, hmx);
-        if (lane == 0) { s_m3 = q[2]; s_m4 = q[3]; }
+        wave_minK<5>(list, len, q, hmx);
+        if (lane == 0) { s_m3 = q[2]; s_m4 = q[3]; s_m5 = q[4]; }
 #else
         uint64_t p1, p2, p3;
         uint32_t hmx;
         wave_min3(list, len, p1, p2, p3, hmx);
-        if (lane == 0) { s_m3 = p3; s_m4 = ~0ull; }
+        if (lane == 0) { s_m3 = p3; s_m4 = ~0ull; s_m5 = ~0ull; }
 #endif
     }
     if (NT >= 256 && plan_on && w == 3 && len) {
@@ -4158,12 +4171,17 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                 st->pr_h2 = (uint32_t)(m2 >> 32);
                 st->pr_h3 = len >= 3 ? (uint32_t)(s_m3 >> 32) : 0u;
                 st->pr_h4 = len >= 4 && s_m4 != ~0ull ? (uint32_t)(s_m4 >> 32) : 0u;
+                st->pr_h5 = len >= 5 && s_m5 != ~0ull ? (uint32_t)(s_m5 >> 32) : 0u;
                 st->pr_hmax = hmax;
                 // chain: the third-smallest home's key for merge X+2 (found with the fourth, wave 4)
                 const uint32_t k3 = (uint32_t)s_m3;
-                st->pr_key2 = chain && m3_w4 && len >= 3 && s_m3 != ~0ull && (k3 & 0xFFFF) != (k3 >> 16) &&
-                                      (len == 3 || s_m4 != ~0ull)
-                                  ? k3 : NO_ID;
+                const bool c2 = chain && m3_w4 && len >= 3 && s_m3 != ~0ull && (k3 & 0xFFFF) != (k3 >> 16) &&
+                                (len == 3 || s_m4 != ~0ull);
+                st->pr_key2 = c2 ? k3 : NO_ID;
+                // chain depth 2 (option pair_chain 2): the fourth key, merge X+3's candidate
+                const uint32_t k4 = (uint32_t)s_m4;
+                st->pr_key3 = c2 && chain2 && len >= 4 && s_m4 != ~0ull && (k4 & 0xFFFF) != (k4 >> 16) && (len == 4 || s_m5 != ~0ull)
+                                  ? k4 : NO_ID;
                 st->pr_plan_gen = 0xFFFFFFFFu;  // (the replace's extra workgroup loads the plan)
                 st->pr_births = 0;
                 st->pr_dt = 0;
@@ -4236,7 +4254,7 @@ struct NextArgs {
     int pair;             // option pair_select (DevState::pr_*)
     int skip_refresh;     // option pair_refresh 0: a pair select's refresh workgroups leave the dirty blocks to the next launch
     int m3_w4;            // option pair_m3w: the decision's third-smallest home by wave 4 (else wave 0)
-    int chain;            // option pair_chain: a pair select names merge X+2's candidate (needs skip_refresh, m3_w4)
+    int chain;            // option pair_chain: a pair select names merge X+2's candidate (needs skip_refresh, m3_w4); 2: and X+3's
     uint32_t *spec_clear; // pair scans: merge X's spare delta buffer (nullptr: off)
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
@@ -4635,15 +4653,17 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 // new pairs of both merges) and plan come from merge X+1's replace, whose home summaries are
                 // still the decision's (this launch refreshed none)
                 const PairTail &PT = *reinterpret_cast<const PairTail *>(&st->pr_plan[0]);
-                const uint32_t key2 = PT.key2, h3 = PT.h3, h4 = PT.h4;
+                const uint32_t key2 = PT.key2, key3 = PT.key3, h3 = PT.h3, h4 = PT.h4, h5 = PT.h5;
                 if (!h && N.skip_refresh && key2 != NO_ID && N.B.X + 1 < N.x_end) {
-                    st->pr_key = key2;
-                    st->pr_key2 = NO_ID;
+                    st->pr_key = key2;  // the chain moves up one: key2 -> key, key3 -> key2, their flags with them
+                    st->pr_key2 = key3;
+                    st->pr_key3 = NO_ID;
                     const uint32_t ties0 = s_p0[P0_TIES], dt0 = s_p0[P0_DT];
                     st->pr_ties = ties0 - 1u;
-                    st->pr_dt = (dt0 & 0xFFFFu) | (((dt0 >> 19) & 1u) << 16);
+                    st->pr_dt = (dt0 & 0xFFFFu) | (((dt0 >> 19) & 1u) << 16) | (((dt0 >> 20) & 1u) << 19);
                     st->pr_h2 = h3;
                     st->pr_h3 = h4;
+                    st->pr_h4 = h5;
                     st->pr_slack = ties0 == 3u ? 0xFFFFFFFFu : 0u;  // (the third was the last tied key)
                     st->pr_plan_gen = 0xFFFFFFFFu;
                     st->pr_x = N.B.X + 1;
@@ -4813,7 +4833,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
                               plan_on, plan, N.gen, N.trust != 0, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u, N.m3_w4 != 0,
-                              N.skip_refresh != 0 && N.chain != 0);
+                              N.skip_refresh != 0 && N.chain != 0, N.chain >= 2);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }

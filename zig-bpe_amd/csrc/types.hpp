@@ -111,9 +111,9 @@ struct DevState {
     // chains (option pair_refresh 0): the third-smallest home's key, candidate of merge X+2 once merge X+1 was a
     // pair select (bit 19 of pr_dt: decremented); the tied homes the replace bounds the free slots with: the
     // candidate's and the next one's (pr_h2, pr_h3), the one after (pr_h4) and the largest (pr_hmax)
-    uint32_t pr_key2, pr_pad1;
-    uint32_t pr_h2, pr_h3, pr_h4, pr_hmax;
-    uint32_t pr_pad2[12];
+    uint32_t pr_key2, pr_key3;        // (pr_key3: merge X+3's, option pair_chain 2; bit 20 of pr_dt: decremented)
+    uint32_t pr_h2, pr_h3, pr_h4, pr_hmax, pr_h5;
+    uint32_t pr_pad2[11];
     // Pair scans (option pair_scan): the scan of merge X also walks merge X+1's candidate (pr_key) into a spare
     // delta buffer, its records after merge X's in the arena, and flags (sp_touch) any of its occurrences
     // that touches one of merge X's; the scan of merge X+1 then only hands the walk over when its pair is
@@ -127,10 +127,10 @@ struct PairHead {  // what the light test reads (the kernel entry's round trip)
     uint32_t x, key, slack, ties, births, dt, hits, plan_gen;
 };
 struct PairTail {  // what a pair select then reads (plan, chain)
-    uint32_t plan[6], key2, pad1;
-    uint32_t h2, h3, h4, hmax;
+    uint32_t plan[6], key2, key3;
+    uint32_t h2, h3, h4, hmax, h5;
 };
-static_assert(sizeof(PairHead) == 32 && sizeof(PairTail) == 48, "pair head: 8 words, tail: 12");
+static_assert(sizeof(PairHead) == 32 && sizeof(PairTail) == 52, "pair head: 8 words, tail: 13");
 // DevState's hot header as one value (StateHead load_head(st))
 struct StateHead {
     uint32_t halt, cur_key, arena_top, lists_valid, lists_x, top_count, theta, hot_len, rec_count;
