@@ -153,7 +153,7 @@ struct Engine {
     int pair_refresh = 0;       // option "pair_refresh": 1 = a pair select's refresh workgroups still refresh the dirty home blocks
     int pair_m3w = 1;           // option "pair_m3w": the decision's third-smallest tied home by a wave of its own
     int pair_scan = 0;          // option "pair_scan": a scan also walks the next merge's candidate (DevState::sp)
-    int pair_chain = 1;         // option "pair_chain": a pair select names the next merge's candidate too (three merges per decision)
+    int pair_chain = 2;         // option "pair_chain": a pair select names the next merge's candidate too (1: three merges per decision, 2: four)
     int lp_lazy = 1;            // option "lp_lazy": the select looks the stream's last pair up only when a tie's capacity needs it
     int tie_trust = 0;          // option "tie_trust": TIMING EXPERIMENT ONLY -- ties taken by smallest home, unverified
     int dense_hist = 1;         // option "dense_hist": the full pair histogram of a byte stream counts every byte pair in a fixed 16-bit LDS bin
