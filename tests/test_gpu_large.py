@@ -271,6 +271,7 @@ PAIR_OPTS = [
     {"pair_select": 1, "pair_chain": 0},
     {"pair_select": 1, "pair_chain": 1},
     {"pair_select": 1, "pair_chain": 2},
+    {"pair_select": 1, "pair_chain": 3},
     {"pair_select": 1, "pair_refresh": 1},
     {"pair_select": 1, "pair_chain": 1, "pair_scan": 1},
 ]
@@ -321,11 +322,12 @@ def test_c4_pair_scans_same_run(c4):
     assert st.pair_scans > 1000 and st.pair_selects > 1000
 
 
-def test_c4_pair_chain2_same_run(c4):
-    """C4 with chains of depth 2 (four merges per decision): all 31,744 merges and counts, the tie count, the
+@pytest.mark.parametrize("depth", [1, 3])
+def test_c4_pair_chain_depths_same_run(c4, depth):
+    """C4 with chains of depth 1 and 3 (the default is 2): all 31,744 merges and counts, the tie count, the
     final stream"""
-    m, c, st, fnv, mism = _train_with(c4.text, c4.vocab, {"pair_chain": 2})
+    m, c, st, fnv, mism = _train_with(c4.text, c4.vocab, {"pair_chain": depth})
     assert np.array_equal(m, c4.merges) and np.array_equal(c, c4.counts)
     assert st.tie_iterations == c4.stats.tie_iterations
     assert fnv == c4.final_fnv and mism == 0
-    assert st.pair_selects > c4.stats.pair_selects
+    assert (st.pair_selects > c4.stats.pair_selects) == (depth > 2)

@@ -164,7 +164,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "pair_select" && (value == 0 || value == 1)) e.pair_select = (int)value;
     else if (k == "pair_refresh" && (value == 0 || value == 1)) e.pair_refresh = (int)value;
     else if (k == "pair_m3w" && (value == 0 || value == 1)) e.pair_m3w = (int)value;
-    else if (k == "pair_chain" && value >= 0 && value <= 2) e.pair_chain = (int)value;
+    else if (k == "pair_chain" && value >= 0 && value <= 3) e.pair_chain = (int)value;
     else if (k == "pair_scan" && (value == 0 || (value == 1 && ZBPE_PAIR_SCAN))) e.pair_scan = (int)value;  // (1: a build with -DZBPE_PAIR_SCAN=1)
     else if (k == "encode_list_ratio" && value >= 1) e.enc_list_ratio = (uint32_t)value;
     else if (k == "list_start" && value >= 0) e.list_start = (uint64_t)value;

@@ -2299,7 +2299,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                                     uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per,
                                     const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta, int prof = 0,
                                     uint32_t top_count = 0, uint32_t pr_key = NO_ID, uint32_t pr_key2 = NO_ID,
-                                    uint32_t pr_key3 = NO_ID) {
+                                    uint32_t pr_key3 = NO_ID, uint32_t pr_key4 = NO_ID) {
     // pr_key != NO_ID: merge X+1 has a pair-select candidate (DevState::pr_key): count the new pairs, the
     // tied pairs decremented (old count == top_count) and flag what rules the candidate out
     // option sel_prof: the latest stamp of each phase over the update blocks (st->pp_t[8..11])
@@ -2407,7 +2407,11 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 if (old == c) { live_delta--; home_add(T, st, key, false); }
                 // (a pair's first decrement sees its count before the merge: each tied pair counts once)
                 if (pr_key != NO_ID && old == top_count)
-                    atomicAdd(&st->pr_dt, key == pr_key ? 0x10001u : key == pr_key2 ? 0x80001u : key == pr_key3 ? 0x100001u : 1u);
+                    atomicAdd(&st->pr_dt, key == pr_key    ? 0x10001u
+                                          : key == pr_key2 ? 0x80001u
+                                          : key == pr_key3 ? 0x100001u
+                                          : key == pr_key4 ? 0x200001u
+                                                           : 1u);
             }
         } else {
             const uint32_t id = s_base + i;
@@ -2491,7 +2495,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     // pair scans: the spare buffer's deltas too (which one holds this merge's is in the state)
     if (ZBPE_PAIR_SCAN && R.spec_left && blockIdx.x >= apply_blocks) update_preload(R.spec_left, R.spec_left + Xp, Xp, blockIdx.x - apply_blocks, per, dv2);
     const StateHead H = load_head(st);  // (with the deltas: one round trip)
-    const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key, pr_key2 = st->pr_key2, pr_key3 = st->pr_key3;  // (same round trip)
+    const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key, pr_key2 = st->pr_key2, pr_key3 = st->pr_key3, pr_key4 = st->pr_key4;
     if (ZBPE_PAIR_SCAN && R.spec_left && st->sp_hit == R.X) {  // this merge's walk was the last scan's candidate walk
 #pragma unroll
         for (int k = 0; k < UPD_MAX_PER; k++) dv[k] = dv2[k];
@@ -2571,7 +2575,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     const uint32_t ublk = blockIdx.x - apply_blocks;
     if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) atomicOr(&st->error, 64u);  // occurrences != count
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof, H.top_count,
-                 R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2, pr_key3);
+                 R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2, pr_key3, pr_key4);
     if (R.prof) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
@@ -4050,7 +4054,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
                                    uint32_t plan_gen = 0, bool trust = false, uint32_t pair_x = 0, bool m3_w4 = false,
-                                   bool chain = false, bool chain2 = false) {
+                                   bool chain = false, bool chain2 = false, bool chain3 = false) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
     // trust (option tie_trust, a TIMING EXPERIMENT only, never a default): the smallest home wins with no
     // cluster or wrap test -- what a decision costs without the home summaries
@@ -4067,7 +4071,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
     const int w = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t ws = V.C > 4096 ? V.C - 4096 : 0;
-    __shared__ uint64_t s_m3, s_m4, s_m5;
+    __shared__ uint64_t s_m3, s_m4, s_m5, s_m6;
     if (w == 0) {
         uint64_t m1 = ~0ull, m2 = ~0ull, m3 = ~0ull;
         uint32_t hmax = 0;
@@ -4086,7 +4090,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                 hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
             }
         }
-        if (lane == 0 && !(NT >= 512 && pair_x && m3_w4)) { s_m3 = m3; s_m4 = ~0ull; s_m5 = ~0ull; }
+        if (lane == 0 && !(NT >= 512 && pair_x && m3_w4)) { s_m3 = m3; s_m4 = ~0ull; s_m5 = ~0ull; s_m6 = ~0ull; }
         const uint32_t h1 = (uint32_t)(m1 >> 32);
         const int64_t f = !len ? -1 : trust ? (int64_t)V.C : cs ? wave_first_free(V, h1, wave_carry_from_super(V, cs, h1)) : wave_free_from(V, h1);
         if (lane == 0) { s_free = f; s_m1 = m1; s_m2 = m2; s_hmax = hmax; }
@@ -4110,15 +4114,15 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
     const bool pair_on = NT >= 512 && pair_x && cs && !trust && len >= 2;
     if (NT >= 512 && pair_x && m3_w4 && w == 4) {  // (option pair_m3w: the third- and fourth-smallest by a wave of its own)
 #if ZBPE_PAIR_MIN4
-        uint64_t q[5];
+        uint64_t q[6];
         uint32_t hmx;
-        wave_minK<5>(list, len, q, hmx);
-        if (lane == 0) { s_m3 = q[2]; s_m4 = q[3]; s_m5 = q[4]; }
+        wave_minK<6>(list, len, q, hmx);
+        if (lane == 0) { s_m3 = q[2]; s_m4 = q[3]; s_m5 = q[4]; s_m6 = q[5]; }
 #else
         uint64_t p1, p2, p3;
         uint32_t hmx;
         wave_min3(list, len, p1, p2, p3, hmx);
-        if (lane == 0) { s_m3 = p3; s_m4 = ~0ull; s_m5 = ~0ull; }
+        if (lane == 0) { s_m3 = p3; s_m4 = ~0ull; s_m5 = ~0ull; s_m6 = ~0ull; }
 #endif
     }
     if (NT >= 256 && plan_on && w == 3 && len) {
@@ -4172,6 +4176,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                 st->pr_h3 = len >= 3 ? (uint32_t)(s_m3 >> 32) : 0u;
                 st->pr_h4 = len >= 4 && s_m4 != ~0ull ? (uint32_t)(s_m4 >> 32) : 0u;
                 st->pr_h5 = len >= 5 && s_m5 != ~0ull ? (uint32_t)(s_m5 >> 32) : 0u;
+                st->pr_h6 = len >= 6 && s_m6 != ~0ull ? (uint32_t)(s_m6 >> 32) : 0u;
                 st->pr_hmax = hmax;
                 // chain: the third-smallest home's key for merge X+2 (found with the fourth, wave 4)
                 const uint32_t k3 = (uint32_t)s_m3;
@@ -4180,8 +4185,12 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                 st->pr_key2 = c2 ? k3 : NO_ID;
                 // chain depth 2 (option pair_chain 2): the fourth key, merge X+3's candidate
                 const uint32_t k4 = (uint32_t)s_m4;
-                st->pr_key3 = c2 && chain2 && len >= 4 && s_m4 != ~0ull && (k4 & 0xFFFF) != (k4 >> 16) && (len == 4 || s_m5 != ~0ull)
-                                  ? k4 : NO_ID;
+                const bool c3 = c2 && chain2 && len >= 4 && s_m4 != ~0ull && (k4 & 0xFFFF) != (k4 >> 16) && (len == 4 || s_m5 != ~0ull);
+                st->pr_key3 = c3 ? k4 : NO_ID;
+                // depth 3 (option pair_chain 3): the fifth key, merge X+4's
+                const uint32_t k5 = (uint32_t)s_m5;
+                st->pr_key4 = c3 && chain3 && len >= 5 && s_m5 != ~0ull && (k5 & 0xFFFF) != (k5 >> 16) && (len == 5 || s_m6 != ~0ull)
+                                  ? k5 : NO_ID;
                 st->pr_plan_gen = 0xFFFFFFFFu;  // (the replace's extra workgroup loads the plan)
                 st->pr_births = 0;
                 st->pr_dt = 0;
@@ -4254,7 +4263,7 @@ struct NextArgs {
     int pair;             // option pair_select (DevState::pr_*)
     int skip_refresh;     // option pair_refresh 0: a pair select's refresh workgroups leave the dirty blocks to the next launch
     int m3_w4;            // option pair_m3w: the decision's third-smallest home by wave 4 (else wave 0)
-    int chain;            // option pair_chain: a pair select names merge X+2's candidate (needs skip_refresh, m3_w4); 2: and X+3's
+    int chain;            // option pair_chain: a pair select names merge X+2's candidate (needs skip_refresh, m3_w4); 2: and X+3's; 3: X+4's
     uint32_t *spec_clear; // pair scans: merge X's spare delta buffer (nullptr: off)
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
@@ -4653,17 +4662,19 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 // new pairs of both merges) and plan come from merge X+1's replace, whose home summaries are
                 // still the decision's (this launch refreshed none)
                 const PairTail &PT = *reinterpret_cast<const PairTail *>(&st->pr_plan[0]);
-                const uint32_t key2 = PT.key2, key3 = PT.key3, h3 = PT.h3, h4 = PT.h4, h5 = PT.h5;
+                const uint32_t key2 = PT.key2, key3 = PT.key3, key4 = PT.key4, h3 = PT.h3, h4 = PT.h4, h5 = PT.h5, h6 = PT.h6;
                 if (!h && N.skip_refresh && key2 != NO_ID && N.B.X + 1 < N.x_end) {
                     st->pr_key = key2;  // the chain moves up one: key2 -> key, key3 -> key2, their flags with them
                     st->pr_key2 = key3;
-                    st->pr_key3 = NO_ID;
+                    st->pr_key3 = key4;
+                    st->pr_key4 = NO_ID;
                     const uint32_t ties0 = s_p0[P0_TIES], dt0 = s_p0[P0_DT];
                     st->pr_ties = ties0 - 1u;
-                    st->pr_dt = (dt0 & 0xFFFFu) | (((dt0 >> 19) & 1u) << 16) | (((dt0 >> 20) & 1u) << 19);
+                    st->pr_dt = (dt0 & 0xFFFFu) | (((dt0 >> 19) & 1u) << 16) | (((dt0 >> 20) & 1u) << 19) | (((dt0 >> 21) & 1u) << 20);
                     st->pr_h2 = h3;
                     st->pr_h3 = h4;
                     st->pr_h4 = h5;
+                    st->pr_h5 = h6;
                     st->pr_slack = ties0 == 3u ? 0xFFFFFFFFu : 0u;  // (the third was the last tied key)
                     st->pr_plan_gen = 0xFFFFFFFFu;
                     st->pr_x = N.B.X + 1;
@@ -4833,7 +4844,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
                               plan_on, plan, N.gen, N.trust != 0, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u, N.m3_w4 != 0,
-                              N.skip_refresh != 0 && N.chain != 0, N.chain >= 2);
+                              N.skip_refresh != 0 && N.chain != 0, N.chain >= 2, N.chain >= 3);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }

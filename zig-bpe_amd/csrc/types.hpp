@@ -113,7 +113,8 @@ struct DevState {
     // candidate's and the next one's (pr_h2, pr_h3), the one after (pr_h4) and the largest (pr_hmax)
     uint32_t pr_key2, pr_key3;        // (pr_key3: merge X+3's, option pair_chain 2; bit 20 of pr_dt: decremented)
     uint32_t pr_h2, pr_h3, pr_h4, pr_hmax, pr_h5;
-    uint32_t pr_pad2[11];
+    uint32_t pr_key4, pr_h6;          // (merge X+4's, option pair_chain 3; bit 21)
+    uint32_t pr_pad2[9];
     // Pair scans (option pair_scan): the scan of merge X also walks merge X+1's candidate (pr_key) into a spare
     // delta buffer, its records after merge X's in the arena, and flags (sp_touch) any of its occurrences
     // that touches one of merge X's; the scan of merge X+1 then only hands the walk over when its pair is
@@ -129,8 +130,9 @@ struct PairHead {  // what the light test reads (the kernel entry's round trip)
 struct PairTail {  // what a pair select then reads (plan, chain)
     uint32_t plan[6], key2, key3;
     uint32_t h2, h3, h4, hmax, h5;
+    uint32_t key4, h6;
 };
-static_assert(sizeof(PairHead) == 32 && sizeof(PairTail) == 52, "pair head: 8 words, tail: 13");
+static_assert(sizeof(PairHead) == 32 && sizeof(PairTail) == 60, "pair head: 8 words, tail: 15");
 // DevState's hot header as one value (StateHead load_head(st))
 struct StateHead {
     uint32_t halt, cur_key, arena_top, lists_valid, lists_x, top_count, theta, hot_len, rec_count;
