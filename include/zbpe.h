@@ -168,7 +168,15 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * (train: list scan when list length * ratio < stream slots), "encode_list_ratio" (the same for encode), "list_start" (build the lists at a compaction
  * once top count * list_start < live tokens; 0: at the first compaction), "compact_den_lists" (compact_den
  * once lists are on), "print_runtime" (0: no generateInitialTokens
- * runtime line on stderr). */
+ * runtime line on stderr), "pair_select" (0/1, default 1: a tied merge's decision qualifies the next
+ * merge's winner, whose select then skips the argmax and the decision), "pair_chain"
+ * (0-3, default 2: a pair select passes that on to up to this many further merges), "pair_refresh"
+ * (0/1, default 0: a pair select's home refresh is left to the next full select; 1 disables chains),
+ * "pair_m3w" (0/1: the decision's further tied homes by a wave of their own), "pair_scan" (0/1: the scan
+ * also walks the next merge's candidate; only in a build with -DZBPE_PAIR_SCAN=1), "lp_lazy" (0/1,
+ * default 1: the stream's last pair is looked up only for a tie whose Zig capacity depends on it),
+ * "refresh_wgs" (home refresh workgroups of a select), "tie_trust" (timing experiment only: ties by
+ * the smallest home, unverified). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* printTimeStats (src/utils/time_statistics.zig:36-60): the reference's "Time statistics" text for
