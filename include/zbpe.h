@@ -79,15 +79,16 @@ typedef struct zbpe_stats {
     /* merges whose winner the previous merge's tie decision qualified (option "pair_select"): their select
      * skipped the argmax and the Zig-order decision */
     uint64_t pair_selects;
-    /* merges whose scan the previous merge's scan had done beside its own (option "pair_scan") */
-    uint64_t pair_scans;
+    /* merges applied by multi-merge rounds beyond each round's first (option "round_k"): their scan,
+     * replace and select launches were shared with the round's first merge */
+    uint64_t round_merges;
 } zbpe_stats;
 
 /* Layout version of zbpe_stats. The struct is caller-allocated and has grown across versions: a
  * consumer compares zbpe_stats_size() with the size of the zbpe_stats of the header it was built against
  * before passing a zbpe_stats: the library writes zbpe_stats_size() bytes.
  *   1: up to tie_fallbacks ... list_builds;  2: + replications, phase split, sharded_merges;
- *   3: + tie_crosschecks, generate_tokens_s;  4: + pair_selects, pair_scans. */
+ *   3: + tie_crosschecks, generate_tokens_s;  4: + pair_selects, round_merges. */
 #define ZBPE_STATS_VERSION 4
 size_t zbpe_stats_size(void);
 
@@ -172,11 +173,9 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * merge's winner, whose select then skips the argmax and the decision), "pair_chain"
  * (0-3, default 2: a pair select passes that on to up to this many further merges), "pair_refresh"
  * (0/1, default 0: a pair select's home refresh is left to the next full select; 1 disables chains),
- * "pair_m3w" (0/1: the decision's further tied homes by a wave of their own), "pair_scan" (0/1: the scan
- * also walks the next merge's candidate; only in a build with -DZBPE_PAIR_SCAN=1), "lp_lazy" (0/1,
+ * "pair_m3w" (0/1: the decision's further tied homes by a wave of their own), "lp_lazy" (0/1,
  * default 1: the stream's last pair is looked up only for a tie whose Zig capacity depends on it),
- * "refresh_wgs" (home refresh workgroups of a select), "tie_trust" (timing experiment only: ties by
- * the smallest home, unverified). */
+ * "refresh_wgs" (home refresh workgroups of a select). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* printTimeStats (src/utils/time_statistics.zig:36-60): the reference's "Time statistics" text for
@@ -233,6 +232,13 @@ zbpe_status zbpe_scan_log(zbpe_ctx *ctx, int32_t *out, size_t cap, size_t *n);
  * preceded; arena_rep: the replicated occurrence-arena fill it was decided on). Sharded ranks must agree
  * on every row (compactions are decided on replicated quantities). Copies up to cap_rows rows of 2 u32. */
 zbpe_status zbpe_compaction_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_t *n_rows);
+
+/* Profiling diagnostic: one row {merge token X, reason, host microseconds} per device-resident batch of the
+ * last train that halted (the device could not finish merge X alone and the host's synchronous path did).
+ * reason: 2 hot-list argmax to rebuild, 3 Zig map capacity changed (home histogram rebuild), 4 tie the
+ * cluster test left undecided (exact emulation), 5 self pair, 6 occurrence arena too small. Host
+ * microseconds: from the batch's return to the end of that synchronous merge. Copies up to cap_rows rows. */
+zbpe_status zbpe_halt_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_t *n_rows);
 
 /* Host-only diagnostic (no device work): the Zig 0.13 pair-map iteration order emulation used by
  * the exact tie fallback. Given every live pair's first-occurrence position, key (first |

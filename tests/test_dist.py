@@ -1,6 +1,8 @@
 """Multi-rank (sharded) training. CPU: the host-collective plumbing with gloo, world_size 2.
-GPU: 2-3 ranks sharing one MI355X (collectives through gloo) must give the oracle's merges --
-shard boundaries, self-pair runs crossing shards, ties resolved by the exact path."""
+GPU: 2, 3, 4 and 8 ranks sharing one MI355X (collectives through gloo) must give the oracle's merges --
+shard boundaries (7 of them at world 8, self-pair run parities chained across all of them), the
+first-occurrence min-reduce over every rank, ties resolved by the exact path -- and C3 (world 8) and C4
+(worlds 2 and 4) must equal their full goldens across the replication hand-over."""
 import numpy as np
 import pytest
 
@@ -73,9 +75,15 @@ def case_id(c) -> str:
     return name + "".join(f"-{k}{v}" for k, v in c.get("options", {}).items())
 
 
+# worlds 4 and 8 (BASELINE config 4 is chunk-sharded over 8 MI355X): the cases whose shards interact most --
+# words (lists, replication), run-heavy (self-pair parities across 3 and 7 shard edges), sharded to the end,
+# a shrunken arena that must grow, skewed shards, and tiny texts where most of the 8 shards are empty
+WIDE = [CASES[0], CASES[1], CASES[3], CASES[6], CASES[7], CASES[9], CASES[10], CASES[13]]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("case", CASES, ids=case_id)
+@pytest.mark.parametrize("world,case", [(w, c) for w in (2, 3) for c in CASES] + [(w, c) for w in (4, 8) for c in WIDE],
+                         ids=lambda x: f"w{x}" if isinstance(x, int) else case_id(x))
 def test_sharded_training_matches_oracle(world, case):
     text = case_text(case)
     ref = O.train(text, case["vocab"])
@@ -157,31 +165,60 @@ def test_sharded_corpus_over_4GiB(tmp_path):
     assert (r1.pair, r1.count) == ((m[1][0], m[1][1]), c[1])
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(1100)
-def test_sharded_c4_world2_vs_golden():
-    """C4 itself (1 GiB, vocab 32000) sharded over 2 ranks that share the GPU (host collectives): every merge and
-    count equals the C4 golden (the fast oracle's full run when committed, else the literal oracle's prefix);
-    the run crosses the replication hand-over (sharded merges, then one gather, then replicas), and both ranks
-    compact at the same merges on the same replicated arena fill."""
+def handover_merge(g: dict, n_bytes: int, world: int, list_start: int = 64) -> int:
+    """the first merge k at which the sharded ranks may replicate (Engine::run_batch): the top count times
+    list_start times world is below the live tokens before merge k (the golden's counts and stream lengths)"""
+    live = [n_bytes] + g["len_after"]
+    return next(k for k in range(len(g["counts"])) if g["counts"][k] * list_start * world < live[k])
+
+
+def check_sharded_vs_golden(g: dict, case: dict, world: int, timeout: int):
+    """`world` ranks sharing the GPU (host collectives) train the case's corpus: every rank's merges and counts
+    equal the golden; the run crosses the replication hand-over, which happens at the first batch start at or
+    after the golden's hand-over merge (batches hold up to 32 merges); every rank shards the same merges and
+    compacts at the same merges on the same replicated arena fill. Returns the sharded merge count."""
+    out = run(train_worker, world, case, timeout=timeout)
+    K = g["n_merges"]
+    k0 = handover_merge(g, case["n"], world)
+    for r in range(world):
+        _, m, c, st, clog = out[r]
+        assert len(m) == case["vocab"] - 256
+        assert m[:K] == g["merges"] and c[:K] == g["counts"], f"rank {r}"
+        assert st["replications"] == 1 and k0 <= st["sharded_merges"] < k0 + 32, (r, st["sharded_merges"], k0)
+        assert out[r][1] == out[0][1] and out[r][2] == out[0][2]
+        assert st["sharded_merges"] == out[0][3]["sharded_merges"]
+        assert out[r][4] == out[0][4] and len(out[r][4]) >= 2  # compactions: same merges, same replicated arena fill
+    if g["complete"]:
+        assert out[0][3]["final_tokens"] == g["len_after"][-1]
+    print(f"HANDOVER corpus={case['n']} world={world} golden_handover={k0} sharded_merges={out[0][3]['sharded_merges']} "
+          f"sharded_s={out[0][3]['sharded_s']:.3f} replicate_s={out[0][3]['replicate_s']:.3f} replicated_s={out[0][3]['replicated_s']:.3f}")
+    return out[0][3]["sharded_merges"]
+
+
+def _golden(name):
     import json
     import os
 
     from helpers import GOLDEN
 
-    full = os.path.join(GOLDEN, "large_c4_words_utf8_1GiB_v32000.json")
-    path = full if os.path.exists(full) else os.path.join(GOLDEN, "large_c4_words_utf8_1GiB_v32000_prefix.json")
-    with open(path) as f:
-        g = json.load(f)
-    case = dict(kind="words_utf8", seed=0x5EED0004, n=1 << 30, vocab=32000)
-    out = run(train_worker, 2, case, timeout=1000)
-    K = g["n_merges"]
-    for r in (0, 1):
-        _, m, c, st, clog = out[r]
-        assert len(m) == 32000 - 256
-        assert m[:K] == g["merges"] and c[:K] == g["counts"], f"rank {r}"
-        assert st["replications"] == 1 and 0 < st["sharded_merges"] < len(m), f"rank {r}"
-    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
-    assert out[0][3]["sharded_merges"] == out[1][3]["sharded_merges"]
-    assert out[0][4] == out[1][4] and len(out[0][4]) >= 2  # compactions: same merges, same replicated arena fill
-    assert out[0][3]["final_tokens"] == g["len_after"][-1] if g["complete"] else True
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(1100)
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_c4_vs_golden(world):
+    """C4 itself (1 GiB, vocab 32000) over 2 and 4 ranks sharing the GPU: the full C4 golden (all 31,744 merges,
+    counts, final length), across the replication hand-over"""
+    g = _golden("large_c4_words_utf8_1GiB_v32000.json")
+    check_sharded_vs_golden(g, dict(kind="words_utf8", seed=0x5EED0004, n=1 << 30, vocab=32000), world, 1000)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_sharded_c3_world8_vs_golden():
+    """C3 (64 MiB, vocab 4096) over 8 ranks sharing the GPU: the full C3 golden (all 3,840 merges, counts, final
+    length); 7 shard edges, the 8-way first-occurrence min-reduce of every exact tie in the sharded phase"""
+    g = _golden("large_c3_words_utf8_64MiB_v4096.json")
+    check_sharded_vs_golden(g, dict(kind="words_utf8", seed=0x5EED0003, n=64 << 20, vocab=4096), 8, 550)

@@ -42,7 +42,7 @@ def main():
                           "scan_s": st.scan_kernel_s,
                           "scan_alg_GBps": st.scan_timed_alg_bytes / max(st.scan_kernel_s, 1e-12) / 1e9, "ev_count_s": st.count_pairs_s, "ev_select_s": st.sort_pairs_s,
                           "ev_replace_s": st.replace_pair_s, "list_scans": st.list_scans,
-                          "pair_selects": getattr(st, "pair_selects", 0), "pair_scans": getattr(st, "pair_scans", 0), "tie_iterations": st.tie_iterations}), flush=True)
+                          "pair_selects": getattr(st, "pair_selects", 0), "round_merges": getattr(st, "round_merges", 0), "tie_iterations": st.tie_iterations}), flush=True)
         e.close()
     eng.close()
 

@@ -34,7 +34,7 @@ def run(out, opts):
     m, c, st = e.train_resident(32000)
     log = e.merge_log()
     json.dump({"scan_log": e.scan_log().tolist(), "ties": log[:, 3].tolist(), "count": log[:, 1].tolist(),
-               "live": log[:, 2].tolist()},
+               "live": log[:, 2].tolist(), "halts": e.halt_log().tolist(), "total_s": st.total_s},
               open(out, "w"))
     print(f"{len(m)} merges, {st.total_s:.3f} s")
     e.close()
@@ -93,7 +93,36 @@ def analyse(d, logp):
         if "zbpe_scan_pairs_t" in nxt[2]:
             add(b, "gap_select_scan", (nxt[0] - sel[1]) / 1e3)
             add(b, "merge_total", (nxt[0] - s[0]) / 1e3)
+    # wall time per bucket from the trace: the first scan launch of the bucket's first merge to the next bucket's
+    # (everything in between: kernels, gaps, batch-boundary syncs, halts and their host path, compactions)
+    first = {}
+    for j, x in enumerate(slog):
+        if x >= 0:
+            first.setdefault(x >> 1, ks[scans[j]][0])
+    wall = {}
+    for b in buckets:
+        lo = min((m for m in first if m >= b[0]), default=None)
+        hi = min((m for m in first if m >= b[1]), default=None)
+        if lo is None:
+            continue
+        t1 = first[hi] if hi is not None else ks[-1][1]
+        n = (hi if hi is not None else len(ties)) - lo
+        wall[b] = ((t1 - first[lo]) / 1e3, n)
+    # halted batches: reason -> count and host-path microseconds, by bucket
+    names = {2: "hot_list_rebuild", 3: "zig_capacity", 4: "undecided_tie", 5: "self_pair", 6: "arena"}
+    halts = {b: {} for b in buckets}
+    for x, reason, us in L.get("halts", []):
+        b = next(bb for bb in buckets if bb[0] <= x - 256 < bb[1])
+        h = halts[b].setdefault(names.get(reason, str(reason)), [0, 0.0])
+        h[0] += 1
+        h[1] += us
     out = {}
+    for b in buckets:
+        key = f"merges [{b[0]}, {b[1] if b[1] < 1 << 30 else 'end'})"
+        if b in wall:
+            out[key + " wall"] = {"ms": round(wall[b][0], 2), "merges": wall[b][1], "us_per_merge": round(wall[b][0] * 1e3 / max(1, wall[b][1]), 2)}
+        out[key + " halts"] = {k: {"n": v[0], "host_us_avg": round(v[1] / v[0], 1), "host_ms": round(v[1] / 1e3, 2)}
+                               for k, v in sorted(halts[b].items())}
     for b in buckets:
         out[f"merges [{b[0]}, {b[1] if b[1] < 1 << 30 else 'end'})"] = {
             k: {"avg_us": round(v[0] / v[1], 2), "p50_us": round(sorted(v[2])[len(v[2]) // 2], 2), "n": v[1]}

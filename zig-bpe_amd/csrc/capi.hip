@@ -1,7 +1,4 @@
 // extern "C" entry points declared in include/zbpe.h.
-#ifndef ZBPE_PAIR_SCAN
-#define ZBPE_PAIR_SCAN 0  // (as kernels.hpp: pair scans compiled in)
-#endif
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -159,13 +156,11 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "list_ratio" && value >= 1) e.list_ratio = (uint32_t)value;
     else if (k == "dense_hist" && (value == 0 || value == 1)) e.dense_hist = (int)value;
     else if (k == "refresh_wgs" && value >= 0) e.refresh_wgs = (uint32_t)value;
-    else if (k == "tie_trust" && (value == 0 || value == 1)) e.tie_trust = (int)value;
     else if (k == "lp_lazy" && (value == 0 || value == 1)) e.lp_lazy = (int)value;
     else if (k == "pair_select" && (value == 0 || value == 1)) e.pair_select = (int)value;
     else if (k == "pair_refresh" && (value == 0 || value == 1)) e.pair_refresh = (int)value;
     else if (k == "pair_m3w" && (value == 0 || value == 1)) e.pair_m3w = (int)value;
     else if (k == "pair_chain" && value >= 0 && value <= 3) e.pair_chain = (int)value;
-    else if (k == "pair_scan" && (value == 0 || (value == 1 && ZBPE_PAIR_SCAN))) e.pair_scan = (int)value;  // (1: a build with -DZBPE_PAIR_SCAN=1)
     else if (k == "encode_list_ratio" && value >= 1) e.enc_list_ratio = (uint32_t)value;
     else if (k == "list_start" && value >= 0) e.list_start = (uint64_t)value;
     else if (k == "hot_target" && value > 0) e.hot_target = (uint64_t)value;
@@ -262,6 +257,15 @@ zbpe_status zbpe_compaction_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, 
     *n_rows = l.size() / 2;
     const size_t k = std::min(cap_rows, *n_rows);
     if (k) memcpy(rows, l.data(), k * 2 * sizeof(uint32_t));
+    return ZBPE_OK;
+}
+
+zbpe_status zbpe_halt_log(zbpe_ctx *ctx, uint32_t *rows, size_t cap_rows, size_t *n_rows) {
+    if (!ctx || !n_rows || (!rows && cap_rows)) return ZBPE_INVALID_ARGUMENT;
+    const auto &l = ctx->eng.halt_log;
+    *n_rows = l.size() / 3;
+    const size_t k = std::min(cap_rows, *n_rows);
+    if (k) memcpy(rows, l.data(), k * 3 * sizeof(uint32_t));
     return ZBPE_OK;
 }
 

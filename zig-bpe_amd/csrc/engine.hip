@@ -59,8 +59,7 @@ void Engine::release() {
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_cs); f(d_rtk); f(d_sizes);
-    f(d_enc_cnt); f(d_enc_ctr); f(d_nb); f(d_ord_pos); f(d_ord_ent); f(d_sort_tmp); f(d_spec);
-    d_spec = nullptr;
+    f(d_enc_cnt); f(d_enc_ctr); f(d_nb); f(d_ord_pos); f(d_ord_ent); f(d_sort_tmp);
     f(d_dir); f(d_dir_row); f(d_row_tok); f(d_dir_tmp); f(d_sort_hist);
     d_dir = d_dir_row = d_row_tok = d_sort_hist = nullptr; d_dir_tmp = nullptr;
     dir_cap = dir_row_cap = row_tok_cap = dir_tmp_cap = sort_hist_cap = 0;
@@ -100,8 +99,6 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipMalloc(&d_st, sizeof(DevState)));
     HIP_OK(hipMalloc(&d_delta, 2 * DELTA_WORDS * sizeof(uint32_t)));  // two: merges alternate (delta_of)
     HIP_OK(hipMemset(d_delta, 0, 2 * DELTA_WORDS * sizeof(uint32_t)));
-    HIP_OK(hipMalloc(&d_spec, 2 * DELTA_WORDS * sizeof(uint32_t)));  // pair scans' spare deltas (spec_of)
-    HIP_OK(hipMemset(d_spec, 0, 2 * DELTA_WORDS * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&T.tok_cnt, 65536 * sizeof(int32_t)));
     HIP_OK(hipMalloc(&d_log, 65536 * sizeof(MergeLog)));
@@ -292,7 +289,8 @@ bool Engine::holes_over() const {
 }
 
 zbpe_status Engine::compact_train(uint32_t X) {
-    compact_log.push_back(X);  // (h_st: the state as of the last sync; every caller synced since its last merge)
+    CHECK(sync_state());  // the arena fill logged is the device's now, whatever the caller last synced
+    compact_log.push_back(X);
     compact_log.push_back(h_st->arena_rep);
     HIP_OK(hipEventRecord(ev[3], stream));
     CHECK(compact());
@@ -1032,6 +1030,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     run.vocab = vocab_size;
     trace.clear();
     compact_log.clear();
+    halt_log.clear();
     scan_log.clear();
     std::fill(h_log.begin(), h_log.end(), MergeLog{});
     uint32_t X = 256;
@@ -1051,10 +1050,19 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             X += done;
             if (!halted) continue;
             // the device stopped at merge X: clear the flag, make the selection valid, finish X here
+            const uint32_t reason = h_st->halt;
+            const double t_h = now_s();
             HIP_OK(hipMemsetAsync(&d_st->halt, 0, 4, stream));
             CHECK(sync_state());
             CHECK(select_ready());
             if (h_st->live <= 0) continue;
+            const double t_m = now_s();
+            CHECK(merge_sync(X));
+            (was_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_m;
+            if (was_sharded) stats.sharded_merges++;
+            halt_log.insert(halt_log.end(), {X, reason, (uint32_t)std::min(4e9, (now_s() - t_h) * 1e6)});
+            X++;
+            continue;
         }
         const bool was_sharded = dist();
         const double t_m = now_s();
@@ -1144,7 +1152,6 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
     stats.distinct_pairs = (uint64_t)std::max(h_st->live, 0);
     stats.pair_selects = h_st->pr_hits;
-    stats.pair_scans = h_st->sp_hits;
     stats.pair_ids = h_st->num_ids;
     trained = true;
     if (out_stats) *out_stats = stats;
@@ -1188,13 +1195,6 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // the refresh counts of zbpe_select_next: each launch zeroes the next one's, unless this batch
     // does not continue the last one's launches
     if (fused_select && !begun) HIP_OK(hipMemsetAsync(d_rtk, 0, RTK_WORDS * sizeof(uint32_t), stream));
-    // pair scans: a batch that does not continue the last one's launches (host-path merges ran between) starts
-    // from clean spare buffers and slots (the selects keep them clean inside a run of batches)
-    const bool pair_scan_on = ZBPE_PAIR_SCAN && pair_scan && pair_select && fused_select && !dist();
-    if (pair_scan_on && !begun) {
-        HIP_OK(hipMemsetAsync(d_spec, 0, 2 * DELTA_WORDS * sizeof(uint32_t), stream));
-        HIP_OK(hipMemsetAsync(&d_st->sp[0], 0, sizeof(d_st->sp), stream));
-    }
     if (dist()) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
     const uint64_t C = home_slots;
     const uint32_t nb = (uint32_t)((C + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
@@ -1234,17 +1234,16 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
                    lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log, nullptr, (int)sel_prof};
         set_list_nb(A);
         A.gen = layout_gen;
-        A.spec_left = pair_scan_on ? spec_of(X + 1) : nullptr;
         // a batch that follows one of list scans only launches a smaller grid (fewer idle workgroups
         // to dispatch); a stream scan still completes on it, only slower
         CHECK(launch_scan(A, list_streak ? list_grid : 0, top0));
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 2], stream));
         CHECK(comm_sum(left, 2ull * X + 2));
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 3], stream));
-        const int pair_blk = fused_select && pair_select && !tie_trust && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS ? 1 : 0;
+        const int pair_blk = fused_select && pair_select && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS ? 1 : 0;
         ReplaceArgs R{d_tok[cur], slots, d_lists, (uint32_t)lists_cap, left, right, tail, 0, 0, X, 0, ab, halo, nullptr,
                       1, dist() ? d_halo : nullptr, 1, (int)sel_prof, pair_blk, d_summ, d_sup, (uint32_t)C, nb, nsb, cs,
-                      A.dir_row, A.dir, A.dir_w, layout_gen, scan_plan && lists_on ? 1 : 0, pair_scan_on ? spec_of(X) : nullptr};
+                      A.dir_row, A.dir, A.dir_w, layout_gen, scan_plan && lists_on ? 1 : 0};
         if (!replace_split) {
             zbpe_replace<<<ab + update_blocks(X, update_per(X)) + pair_blk, 256, 0, stream>>>(d_st, R.left, R.X, R.apply_blocks, R, T);
         } else {  // profiling: apply and count update as two launches (no pair-select bound)
@@ -1273,10 +1272,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
             NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
-                       dist() ? world : 1, (int)sel_prof, tie_trust ? nullptr : cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
-                       scan_plan && lists_on ? 1 : 0, tie_trust ? 1 : 0, lp_lazy, pair_select, pair_refresh ? 0 : 1, pair_m3w, pair_chain,
-                       pair_scan_on ? spec_of(X) : nullptr};
-            const uint32_t nref = C && !tie_trust ? (refresh_wgs ? std::min<uint32_t>(nsb, refresh_wgs) : nsb) : 0u;
+                       dist() ? world : 1, (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
+                       scan_plan && lists_on ? 1 : 0, lp_lazy, pair_select, pair_refresh ? 0 : 1, pair_m3w, pair_chain};
+            const uint32_t nref = C ? (refresh_wgs ? std::min<uint32_t>(nsb, refresh_wgs) : nsb) : 0u;
             zbpe_select_next<<<sel + nref, NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hcnt, T.hot_cap, nref, sel,
                                                                                  d_tok[cur], slots, T, d_partial, left, X, N);
             LAUNCH_OK();

@@ -46,9 +46,6 @@ struct Engine {
     // scan merge X + 1 into the other buffer while its own merge's words are still being cleared)
     uint32_t *d_delta = nullptr, *d_hist = nullptr;
     uint32_t *delta_of(uint32_t X) const { return d_delta + (size_t)(X & 1) * DELTA_WORDS; }
-    // pair scans (option pair_scan): merge X's spare delta buffer, filled by the scan of merge X-1 (DevState::sp)
-    uint32_t *d_spec = nullptr;
-    uint32_t *spec_of(uint32_t X) const { return d_spec + (size_t)(X & 1) * DELTA_WORDS; }
 
     // multi-GPU: this rank's shard and its neighbours' boundary tokens
     int rank = 0, world = 1;
@@ -152,10 +149,8 @@ struct Engine {
     int pair_select = 1;        // option "pair_select": a tied merge's decision qualifies the next merge's winner (DevState::pr_*)
     int pair_refresh = 0;       // option "pair_refresh": 1 = a pair select's refresh workgroups still refresh the dirty home blocks
     int pair_m3w = 1;           // option "pair_m3w": the decision's third-smallest tied home by a wave of its own
-    int pair_scan = 0;          // option "pair_scan": a scan also walks the next merge's candidate (DevState::sp)
     int pair_chain = 2;         // option "pair_chain": a pair select names the next merge's candidate too (1: three merges per decision, 2: four)
     int lp_lazy = 1;            // option "lp_lazy": the select looks the stream's last pair up only when a tie's capacity needs it
-    int tie_trust = 0;          // option "tie_trust": TIMING EXPERIMENT ONLY -- ties taken by smallest home, unverified
     int dense_hist = 1;         // option "dense_hist": the full pair histogram of a byte stream counts every byte pair in a fixed 16-bit LDS bin
     uint32_t list_ratio = 96;   // training: list scan when list length * ratio < stream slots
     uint32_t enc_list_ratio = 48;   // the same for encode (option "encode_list_ratio")
@@ -166,6 +161,9 @@ struct Engine {
     std::vector<float> trace;
     std::vector<int32_t> scan_log;  // per pair-scan launch of the last train (zbpe_scan_log)
     std::vector<uint32_t> compact_log;  // per training compaction: merge X, arena_rep (zbpe_compaction_log)
+    // per halted device-resident batch of the last train (zbpe_halt_log): merge X, HaltReason, host-path
+    // microseconds (from the batch's return to the end of the synchronous merge that finished X)
+    std::vector<uint32_t> halt_log;
     // encode: merges applied per launch pair (option "encode_batch"; 1 = one merge at a time)
     uint32_t enc_batch = 32;
     uint64_t enc_batches = 0;       // launch pairs of the last encode

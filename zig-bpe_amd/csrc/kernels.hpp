@@ -13,15 +13,6 @@
 
 #include "types.hpp"
 
-#ifndef ZBPE_PAIR_SCAN
-#define ZBPE_PAIR_SCAN 0  // pair scans compiled in (option pair_scan; 0: the scan, replace and select kernels have no trace of them)
-#endif
-#ifndef ZBPE_PAIR_MIN4
-#define ZBPE_PAIR_MIN4 1  // decide_body: the pair-select chain's fourth-smallest home (0: min3 only, no chains past two)
-#endif
-#ifndef ZBPE_LP_CACHE
-#define ZBPE_LP_CACHE 1  // zbpe_select_next: the stream's last pair id cached in the state head (0: looked up every merge)
-#endif
 namespace zbpe {
 // DevState's hot header in one round trip: every word is loaded here at kernel entry, before any
 // branch on them (the empty asm makes each value live at this point, so the compiler issues the
@@ -380,9 +371,6 @@ __device__ inline int64_t prev_live(const uint16_t *tok, int64_t i) {
 // ones, the common neighbours once merges are long) in a small LDS hash of (token << 16 | count)
 // with a few linear probes, and only the rest straight to HBM. Contended global atomics on a few hot
 // neighbour tokens cost more than the whole list walk of a late merge.
-#ifndef ZBPE_LIST_WIDE
-#define ZBPE_LIST_WIDE 0  // list scans: load each entry's neighbour words with its vector (A/B build switch)
-#endif
 constexpr int HASH_LOG = 9;
 constexpr int HASH_BINS = 1 << HASH_LOG;
 struct NeighbourHist {
@@ -468,12 +456,6 @@ struct ScanArgs {
     uint32_t top_count;
     uint32_t plan_ok;
     uint32_t pl[6];
-    // pair scans (option pair_scan, batch mode): the spare delta buffer of merge X+1's candidate walk
-    // (nullptr: off), and in that walk the merged pair whose occurrences it must not touch (touch_out nullptr:
-    // not such a walk)
-    uint32_t *spec_left;
-    uint32_t touch_key;
-    uint32_t *touch_out;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // batching pays below about one occurrence per 400 slots and costs above it (tools/scan_bands.py:
@@ -501,7 +483,7 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0, const StateHead
     ScanArgs A{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
                A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
                A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb, A0.batch,
-               A0.dir_row, A0.dir, A0.dir_w, A0.gen, H.top_count, 0u, {}, A0.spec_left, 0u, nullptr};
+               A0.dir_row, A0.dir, A0.dir_w, A0.gen, H.top_count, 0u, {}};
     // batch mode: the plan the select stored with this merge's pair, for the current lists
     A.plan_ok = A0.dyn && H.plan_x == A0.X && H.plan_key == pair_key(a, b) && H.plan_gen == A0.gen ? 1u : 0u;
     A.pl[0] = H.plan_la; A.pl[1] = H.plan_lb; A.pl[2] = H.plan_oa; A.pl[3] = H.plan_ob; A.pl[4] = H.plan_r0; A.pl[5] = H.plan_r1;
@@ -723,18 +705,8 @@ __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64
                 if (r_occ) xx++;
                 else H.right((uint16_t)tr);
             }
-            if (ZBPE_PAIR_SCAN && hit && A.touch_out) {
-                // pair scan: does this occurrence touch one of the merged pair (ta, tb)'s? Its left neighbour
-                // ends one (L = tb after ta), its right neighbour starts one (R = ta before tb), or it shares a
-                // token with one (a == tb after ta at L, b == ta before tb at R); unknown past the window: yes
-                const uint32_t ta = A.touch_key & 0xFFFFu, tb = A.touch_key >> 16, tl = win(l), tr = win(r);
-                const bool t = (tl == tb && (ll < 0 || win(ll < 0 ? 0 : ll) == ta)) || (tr == ta && (rn >= 14 || win(rn > 13 ? 13 : rn) == tb)) ||
-                               (A.a == tb && tl == ta) || (A.b == ta && tr == tb);
-                if (t) atomicOr(A.touch_out, 1u);
-            }
         } else {
             hit = occ_slow(A, H, p, xx);
-            if (ZBPE_PAIR_SCAN && hit && A.touch_out) atomicOr(A.touch_out, 1u);  // (not resolved here: counted as touching)
         }
         if (hit) hits |= 1u << k;
     }
@@ -897,11 +869,10 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
                                                                          ScanLds &S, uint32_t vb, uint32_t vg, bool all = false);
 // one pair scan with resolved arguments: the list form when the shorter token list is short
 // enough, else the stream form
-// (vb, vg: this workgroup among the vg that walk a list; spec: a pair scan's candidate walk, list forms
-// only -- returns whether it walked)
+// (vb, vg: this workgroup among the vg that walk a list)
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false, bool BATCH = false>
-__device__ __attribute__((always_inline)) inline bool scan_dispatch(const ScanArgs &A, ScanLds &S, const StateHead &H,
-                                                                    uint32_t vb, uint32_t vg, bool spec = false) {
+__device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S, const StateHead &H,
+                                                                    uint32_t vb, uint32_t vg) {
     // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
     const uint32_t lists_x = H.lists_x;
     if (A.lists && A.a != A.b && H.lists_valid) {
@@ -927,7 +898,7 @@ __device__ __attribute__((always_inline)) inline bool scan_dispatch(const ScanAr
         // a's list sorted by build-time successor (a long list): by the invariant below, every occurrence
         // is in the range of successor b -- about the pair's count of entries, wherever a's list is
         if (ranged) {
-            if (vb == 0 && threadIdx.x == 0 && !spec) {
+            if (vb == 0 && threadIdx.x == 0) {
                 A.st->scan_mode = 1;
                 if (A.log) {
                     A.log[A.X - 256].mode = 1;
@@ -937,9 +908,8 @@ __device__ __attribute__((always_inline)) inline bool scan_dispatch(const ScanAr
                 }
                 if (PROF) A.st->pp_t[4] = 1;
             }
-            if (spec && vb == 0 && threadIdx.x == 0) A.st->sp[A.X & 1].len = r1 - r0;
             scan_list_filtered<PROF>(A, false, r0, r1 - r0, S, vb, vg, true);
-            return true;
+            return;
         }
         // Both tokens existed when the lists were built: since then a position's successor (its
         // predecessor) has only ever changed into a token created after the build (a merge at the
@@ -949,7 +919,7 @@ __device__ __attribute__((always_inline)) inline bool scan_dispatch(const ScanAr
         // (coalesced) and gathers the stream only where it matches: ~count gathers, not ~len.
         const bool NB = A.nb && A.a < lists_x && A.b < lists_x;
         if (len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n) {
-            if (vb == 0 && threadIdx.x == 0 && !spec) {
+            if (vb == 0 && threadIdx.x == 0) {
                 A.st->scan_mode = 1;
                 if (A.log) {
                     A.log[A.X - 256].mode = 1;
@@ -958,16 +928,13 @@ __device__ __attribute__((always_inline)) inline bool scan_dispatch(const ScanAr
                 }
                 if (PROF) A.st->pp_t[4] = 1;
             }
-            if (spec && vb == 0 && threadIdx.x == 0) A.st->sp[A.X & 1].len = len;
             if (NB) scan_list_filtered<PROF>(A, by_b, by_b ? ob : oa, len, S, vb, vg);
             else scan_list_body<PROF>(A, by_b, A.lists + (by_b ? ob : oa), len, S, nullptr, vb, vg);
-            return true;
+            return;
         }
     }
-    if (spec) return false;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
     scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH>(A, S);
-    return true;
 }
 // the scan plan says this merge's scan walks a list (scan_dispatch's test, on the plan's words)
 __device__ inline bool plan_is_list(const ScanArgs &A, const StateHead &H) {
@@ -1001,66 +968,6 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
     if (A0.dyn && H.halt) return;
     __shared__ ScanLds S;
     const ScanArgs A = scan_args_resolve(A0, H);
-    if (ZBPE_PAIR_SCAN && A0.spec_left) {  // pair scans (option pair_scan; batch mode, one GPU or replicas)
-        DevState *st = A0.st;
-        const SpecHead SP = st->sp[A0.X & 1];  // (written by the last scan for this merge)
-        const uint32_t px = st->pr_x, pk = st->pr_key;
-        if (SP.x == A0.X && SP.key == H.cur_key && SP.gen == A0.gen && SP.touch == 0) {
-            // the last scan walked this merge (merge X-1 touched none of its occurrences, so the walk over
-            // the stream before merge X-1 found what one now would): records in place after merge X-1's,
-            // deltas in the spare buffer (the replace reads them there); hand over the counts
-            if (blockIdx.x == 0 && threadIdx.x == 0) {
-                st->rec_count = SP.rec;
-                A0.xx_out[0] = SP.xx;
-                A0.occ_out[0] = SP.occ;
-                st->sp_hit = A0.X;
-                st->sp_hits++;
-                st->scan_mode = 1;
-                if (A0.log) {
-                    A0.log[A0.X - 256].mode = 1;
-                    A0.log[A0.X - 256].list_len = SP.len;
-                }
-            }
-            return;
-        }
-        // the candidate of merge X+1 (pr_x, pr_key) is walked beside this merge's list walk, by the grid's
-        // upper half, when both walks are list walks and the arena holds both merges' records
-        const uint32_t half = gridDim.x / 2;
-        const bool spec = px == A0.X + 1 && pk != NO_ID && (pk & 0xFFFFu) != (pk >> 16) && half >= 1 && plan_is_list(A, H) &&
-                          (uint64_t)H.arena_top + 2ull * H.top_count <= (uint64_t)A0.rec_cap;
-        if (spec) {
-            if (blockIdx.x >= half) {
-                ScanArgs B = A;
-                B.a = pk & 0xFFFFu;
-                B.b = pk >> 16;
-                B.left = A0.spec_left;
-                B.right = A0.spec_left + (A0.X + 1);
-                B.X = A0.X + 1;
-                B.rec = A.rec + H.top_count;  // after merge X's records (its count: every occurrence is one)
-                B.rec_cap = A.rec_cap > H.top_count ? A.rec_cap - H.top_count : 0u;
-                SpecHead *sn = &st->sp[(A0.X + 1) & 1];  // (zeroed by the last select)
-                B.rec_ctr = &sn->rec;
-                B.xx_out = &sn->xx;
-                B.occ_out = &sn->occ;
-                B.log = nullptr;
-                B.prof = 0;
-                B.plan_ok = 0;
-                B.pres = nullptr;
-                B.touch_key = H.cur_key;
-                B.touch_out = &sn->touch;
-                const uint32_t vb = blockIdx.x - half;
-                if (scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, false, BATCH>(B, S, H, vb, gridDim.x - half, true) && vb == 0 &&
-                    threadIdx.x == 0) {
-                    sn->key = pk;
-                    sn->gen = A0.gen;
-                    sn->x = A0.X + 1;
-                }
-                return;
-            }
-            scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF, BATCH>(A, S, H, blockIdx.x, half);
-            return;
-        }
-    }
     scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF, BATCH>(A, S, H, blockIdx.x, gridDim.x);
 }
 
@@ -1363,35 +1270,16 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
         uint4 cvs[LU];
 #pragma unroll
         for (int u = 0; u < LU; u++) cvs[u] = tv[(ps[u] < 0 ? 0 : ps[u]) >> 3];
-#if ZBPE_LIST_WIDE
-        // the window's neighbour words with the vector (no second round trip for a candidate)
-        uint32_t pws[LU];
-        uint2 nvs[LU];
-#pragma unroll
-        for (int u = 0; u < LU; u++) {
-            const int64_t vi = (ps[u] < 0 ? 0 : ps[u]) >> 3;
-            pws[u] = tv[vi > 0 ? vi - 1 : 0].w;
-            nvs[u] = *reinterpret_cast<const uint2 *>(&tv[vi + 1 < nvec ? vi + 1 : vi]);
-        }
-#endif
 #pragma unroll 1
         for (int u = 0; u < LU; u++) {
             // this entry's values (selects, not an indexed private array)
             int64_t p = ps[0];
             uint4 cv = cvs[0];
-#if ZBPE_LIST_WIDE
-            uint32_t wpw = pws[0];
-            uint2 wnv = nvs[0];
-#endif
 #pragma unroll
             for (int k2 = 1; k2 < LU; k2++)
                 if (u == k2) {
                     p = ps[k2];
                     cv = cvs[k2];
-#if ZBPE_LIST_WIDE
-                    wpw = pws[k2];
-                    wnv = nvs[k2];
-#endif
                 }
             bool cand = false;
             if (p >= 0) {
@@ -1404,17 +1292,12 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
             uint32_t pw = 0xffffffffu, nx = 0xffffffffu, ny = 0xffffffffu;
             if (cand) {
                 const int64_t vi = p >> 3;
-#if ZBPE_LIST_WIDE
-                if (vi > 0) pw = wpw;
-                if (vi + 1 < nvec) { nx = wnv.x; ny = wnv.y; }
-#else
                 if (vi > 0) pw = tv[vi - 1].w;
                 if (vi + 1 < nvec) {
                     const uint2 nv = *reinterpret_cast<const uint2 *>(&tv[vi + 1]);
                     nx = nv.x;
                     ny = nv.y;
                 }
-#endif
             }
             bool hit = false;
             uint32_t pr = 0;
@@ -2464,7 +2347,6 @@ struct ReplaceArgs {
     const uint32_t *dir_row, *dir;  // the candidate's scan plan (ScanArgs::dir_row, dir, dir_w)
     uint32_t dir_w, gen;
     int plan;
-    uint32_t *spec_left;  // pair scans: this merge's spare delta buffer (its walk by the last scan; nullptr: off)
 };
 // pair selects: merge X+1's candidate bound, by the replace's extra workgroup (defined with the home views below)
 __device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Summ *sup, uint32_t C, uint32_t nb,
@@ -2489,19 +2371,11 @@ __device__ inline void update_preload(const uint32_t *left, const uint32_t *righ
 // R.apply_blocks; right = left + X), so they issue at entry beside the state head.
 __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t *__restrict__ left, uint32_t Xp, uint32_t apply_blocks,
                                                     ReplaceArgs R, Tables T) {
-    uint32_t dv[UPD_MAX_PER], dv2[UPD_MAX_PER];
+    uint32_t dv[UPD_MAX_PER];
     const uint32_t per = update_per(Xp);
     if (blockIdx.x >= apply_blocks) update_preload(left, left + Xp, Xp, blockIdx.x - apply_blocks, per, dv);
-    // pair scans: the spare buffer's deltas too (which one holds this merge's is in the state)
-    if (ZBPE_PAIR_SCAN && R.spec_left && blockIdx.x >= apply_blocks) update_preload(R.spec_left, R.spec_left + Xp, Xp, blockIdx.x - apply_blocks, per, dv2);
     const StateHead H = load_head(st);  // (with the deltas: one round trip)
     const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key, pr_key2 = st->pr_key2, pr_key3 = st->pr_key3, pr_key4 = st->pr_key4;
-    if (ZBPE_PAIR_SCAN && R.spec_left && st->sp_hit == R.X) {  // this merge's walk was the last scan's candidate walk
-#pragma unroll
-        for (int k = 0; k < UPD_MAX_PER; k++) dv[k] = dv2[k];
-        R.left = R.spec_left;
-        R.right = R.spec_left + Xp;
-    }
     const uint32_t theta = H.theta;
     if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the list scan's stamps
         const unsigned long long now = wall_clock64();
@@ -4053,11 +3927,9 @@ template <int NT = DECIDE_THREADS>
 __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, const uint64_t *list, uint32_t len, uint32_t total, const HomeView &V,
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
-                                   uint32_t plan_gen = 0, bool trust = false, uint32_t pair_x = 0, bool m3_w4 = false,
+                                   uint32_t plan_gen = 0, uint32_t pair_x = 0, bool m3_w4 = false,
                                    bool chain = false, bool chain2 = false, bool chain3 = false) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
-    // trust (option tie_trust, a TIMING EXPERIMENT only, never a default): the smallest home wins with no
-    // cluster or wrap test -- what a decision costs without the home summaries
     // plan (NT >= 256): wave 3 finds the smallest home's key itself and loads its scan plan during the
     // carries; the commit below stores it with cur_key
     __shared__ uint32_t s_plan[6];
@@ -4092,10 +3964,8 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
         }
         if (lane == 0 && !(NT >= 512 && pair_x && m3_w4)) { s_m3 = m3; s_m4 = ~0ull; s_m5 = ~0ull; s_m6 = ~0ull; }
         const uint32_t h1 = (uint32_t)(m1 >> 32);
-        const int64_t f = !len ? -1 : trust ? (int64_t)V.C : cs ? wave_first_free(V, h1, wave_carry_from_super(V, cs, h1)) : wave_free_from(V, h1);
+        const int64_t f = !len ? -1 : cs ? wave_first_free(V, h1, wave_carry_from_super(V, cs, h1)) : wave_free_from(V, h1);
         if (lane == 0) { s_free = f; s_m1 = m1; s_m2 = m2; s_hmax = hmax; }
-    } else if (trust) {
-        if (w == 1 && lane == 0) { s_c0 = 0; s_last = -2; }
     } else if (cs) {  // carry into slot 0 and the wrap test's last free slot: precomputed (refresh_prefix)
         if (w == 1 && lane == 0) {
             s_c0 = (int32_t)ld_wt(cs);
@@ -4111,19 +3981,12 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
     // pair_x (merge X+1 = pair_x, NT >= 512, precomputed carries): the second-smallest home's key is merge
     // X+1's candidate; wave 0 also finds the third-smallest home (merge X's replace bounds the free slots
     // between them and loads the candidate's scan plan: pair_slack_block)
-    const bool pair_on = NT >= 512 && pair_x && cs && !trust && len >= 2;
+    const bool pair_on = NT >= 512 && pair_x && cs && len >= 2;
     if (NT >= 512 && pair_x && m3_w4 && w == 4) {  // (option pair_m3w: the third- and fourth-smallest by a wave of its own)
-#if ZBPE_PAIR_MIN4
         uint64_t q[6];
         uint32_t hmx;
         wave_minK<6>(list, len, q, hmx);
         if (lane == 0) { s_m3 = q[2]; s_m4 = q[3]; s_m5 = q[4]; s_m6 = q[5]; }
-#else
-        uint64_t p1, p2, p3;
-        uint32_t hmx;
-        wave_min3(list, len, p1, p2, p3, hmx);
-        if (lane == 0) { s_m3 = p3; s_m4 = ~0ull; s_m5 = ~0ull; s_m6 = ~0ull; }
-#endif
     }
     if (NT >= 256 && plan_on && w == 3 && len) {
         uint64_t m1 = ~0ull;
@@ -4133,7 +3996,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
         if (lane == 0) plan_compute(plan, (uint32_t)m1, s_plan);
     }
     __syncthreads();
-    if (!ws && !cs && !trust) {  // a map of at most 4096 slots: the last free slot needs the carry into slot 0
+    if (!ws && !cs) {  // a map of at most 4096 slots: the last free slot needs the carry into slot 0
         if (w == 2) {
             const int64_t lf = s_c0 > 0 ? wave_last_free(V, 0, V.C, s_c0) : -2;
             if (lane == 0) s_last = lf;
@@ -4147,7 +4010,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
     uint32_t verdict = total > len ? 1u : 0u;
     const int64_t s = s_free;  // first free slot at or after h1
     if (s < 0) verdict = 1;     // the run of h1 wraps (or is absurdly long)
-    if (!trust && m2 != ~0ull && s > (int64_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
+    if (m2 != ~0ull && s > (int64_t)(m2 >> 32)) verdict = 1;  // second tied pair in the same run
     const long long lf = s_c0 > 0 ? s_last : -2;  // -2: no run wraps past slot C-1
     if (lf != -2 && (lf < 0 || (long long)hmax >= lf + 1)) verdict = 1;  // a tied pair may have wrapped
     st->tie_verdict = verdict;
@@ -4234,7 +4097,9 @@ constexpr int NEXT_CAND = 64;          // keys kept per argmax block at the bloc
 constexpr int NEXT_MAX_SEL = 1024;     // argmax blocks (the reducer keeps one LDS entry per block)
 constexpr int SEL_U = 8;               // hot entries per argmax thread per step (loads issued together)
 constexpr int NEXT_TIE_LDS = 512;      // tied keys the decision reads from LDS (more: from N.tie_list)
-constexpr unsigned long long SPIN_LIMIT_TICKS = 2000000ull;  // 20 ms of wall_clock64 (100 MHz): bounded spin-waits
+// bounded spin-waits: 1 s of wall_clock64 (100 MHz). Only a guard against a broken dispatch-order assumption, not a
+// performance limit: a queue time-sliced away (several processes on one GPU) can stall a wait for many ms
+constexpr unsigned long long SPIN_LIMIT_TICKS = 100000000ull;
 struct NextArgs {
     BeginArgs B;          // merge X + 1 (B.X < x_end)
     uint32_t x_end;       // vocab size: no merge starts at x_end
@@ -4255,7 +4120,6 @@ struct NextArgs {
     const uint32_t *dir_row, *dir;
     uint32_t dir_w, gen;
     int plan;
-    int trust;            // option tie_trust (timing experiment): no refresh workgroups, no cluster test
     // option lp_lazy: the stream's last pair count (the Zig map's final grow) is looked up by the last block
     // only for a tie whose capacity depends on it, not by argmax wave 1 at every merge (its dependent loads
     // held the argmax block's max behind them)
@@ -4264,7 +4128,6 @@ struct NextArgs {
     int skip_refresh;     // option pair_refresh 0: a pair select's refresh workgroups leave the dirty blocks to the next launch
     int m3_w4;            // option pair_m3w: the decision's third-smallest home by wave 4 (else wave 0)
     int chain;            // option pair_chain: a pair select names merge X+2's candidate (needs skip_refresh, m3_w4); 2: and X+3's; 3: X+4's
-    uint32_t *spec_clear; // pair scans: merge X's spare delta buffer (nullptr: off)
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -4348,10 +4211,6 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // critical path: the argmax grid is sized by the hot list alone; nothing in this launch reads
         // [0, 2X) -- the roll reads the tail words past it)
         for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
-        if (ZBPE_PAIR_SCAN && N.spec_clear) {  // pair scans: merge X's spare deltas (read by its replace) and the slot merge X+2's walk fills
-            for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) N.spec_clear[t] = 0;
-            if (blockIdx.x == 0 && tid < 8) reinterpret_cast<uint32_t *>(&st->sp[X & 1])[tid] = 0u;
-        }
         if (N.pair && N.skip_refresh) {  // a pair select: no decision in this launch reads the summaries
             const PairHead P0 = *reinterpret_cast<const PairHead *>(&st->pr_x);
             if (pair_light(N.pair, N.B.X, N.x_end, N.V.C, P0, st->live)) return;
@@ -4496,7 +4355,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 uint32_t lp = 0;
                 if (got == 2) {
                     const uint32_t key = pair_key(lt[1], lt[0]);
-                    if (ZBPE_LP_CACHE && key == H0.lp_key && c_key == key && H0.lp_id < c_nid && H0.lp_id < T.id_cap) {
+                    if (key == H0.lp_key && c_key == key && H0.lp_id < c_nid && H0.lp_id < T.id_cap) {
                         lp = c_cnt;
                     } else {
                         const uint32_t id = ht_find(T, key);
@@ -4799,29 +4658,33 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // dispatching a grid's workgroups in id order: the refresh workgroups (ids [0, nref)) were
         // dispatched before this argmax workgroup, so none of them waits for a slot this one holds.
         // pfx: the top counter reaches the groups + the prefix's arrival; else the XCD counters sum to nref
-        // Bounded: a wait past SPIN_LIMIT_TICKS (a broken dispatch-order assumption) sets error bit 1024
-        // (sync_state fails the train) and the decision goes on with whatever summaries it reads.
+        // Bounded: a wait past SPIN_LIMIT_TICKS (a broken dispatch-order assumption) reads the counters once
+        // more and, still short, sets error bit 1024 (sync_state fails the train); the decision goes on with
+        // whatever summaries it reads.
         const uint32_t *rtk = N.rtk + (X & 1) * RTK_SET;
         const unsigned long long t_spin = wall_clock64();
         if (pfx) {
-            while (ld_wt(rtk + 8 * RTK_STRIDE) < min(nref, 8u) + 1u) {
+            const uint32_t want = min(nref, 8u) + 1u;
+            while (ld_wt(rtk + 8 * RTK_STRIDE) < want) {
                 __builtin_amdgcn_s_sleep(1);
                 if (wall_clock64() - t_spin > SPIN_LIMIT_TICKS) {
-                    if (tid == 0) atomicOr(&st->error, 1024u);
+                    if (tid == 0 && ld_wt(rtk + 8 * RTK_STRIDE) < want) atomicOr(&st->error, 1024u);
                     break;
                 }
             }
         } else {
-            for (;;) {
+            for (bool last = false;;) {
                 uint32_t c = tid < 8 ? ld_wt(rtk + tid * RTK_STRIDE) : 0u;
 #pragma unroll
                 for (int off = 4; off >= 1; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off);
-                if ((uint32_t)__shfl((int)c, 0) >= nref) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - t_spin > SPIN_LIMIT_TICKS) {
+                const bool done = (uint32_t)__shfl((int)c, 0) >= nref;
+                if (done) break;
+                if (last) {  // timed out, and the counters read once more are still short
                     if (tid == 0) atomicOr(&st->error, 1024u);
                     break;
                 }
+                __builtin_amdgcn_s_sleep(1);
+                last = wall_clock64() - t_spin > SPIN_LIMIT_TICKS;
             }
         }
     }
@@ -4843,7 +4706,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
-                              plan_on, plan, N.gen, N.trust != 0, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u, N.m3_w4 != 0,
+                              plan_on, plan, N.gen, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u, N.m3_w4 != 0,
                               N.skip_refresh != 0 && N.chain != 0, N.chain >= 2, N.chain >= 3);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();

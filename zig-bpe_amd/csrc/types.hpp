@@ -23,10 +23,6 @@ constexpr int PRES_GROUP = 32;       // presence blocks per bitmap word
 __host__ __device__ constexpr inline uint32_t pair_key(uint32_t first, uint32_t second) { return first | (second << 16); }
 
 // Device-resident state. Host reads a copy after each merge (one small D2H per merge).
-struct SpecHead {  // DevState::sp[]: a pair scan's candidate walk
-    uint32_t x, key, gen, touch, rec, xx, occ, len;
-};
-static_assert(sizeof(SpecHead) == 32, "spec head: 8 words");
 struct DevState {
     // ---- hot header (the first 96 B): the words the merge kernels read first, loaded together in one
     // scalar round trip at kernel entry (StateHead; a chain of dependent state loads was several
@@ -115,14 +111,6 @@ struct DevState {
     uint32_t pr_h2, pr_h3, pr_h4, pr_hmax, pr_h5;
     uint32_t pr_key4, pr_h6;          // (merge X+4's, option pair_chain 3; bit 21)
     uint32_t pr_pad2[9];
-    // Pair scans (option pair_scan): the scan of merge X also walks merge X+1's candidate (pr_key) into a spare
-    // delta buffer, its records after merge X's in the arena, and flags (sp_touch) any of its occurrences
-    // that touches one of merge X's; the scan of merge X+1 then only hands the walk over when its pair is
-    // that candidate (sp_hit = X+1: the replace reads the spare buffer). sp_hits counts them.
-    // Two slots by the candidate merge's parity: the scan of merge X writes slot (X+1) & 1 and reads slot X & 1,
-    // which every select of merge X then zeroes for the scan of merge X+1.
-    alignas(64) SpecHead sp[2];
-    uint32_t sp_hit, sp_hits, sp_pad[14];
 };
 struct PairHead {  // what the light test reads (the kernel entry's round trip)
     uint32_t x, key, slack, ties, births, dt, hits, plan_gen;

@@ -141,7 +141,7 @@ class Stats(ctypes.Structure):
         ("tie_crosschecks", ctypes.c_uint64),
         ("generate_tokens_s", ctypes.c_double),
         ("pair_selects", ctypes.c_uint64),
-        ("pair_scans", ctypes.c_uint64),
+        ("round_merges", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -151,7 +151,7 @@ class Stats(ctypes.Structure):
 EXPORTS = (
     "zbpe_create", "zbpe_comm_unique_id", "zbpe_create_dist", "zbpe_create_dist_host", "zbpe_destroy", "zbpe_last_error",
     "zbpe_train", "zbpe_upload", "zbpe_train_resident", "zbpe_encode", "zbpe_verify_counts", "zbpe_tokens",
-    "zbpe_set_option", "zbpe_format_time_stats", "zbpe_bench_scan", "zbpe_bench_train_scan", "zbpe_merge_log", "zbpe_trace", "zbpe_scan_log", "zbpe_compaction_log", "zbpe_zig_order_winner", "zbpe_version",
+    "zbpe_set_option", "zbpe_format_time_stats", "zbpe_bench_scan", "zbpe_bench_train_scan", "zbpe_merge_log", "zbpe_trace", "zbpe_scan_log", "zbpe_compaction_log", "zbpe_halt_log", "zbpe_zig_order_winner", "zbpe_version",
     "zbpe_stats_size", "zbpe_bench_recount",
 )
 MERGE_LOG_COLUMNS = ("key", "count", "live", "ties", "list_scan", "list_len", "key_live", "range")
@@ -231,6 +231,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.zbpe_trace.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.zbpe_scan_log.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.zbpe_compaction_log.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    L.zbpe_halt_log.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.zbpe_zig_order_winner.argtypes = [vp, vp, vp, sz, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
     L.zbpe_version.restype = ctypes.c_char_p
     for name in EXPORTS:
@@ -383,6 +384,15 @@ class Engine:
         out = np.zeros((n.value, 2), dtype=np.uint32)
         if n.value:
             self._check(self._L.zbpe_compaction_log(self._ctx, _ptr(out), n.value, ctypes.byref(n)), "zbpe_compaction_log")
+        return out
+
+    def halt_log(self) -> np.ndarray:
+        """Per halted device-resident batch of the last train: (merge token X, HaltReason, host-path microseconds)."""
+        n = ctypes.c_size_t(0)
+        self._check(self._L.zbpe_halt_log(self._ctx, None, 0, ctypes.byref(n)), "zbpe_halt_log")
+        out = np.zeros((n.value, 3), dtype=np.uint32)
+        if n.value:
+            self._check(self._L.zbpe_halt_log(self._ctx, _ptr(out), n.value, ctypes.byref(n)), "zbpe_halt_log")
         return out
 
     def tokens(self) -> np.ndarray:
