@@ -41,6 +41,7 @@ class Run:
         self.e = zbpe.Engine(0)
         self.e.upload(self.text)
         self.merges, self.counts, self.stats = self.e.train_resident(vocab)
+        self.log = self.e.merge_log()  # (pair, count, live tokens, tied pairs, ...) per merge
         self.mismatches = self.e.verify_counts()
         fin = self.e.tokens()
         self.final_len = len(fin)
@@ -161,6 +162,8 @@ def test_c4_full_sequence_vs_oracle_golden(c4):
     assert g["complete"] and g["n_merges"] == 31744 and g["tie_replays"]["mismatches"] == 0
     check_vs_golden(c4, g, 31744)
     assert c4.stats.tie_iterations == sum(t > 1 for t in g["ties"])
+    assert c4.log[:, 3].astype(int).tolist() == g["ties"]  # every merge's tied-pair count (rounds derive them)
+    assert c4.log[:, 1].astype(int).tolist() == g["counts"]
     k, ln, fnv = g["fnv64_after"][-1]
     assert k == 31744 and c4.final_len == ln and c4.final_fnv == int(fnv, 16)
     cps = {k: (ln, h) for k, ln, h in g["fnv64_after"]}
@@ -231,6 +234,7 @@ def test_c3_full_sequence_vs_oracle_golden(c3):
     g = large_golden(C3_GOLDEN)
     assert g["complete"] and g["n_merges"] == 3840
     check_vs_golden(c3, g, 3840)
+    assert c3.log[:, 3].astype(int).tolist() == g["ties"]
     k, ln, fnv = g["fnv64_after"][-1]
     assert k == 3840 and c3.final_len == ln and c3.final_fnv == int(fnv, 16)
 

@@ -120,7 +120,9 @@ def analyse(d, logp):
     for b in buckets:
         key = f"merges [{b[0]}, {b[1] if b[1] < 1 << 30 else 'end'})"
         if b in wall:
-            out[key + " wall"] = {"ms": round(wall[b][0], 2), "merges": wall[b][1], "us_per_merge": round(wall[b][0] * 1e3 / max(1, wall[b][1]), 2)}
+            nl = sum(1 for x in slog if x >= 0 and b[0] <= (x >> 1) < b[1])  # scan launches (a multi-merge round: one)
+            out[key + " wall"] = {"ms": round(wall[b][0], 2), "merges": wall[b][1], "us_per_merge": round(wall[b][0] * 1e3 / max(1, wall[b][1]), 2),
+                                  "scan_launches": nl, "merges_per_launch": round(wall[b][1] / max(1, nl), 3)}
         out[key + " halts"] = {k: {"n": v[0], "host_us_avg": round(v[1] / v[0], 1), "host_ms": round(v[1] / 1e3, 2)}
                                for k, v in sorted(halts[b].items())}
     for b in buckets:

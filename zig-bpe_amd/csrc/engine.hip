@@ -59,7 +59,8 @@ void Engine::release() {
     f(d_delta); f(d_st); f(d_rec); f(d_partial); f(d_hist); f(d_bnd_mine); f(d_bnd_all); f(d_x0); f(d_shard_fn); f(d_fns_all);
     f(d_tile_cnt); f(d_tile_off); f(d_tile_fn); f(d_carry); f(d_bitmap); f(d_tie_list);
     f(d_first); f(d_gather); f(d_recount); f(T.hot); f(T.home_cnt); f(d_summ); f(d_count_hist); f(T.home_dirty); f(d_sup); f(d_pres); f(T.tok_cnt); f(d_log); f(d_halo); f(T.lst_off); f(T.lst_len); f(d_list_total); f(d_lists); f(d_list_cnt); f(d_cand); f(d_cs); f(d_rtk); f(d_sizes);
-    f(d_enc_cnt); f(d_enc_ctr); f(d_nb); f(d_ord_pos); f(d_ord_ent); f(d_sort_tmp);
+    f(d_enc_cnt); f(d_enc_ctr); f(d_nb); f(d_ord_pos); f(d_ord_ent); f(d_sort_tmp); f(d_rdelta); f(d_rlog);
+    d_rdelta = d_rlog = nullptr;
     f(d_dir); f(d_dir_row); f(d_row_tok); f(d_dir_tmp); f(d_sort_hist);
     d_dir = d_dir_row = d_row_tok = d_sort_hist = nullptr; d_dir_tmp = nullptr;
     dir_cap = dir_row_cap = row_tok_cap = dir_tmp_cap = sort_hist_cap = 0;
@@ -99,6 +100,10 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipMalloc(&d_st, sizeof(DevState)));
     HIP_OK(hipMalloc(&d_delta, 2 * DELTA_WORDS * sizeof(uint32_t)));  // two: merges alternate (delta_of)
     HIP_OK(hipMemset(d_delta, 0, 2 * DELTA_WORDS * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_rdelta, (size_t)ROUND_MAX * DELTA_WORDS * sizeof(uint32_t)));
+    HIP_OK(hipMemset(d_rdelta, 0, (size_t)ROUND_MAX * DELTA_WORDS * sizeof(uint32_t)));
+    HIP_OK(hipMalloc(&d_rlog, MAX_BATCH * sizeof(uint32_t)));
+    h_rlog.resize(MAX_BATCH);
     HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
     HIP_OK(hipMalloc(&T.tok_cnt, 65536 * sizeof(int32_t)));
     HIP_OK(hipMalloc(&d_log, 65536 * sizeof(MergeLog)));
@@ -1152,6 +1157,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
     stats.distinct_pairs = (uint64_t)std::max(h_st->live, 0);
     stats.pair_selects = h_st->pr_hits;
+    stats.round_merges = h_st->rd_merges;
     stats.pair_ids = h_st->num_ids;
     trained = true;
     if (out_stats) *out_stats = stats;
@@ -1186,16 +1192,6 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         CHECK(sync_state());
         stats.replicate_s += now_s() - t_rep;  // (inside this batch's wall, taken out of sharded_s in train)
     }
-    // headroom for K merges: ids, occurrence records (counts never grow), tie list; compaction
-    CHECK(maybe_grow_tables(X0, K));
-    if (hot_stale) CHECK(rebuild_hot());  // a table rebuild renumbered the ids the tie kernels read
-    const uint32_t top0 = h_st->top_count;
-    if (holes_over() || arena_used() + (uint64_t)K * top0 > arena_limit()) CHECK(compact_train(X0));
-    CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
-    // the refresh counts of zbpe_select_next: each launch zeroes the next one's, unless this batch
-    // does not continue the last one's launches
-    if (fused_select && !begun) HIP_OK(hipMemsetAsync(d_rtk, 0, RTK_WORDS * sizeof(uint32_t), stream));
-    if (dist()) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
     const uint64_t C = home_slots;
     const uint32_t nb = (uint32_t)((C + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
     const HomeView V{T.home_cnt, d_summ, d_sup, (uint32_t)C, nb, nsb};
@@ -1205,12 +1201,40 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         CHECK(ensure(&d_cs, cs_cap, nsb + 1, "home carries"));
         cs = d_cs;
     }
+    // multi-merge rounds: once the merges walk occurrence lists (the last batch only did),
+    // one GPU or replicas, with the naming decisions of the pair selects; a launch triple then does 1 .. round_k
+    // merges, which the device decides (round_valid), so the kernels take the merge index from the state and
+    // the batch's merges are counted after it
+    const bool rounds = round_k >= 2 && !dist() && fused_select && pair_select && refresh_prefix && lists_on && list_streak &&
+                        !replace_split && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS;
+    const uint32_t KM = rounds ? std::min<uint32_t>(K * (uint32_t)round_k, run.vocab - X0) : K;  // merges the batch may do
+    // headroom for KM merges: ids, occurrence records (counts never grow), tie list; compaction
+    CHECK(maybe_grow_tables(X0, KM));
+    if (hot_stale) CHECK(rebuild_hot());  // a table rebuild renumbered the ids the tie kernels read
+    const uint32_t top0 = h_st->top_count;
+    if (holes_over() || arena_used() + (uint64_t)KM * top0 > arena_limit()) CHECK(compact_train(X0));
+    CHECK(ensure(&d_tie_list, tie_list_cap, 1u << 16, "tie list"));
+    // the refresh counts of zbpe_select_next: each launch zeroes the next one's (by X's parity, or the rounds'
+    // launch parity), unless this batch does not continue the last one's launches in the same form
+    if (fused_select && (!begun || rounds != last_rounds)) {
+        HIP_OK(hipMemsetAsync(d_rtk, 0, RTK_WORDS * sizeof(uint32_t), stream));
+        rpar = 0;
+    }
+    last_rounds = rounds;
+    if (rounds) HIP_OK(hipMemsetAsync(d_rlog, 0, K * sizeof(uint32_t), stream));
+    if (dist()) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
+    // rounds: the kernels' bound on the merge index (delta clearing, update grids)
+    const uint32_t Xmax = X0 + KM;
     const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top0 / 256 + 1);
     const int64_t slots = n_slots;
     const double t0 = now_s();
     lists_at_batch = list_streak;  // the last batch only walked lists: sample this one
     if (merge_timing) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * MAX_BATCH], stream));
     for (uint32_t i = 0; i < K; i++) {
+        if (rounds) {
+            CHECK(launch_round(i, X0, Xmax, K, top0, V, cs));
+            continue;
+        }
         const uint32_t X = X0 + i;
         const bool timed = merge_timed(X);
         if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i], stream));
@@ -1288,7 +1312,15 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     CHECK(sync_state());
     const double wall = now_s() - t0;
     batches++;
-    const uint32_t m = h_st->halt ? h_st->halt_at - X0 : K;
+    // rounds: the merges the batch did follow from the state (the last select began cur_x); a round that reached the
+    // vocabulary's end halted the launches after it (HALT_DONE at the end: not a halt of the merge loop)
+    if (rounds && h_st->halt == HALT_DONE && h_st->halt_at == run.vocab) {
+        h_st->halt = 0;
+        h_st->cur_x = run.vocab;
+        HIP_OK(hipMemsetAsync(&d_st->halt, 0, 4, stream));
+    }
+    const uint32_t m = h_st->halt ? h_st->halt_at - X0 : rounds ? h_st->cur_x - X0 : K;
+    if (rounds) HIP_OK(hipMemcpy(h_rlog.data(), d_rlog, K * sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (merge_timing) {
         float ms = 0;
         HIP_OK(hipEventElapsedTime(&ms, bev[BEV_PER_MERGE * MAX_BATCH], bev[BEV_PER_MERGE * MAX_BATCH + 1]));
@@ -1298,7 +1330,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     if (h_st->halt) {
         *halted = true;
         batch_halts++;
-        if (m > K) return fail(ZBPE_INTERNAL, "batch halted at merge %u outside [%u, %u)", h_st->halt_at, X0, X0 + K);
+        if (m > KM) return fail(ZBPE_INTERNAL, "batch halted at merge %u outside [%u, %u)", h_st->halt_at, X0, X0 + KM);
     }
     if (m) HIP_OK(hipMemcpy(h_log.data() + (X0 - 256), d_log + (X0 - 256), m * sizeof(MergeLog), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < m; i++) {
@@ -1322,7 +1354,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         if (L.ties > 1) stats.tie_iterations++;
         if (L.mode) stats.list_scans++;
         float ms_sel = 0, ms_scan = 0, ms_rep = 0, ms_begin = 0, ms_comm = 0;
-        if (merge_timed(X)) {
+        if (!rounds && merge_timed(X)) {
             const hipEvent_t *E = &bev[BEV_PER_MERGE * i];
             const double w = merge_weight();  // the merges this one stands for
             HIP_OK(hipEventElapsedTime(&ms_begin, E[0], E[1]));
@@ -1349,14 +1381,110 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             trace.insert(trace.end(), row, row + ZBPE_TRACE_COLS);
         }
     }
-    for (uint32_t i = 0; i < K; i++)  // every merge of the batch launched one scan; those past a halt returned at once
-        scan_log.push_back(i < m ? (int32_t)(2 * (X0 + i - 256) + (h_log[X0 - 256 + i].mode ? 1 : 0)) : -1);
+    if (rounds) {
+        // launch i's round (rlog: first merge | members << 16; 0: the launch returned at once after a halt); its
+        // events time the whole round, whose merges share them for the stage split
+        for (uint32_t i = 0; i < K; i++) {
+            const uint32_t r = h_rlog[i], x = r & 0xFFFF;
+            scan_log.push_back(r ? (int32_t)(2 * (x - 256) + (h_log[x - 256].mode ? 1 : 0)) : -1);
+            if (r && merge_timing && i % merge_timing == 0) {
+                const hipEvent_t *E = &bev[BEV_PER_MERGE * i];
+                float ms_b = 0, ms_s = 0, ms_r = 0, ms_x = 0;
+                HIP_OK(hipEventElapsedTime(&ms_b, E[0], E[1]));
+                HIP_OK(hipEventElapsedTime(&ms_s, E[1], E[2]));
+                HIP_OK(hipEventElapsedTime(&ms_r, E[3], E[4]));
+                HIP_OK(hipEventElapsedTime(&ms_x, E[4], E[5]));
+                const double w = merge_timing;
+                run.tm_count += w * ms_s * 1e-3;
+                run.tm_replace += w * ms_r * 1e-3;
+                run.tm_select += w * (ms_x + ms_b) * 1e-3;
+                if (!h_log[x - 256].mode) {
+                    stats.scan_kernel_s += ms_s * 1e-3;
+                    stats.scan_timed_launches++;
+                    stats.scan_timed_alg_bytes += 2ull * h_log[x - 256].live;
+                }
+            }
+        }
+    } else {
+        for (uint32_t i = 0; i < K; i++)  // every merge of the batch launched one scan; those past a halt returned at once
+            scan_log.push_back(i < m ? (int32_t)(2 * (X0 + i - 256) + (h_log[X0 - 256 + i].mode ? 1 : 0)) : -1);
+    }
     uint32_t nlist = 0;
     for (uint32_t i = 0; i < m; i++) nlist += h_log[X0 - 256 + i].mode;
     list_streak = m > 0 && nlist == m;
     n_live = h_st->live_tokens;
     if (dist()) halo_from_boundaries();
     *done = m;
+    return ZBPE_OK;
+}
+
+// Launch triple i of a batch of multi-merge rounds (run_batch): the round scan, the round replace and the
+// select, each reading the round's first merge from the state; X0: the batch's first merge (begun by the last
+// batch's select, else here), Xmax: the bound on every merge index of the batch (delta clearing, update grids).
+zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_t K, uint32_t top0, const HomeView &V, uint32_t *cs) {
+    const uint64_t C = V.C;
+    const bool timed = merge_timing && i % merge_timing == 0;
+    if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i], stream));
+    if (i == 0 && !begun) {  // merge X0's start (its select did not run on the device: a halt or a host-path merge)
+        zbpe_tie_collect<<<64, 256, 0, stream>>>(T, d_st, 0, (uint32_t)(C - 1), d_tie_list, (uint32_t)tie_list_cap, 1,
+                                                 BeginArgs{X0, C, (uint32_t)arena_limit(), d_log, 0});
+        LAUNCH_OK();
+        zbpe_home_refresh<<<V.nsb, REFRESH_THREADS, 0, stream>>>(T, d_st, (uint32_t)C, V.nb, d_summ, d_sup, 1);
+        LAUNCH_OK();
+        zbpe_tie_decide<<<1, DECIDE_THREADS, 0, stream>>>(d_st, d_tie_list, (uint32_t)tie_list_cap, V, d_log, 1);
+        LAUNCH_OK();
+    }
+    if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 1], stream));
+    uint32_t *base = d_rdelta;
+    ScanArgs A{d_tok[cur], n_slots, 0, 0, base, base + 65536, d_st, d_lists, (uint32_t)lists_cap, 1, base + 2 * 65536,
+               base + 2 * 65536 + 1, halo, pres_on ? d_pres : nullptr, pres_vp, Xmax, T.tok_cnt, 1, nullptr,
+               lists_on ? d_lists : nullptr, T.lst_off, T.lst_len, list_ratio, 1, d_log, nullptr, 0};
+    set_list_nb(A);
+    A.gen = layout_gen;
+    A.batch = scan_batch;
+    A.round = round_k;
+    A.x_end = run.vocab;
+    A.hv = HomeView{nullptr, d_summ, d_sup, (uint32_t)C, V.nb, V.nsb};
+    A.cs = cs;
+    const int g = list_streak && list_grid > 0 ? list_grid : scan_grid(n_slots);
+    hipLaunchKernelGGL((zbpe_scan_pairs_t<4, true, true, true, true, false, false, true>), dim3(g + RD_FREE_WGS), dim3(SCAN_THREADS),
+                       0, stream, (const DevState *)d_st, A);
+    LAUNCH_OK();
+    if (timed) {
+        HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 2], stream));
+        HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 3], stream));
+    }
+    const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top0 / 256 + 1);
+    const uint32_t pm = ab + update_blocks(Xmax, update_per(Xmax));
+    ReplaceArgs R{d_tok[cur], n_slots, d_lists, (uint32_t)lists_cap, base, base + 65536, base + 2 * 65536, 0, 0, Xmax, 0, ab, halo,
+                  nullptr, 1, nullptr, 1, 0, 0, d_summ, d_sup, (uint32_t)C, V.nb, V.nsb, cs, nullptr, nullptr, 0, layout_gen, 0};
+    R.round = round_k;
+    R.per_member = pm;
+    R.x_end = run.vocab;
+    zbpe_replace_round<<<(uint32_t)round_k * pm, 256, 0, stream>>>(d_st, base, Xmax, ab, R, T);
+    LAUNCH_OK();
+    if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 4], stream));
+    if (hot_stale) CHECK(rebuild_hot());
+    const uint64_t hot_est = std::min<uint64_t>(T.hot_cap, (uint64_t)h_st->hot_len + (uint64_t)K * round_k * sel_growth + sel_margin);
+    const uint64_t work = hot_est / SEL_U;
+    const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
+    // the naming decision must name every member the rounds take: chains up to round_k - 1 further keys
+    const int chain = std::min(3, std::max(pair_chain, round_k - 2));
+    NextArgs N{BeginArgs{Xmax, C, (uint32_t)arena_limit(), d_log, 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
+               d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all, 1,
+               (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen, scan_plan && lists_on ? 1 : 0, lp_lazy, pair_select,
+               1, 1, chain};
+    N.round = round_k;
+    N.par = rpar;
+    N.seq = launch_seq++;
+    N.rlog_i = i;
+    N.rlog = d_rlog;
+    rpar ^= 1u;
+    const uint32_t nref = refresh_wgs ? std::min<uint32_t>(V.nsb, refresh_wgs) : V.nsb;
+    zbpe_select_next<<<sel + nref, NEXT_THREADS, 0, stream>>>(d_st, T.hot, T.hcnt, T.hot_cap, nref, sel, d_tok[cur], n_slots, T,
+                                                              d_partial, base, Xmax, N);
+    LAUNCH_OK();
+    if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 5], stream));
     return ZBPE_OK;
 }
 
@@ -1455,6 +1583,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         float ms;
         float ms_r, ms_s;
         HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1])); run.ev_count += ms * 1e-3;
+        h_log[X - 256] = MergeLog{key, top, (uint32_t)live_before, ties, self ? 0u : h_st->scan_mode, 0, 0, 0};  // (zbpe_merge_log)
         if (!self) {
             scan_log.push_back((int32_t)(2 * (X - 256) + (h_st->scan_mode ? 1 : 0)));
             stats.scan_alg_bytes += 2ull * (uint64_t)n_live;

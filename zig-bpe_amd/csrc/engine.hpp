@@ -46,6 +46,15 @@ struct Engine {
     // scan merge X + 1 into the other buffer while its own merge's words are still being cleared)
     uint32_t *d_delta = nullptr, *d_hist = nullptr;
     uint32_t *delta_of(uint32_t X) const { return d_delta + (size_t)(X & 1) * DELTA_WORDS; }
+    // multi-merge rounds (option round_k): the members' delta buffers (ROUND_MAX of
+    // DELTA_WORDS, fixed layout: left at +0, right at +65536, tail at +131072), the rounds' log of a batch
+    // (d_rlog[i] = the first merge of launch i's round | members << 16), the refresh counters' parity of the
+    // next round select and a launch id (ref_noprefix) that no merge index equals
+    uint32_t *d_rdelta = nullptr, *d_rlog = nullptr;
+    std::vector<uint32_t> h_rlog;
+    uint32_t rpar = 0, launch_seq = 1u << 20;
+    bool last_rounds = false;
+    int round_k = 4;            // option "round_k": members of a multi-merge round (1: no rounds; at most ROUND_MAX)
 
     // multi-GPU: this rank's shard and its neighbours' boundary tokens
     int rank = 0, world = 1;
@@ -257,6 +266,7 @@ struct Engine {
     zbpe_status maybe_grow_tables(uint32_t X, uint32_t k);
     zbpe_status merge_sync(uint32_t X);
     zbpe_status run_batch(uint32_t X0, uint32_t *done, bool *halted);
+    zbpe_status launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_t K, uint32_t top0, const HomeView &V, uint32_t *cs);
     zbpe_status alloc_stream(size_t n);
     zbpe_status generate_initial_tokens(size_t n);
     zbpe_status build_presence();

@@ -165,9 +165,10 @@ __device__ inline void pair_new(const Tables &T, DevState *st, uint32_t key, uin
     if (count >= st->theta) hot_put(T, atomicAdd(&st->hot_len, 1u), id, key, count);
     else T.hpos[id] = NO_ID;
 }
-__device__ inline void pair_dec(const Tables &T, DevState *st, uint32_t key, uint32_t d) {
+// (returns the count before the decrement, 0 for a missing key)
+__device__ inline uint32_t pair_dec(const Tables &T, DevState *st, uint32_t key, uint32_t d) {
     uint32_t id = ht_find(T, key);
-    if (id == NO_ID) { atomicOr(&st->error, 4u); return; }
+    if (id == NO_ID) { atomicOr(&st->error, 4u); return 0; }
     hot_sub(T, id, d);
     uint32_t old = atomicSub(&T.id_cnt[id], d);
     if (old < d) atomicOr(&st->error, 2u);
@@ -175,6 +176,7 @@ __device__ inline void pair_dec(const Tables &T, DevState *st, uint32_t key, uin
         atomicSub(&st->live, 1);
         home_add(T, st, key, false);
     }
+    return old;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -377,7 +379,21 @@ struct NeighbourHist {
     uint32_t *lds_left, *lds_right;
     uint32_t *g_left, *g_right;
     uint32_t *h_left = nullptr, *h_right = nullptr;  // nullptr: no hash (large tokens go to HBM)
-    __device__ static inline void add(uint32_t *lds, uint32_t *h, uint32_t *g, uint16_t t) {
+    // multi-merge rounds: every add to the global deltas returns the old value, so that the workgroup counts the
+    // new pairs (a delta word leaving 0: one per distinct neighbour token, whichever workgroup adds first) and
+    // sees a new pair reaching the top count (the add that completes it); rd = its LDS words {new pairs, top}
+    uint32_t *rd = nullptr;
+    uint32_t top = 0;
+    __device__ inline void gadd(uint32_t *g, uint32_t t, uint32_t v) const {
+        if (!rd) {
+            atomicAdd(&g[t], v);
+            return;
+        }
+        const uint32_t old = atomicAdd(&g[t], v);
+        if (old == 0) atomicAdd(&rd[0], 1u);
+        if (old + v >= top) rd[1] = 1u;
+    }
+    __device__ inline void add(uint32_t *lds, uint32_t *h, uint32_t *g, uint16_t t) const {
         if (t < LDS_BINS) {
             atomicAdd(&lds[t], 1u);
             return;
@@ -395,13 +411,13 @@ struct NeighbourHist {
                     const uint32_t old = atomicAdd(&h[s], 1u);
                     if ((old & 0xffffu) == 0x7fffu) {
                         atomicSub(&h[s], 0x8000u);
-                        atomicAdd(&g[t], 0x8000u);
+                        gadd(g, t, 0x8000u);
                     }
                     return;
                 }
             }
         }
-        atomicAdd(&g[t], 1u);
+        gadd(g, t, 1u);
     }
     __device__ inline void left(uint16_t t) { add(lds_left, h_left, g_left, t); }
     __device__ inline void right(uint16_t t) { add(lds_right, h_right, g_right, t); }
@@ -456,6 +472,17 @@ struct ScanArgs {
     uint32_t top_count;
     uint32_t plan_ok;
     uint32_t pl[6];
+    // multi-merge rounds (zbpe_scan_pairs_t ROUND, batch mode): rounds of up to `round` members (option round_k;
+    // < 2: none) and no member at or past token x_end; the home view the naming decision saw (RoundHead::freeb)
+    int round;
+    uint32_t x_end;
+    HomeView hv;  // (hc unused)
+    const uint32_t *cs;
+    // a member walk (filled by the round scan): the earlier members' keys its occurrences must not touch, and
+    // its RoundHead words
+    uint32_t tk[ROUND_MAX - 1];
+    uint32_t ntk;
+    uint32_t *rd_touch, *rd_top, *rd_birth;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // batching pays below about one occurrence per 400 slots and costs above it (tools/scan_bands.py:
@@ -464,7 +491,8 @@ constexpr uint64_t SCAN_BATCH_DENSITY = 400;
 // the device-held parts of the arguments: pair (batch mode), halo (batch mode, multi-GPU), record
 // window in the arena
 // (H: the state head, load_head at kernel entry)
-__device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0, const StateHead &H) {
+// (X: the merge token, A0.X unless the state names it: a multi-merge round's first member, H.cur_x)
+__device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0, const StateHead &H, uint32_t X) {
     uint32_t a = A0.a, b = A0.b;
     Halo h = A0.halo;
     if (A0.dyn) {
@@ -481,11 +509,11 @@ __device__ inline ScanArgs scan_args_resolve(const ScanArgs &A0, const StateHead
         cap = cap > top ? cap - top : 0;
     }
     ScanArgs A{A0.tok, A0.n, a, b, A0.left, A0.right, A0.st, rec, cap, A0.count_deltas, A0.xx_out, A0.occ_out, h,
-               A0.pres, A0.vp, A0.X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
+               A0.pres, A0.vp, X, A0.tokcnt, 0, nullptr, A0.lists, A0.lst_off, A0.lst_len, A0.list_ratio, 0,
                A0.log, A0.rec_ctr ? A0.rec_ctr : &A0.st->rec_count, A0.prof, A0.nb, A0.batch,
                A0.dir_row, A0.dir, A0.dir_w, A0.gen, H.top_count, 0u, {}};
     // batch mode: the plan the select stored with this merge's pair, for the current lists
-    A.plan_ok = A0.dyn && H.plan_x == A0.X && H.plan_key == pair_key(a, b) && H.plan_gen == A0.gen ? 1u : 0u;
+    A.plan_ok = A0.dyn && H.plan_x == X && H.plan_key == pair_key(a, b) && H.plan_gen == A0.gen ? 1u : 0u;
     A.pl[0] = H.plan_la; A.pl[1] = H.plan_lb; A.pl[2] = H.plan_oa; A.pl[3] = H.plan_ob; A.pl[4] = H.plan_r0; A.pl[5] = H.plan_r1;
     return A;
 }
@@ -637,8 +665,12 @@ __device__ inline void wave_flush_records(const ScanArgs &A, const uint32_t *rec
 // occurrences of (a, b) starting in vector vi (8 tokens) whose bits are set in m, from the window
 // tok[p0-2 .. p0+11] (p0 = 8*vi) given as the previous vector's last dword pw, the vector cv and the
 // next vector's first two dwords nx, ny (holes outside the stream); returns the hit mask.
+// RD: a multi-merge round's member walk -- every occurrence is also tested against the earlier members' pairs
+// (A.tk): does it touch one of their occurrences (share a token with one, or sit next to one)? Then A.rd_touch.
+template <bool RD = false>
 __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64_t vi, uint32_t m, uint32_t &xx,
                                       uint32_t pw, uint4 cv, uint32_t nx, uint32_t ny);
+template <bool RD = false>
 __device__ inline uint32_t occ_vector(const ScanArgs &A, NeighbourHist &H, int64_t vi, int64_t nvec, uint32_t m,
                                       uint32_t &xx) {
     const uint16_t *tok = A.tok;
@@ -651,8 +683,9 @@ __device__ inline uint32_t occ_vector(const ScanArgs &A, NeighbourHist &H, int64
         nx = nv.x;
         ny = nv.y;
     }
-    return occ_window(A, H, vi, m, xx, pw, cv, nx, ny);
+    return occ_window<RD>(A, H, vi, m, xx, pw, cv, nx, ny);
 }
+template <bool RD>
 __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64_t vi, uint32_t m, uint32_t &xx,
                                       uint32_t pw, uint4 cv, uint32_t nx, uint32_t ny) {
     const int64_t n = A.n;
@@ -705,8 +738,26 @@ __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64
                 if (r_occ) xx++;
                 else H.right((uint16_t)tr);
             }
+            if (RD && hit) {
+                // against each earlier member (ta, tb): the left neighbour ends an occurrence of it (unknown before
+                // the window: yes), the right neighbour starts one (unknown past it: yes), or this occurrence shares
+                // a token with one (its a is the tb after a ta, its b the ta before a tb). Any of them is also
+                // what a decrement of this pair by that member needs, so an untouched member keeps its count.
+                const uint32_t tl = win(l), tr = win(r), tll = win(ll < 0 ? 0 : ll), trn = win(rn > 13 ? 13 : rn);
+                bool t = false;
+#pragma unroll
+                for (int e = 0; e < ROUND_MAX - 1; e++) {
+                    if ((uint32_t)e < A.ntk) {
+                        const uint32_t ta = A.tk[e] & 0xFFFFu, tb = A.tk[e] >> 16;
+                        t |= (tl == tb && (ll < 0 || tll == ta)) || (tr == ta && (rn >= 14 || trn == tb)) || (A.a == tb && tl == ta) ||
+                             (A.b == ta && tr == tb);
+                    }
+                }
+                if (t) atomicOr(A.rd_touch, 1u);
+            }
         } else {
             hit = occ_slow(A, H, p, xx);
+            if (RD && hit && A.ntk) atomicOr(A.rd_touch, 1u);  // (not resolved here: counted as touching)
         }
         if (hit) hits |= 1u << k;
     }
@@ -762,6 +813,7 @@ __device__ inline void pres_set(const ScanArgs &A, int64_t pos) {
 // One candidate position p holding the scan's key token (a, or b when by_b): is it (part of) an
 // occurrence of (a, b)? On a hit *pr = the occurrence's start and the deltas are counted. The
 // window around p comes from one 16-B vector (+ its cached neighbours in occ_vector).
+template <bool RD = false>
 __device__ inline bool resolve_candidate(const ScanArgs &A, NeighbourHist &H, int64_t p, bool by_b, int64_t nvec,
                                          uint32_t &xx, uint32_t &pr) {
     const uint16_t *tok = A.tok;
@@ -769,7 +821,7 @@ __device__ inline bool resolve_candidate(const ScanArgs &A, NeighbourHist &H, in
     const int k = (int)(p & 7);
     if (!by_b) {
         pr = (uint32_t)p;
-        return occ_vector(A, H, vi, nvec, 1u << k, xx) != 0;
+        return occ_vector<RD>(A, H, vi, nvec, 1u << k, xx) != 0;
     }
     const uint4 cv = reinterpret_cast<const uint4 *>(tok)[vi];
     int64_t q = -1;  // the live token before p (q < 0: the left shard's, which owns the occurrence)
@@ -782,7 +834,7 @@ __device__ inline bool resolve_candidate(const ScanArgs &A, NeighbourHist &H, in
         q = prev_live_h(A, p);
         if (q >= 0) tq = tok[q];
     }
-    if (q >= 0 && tq == A.a && occ_vector(A, H, q >> 3, nvec, 1u << (q & 7), xx)) {
+    if (q >= 0 && tq == A.a && occ_vector<RD>(A, H, q >> 3, nvec, 1u << (q & 7), xx)) {
         pr = (uint32_t)q;
         return true;
     }
@@ -800,6 +852,7 @@ struct ScanLds {
     unsigned long long scanned;
     uint32_t lrec[LREC_CAP];
     uint32_t lrec_n, lrec_base;
+    uint32_t rd[2];  // multi-merge rounds: {new pairs, a new pair reached the top count} (NeighbourHist::rd)
 };
 // A list walk's wave with hit lanes: stage their record starts `pr` in the workgroup's LDS buffer; lanes
 // past its capacity reserve in the arena directly (one atomic per wave). Every lane of the wave calls it.
@@ -845,6 +898,25 @@ __device__ inline void scan_lds_clear(ScanLds &S) {
     for (int i = threadIdx.x; i < LDS_BINS; i += blockDim.x) { S.left[i] = 0; S.right[i] = 0; }
     for (int i = threadIdx.x; i < HASH_BINS; i += blockDim.x) { S.hleft[i] = 0; S.hright[i] = 0; }
 }
+// the same through a round member walk's returning adds (NeighbourHist::gadd), then the workgroup's counts of
+// new pairs and top-count pairs into the member's RoundHead words (every thread calls it)
+__device__ inline void scan_lds_flush_rd(const ScanArgs &A, ScanLds &S, const NeighbourHist &H) {
+    for (int i = threadIdx.x; i < LDS_BINS; i += blockDim.x) {
+        const uint32_t l = S.left[i], r = S.right[i];
+        if (l) H.gadd(A.left, i, l);
+        if (r) H.gadd(A.right, i, r);
+    }
+    for (int i = threadIdx.x; i < HASH_BINS; i += blockDim.x) {
+        const uint32_t l = S.hleft[i], r = S.hright[i];
+        if (l) H.gadd(A.left, l >> 16, l & 0xffffu);
+        if (r) H.gadd(A.right, r >> 16, r & 0xffffu);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (S.rd[0]) atomicAdd(A.rd_birth, S.rd[0]);
+        if (S.rd[1]) atomicOr(A.rd_top, 1u);
+    }
+}
 // add the workgroup's neighbour histograms to the global deltas (every thread calls it)
 __device__ inline void scan_lds_flush(ScanLds &S, uint32_t *g_left, uint32_t *g_right) {
     for (int i = threadIdx.x; i < LDS_BINS; i += blockDim.x) {
@@ -860,19 +932,18 @@ __device__ inline void scan_lds_flush(ScanLds &S, uint32_t *g_left, uint32_t *g_
 }
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool BATCH = false>
 __device__ __attribute__((always_inline)) inline void scan_pairs_body(const ScanArgs A, ScanLds &S);
-template <bool PROF = false, int NT = SCAN_THREADS>
+template <bool PROF = false, int NT = SCAN_THREADS, bool RD = false>
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
                                                                      uint32_t len, ScanLds &S, const uint16_t *NB,
                                                                      uint32_t vb, uint32_t vg);
-template <bool PROF = false, int NT = SCAN_THREADS>
+template <bool PROF = false, int NT = SCAN_THREADS, bool RD = false>
 __device__ __attribute__((always_inline)) inline void scan_list_filtered(const ScanArgs A, bool by_b, uint32_t off, uint32_t len,
                                                                          ScanLds &S, uint32_t vb, uint32_t vg, bool all = false);
-// one pair scan with resolved arguments: the list form when the shorter token list is short
-// enough, else the stream form
-// (vb, vg: this workgroup among the vg that walk a list)
-template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false, bool BATCH = false>
-__device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S, const StateHead &H,
-                                                                    uint32_t vb, uint32_t vg) {
+// the list forms of one pair scan: true when it walked a list (false: the stream form is the caller's)
+// (RD: a multi-merge round's member walk, round_scan)
+template <bool PROF = false, bool RD = false>
+__device__ __attribute__((always_inline)) inline bool scan_list_dispatch(const ScanArgs &A, ScanLds &S, const StateHead &H,
+                                                                         uint32_t vb, uint32_t vg) {
     // occurrence lists: key the scan by the shorter list when it is much shorter than the stream
     const uint32_t lists_x = H.lists_x;
     if (A.lists && A.a != A.b && H.lists_valid) {
@@ -908,8 +979,8 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
                 }
                 if (PROF) A.st->pp_t[4] = 1;
             }
-            scan_list_filtered<PROF>(A, false, r0, r1 - r0, S, vb, vg, true);
-            return;
+            scan_list_filtered<PROF, SCAN_THREADS, RD>(A, false, r0, r1 - r0, S, vb, vg, true);
+            return true;
         }
         // Both tokens existed when the lists were built: since then a position's successor (its
         // predecessor) has only ever changed into a token created after the build (a merge at the
@@ -928,11 +999,20 @@ __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanAr
                 }
                 if (PROF) A.st->pp_t[4] = 1;
             }
-            if (NB) scan_list_filtered<PROF>(A, by_b, by_b ? ob : oa, len, S, vb, vg);
-            else scan_list_body<PROF>(A, by_b, A.lists + (by_b ? ob : oa), len, S, nullptr, vb, vg);
-            return;
+            if (NB) scan_list_filtered<PROF, SCAN_THREADS, RD>(A, by_b, by_b ? ob : oa, len, S, vb, vg);
+            else scan_list_body<PROF, SCAN_THREADS, RD>(A, by_b, A.lists + (by_b ? ob : oa), len, S, nullptr, vb, vg);
+            return true;
         }
     }
+    return false;
+}
+// one pair scan with resolved arguments: the list form when the shorter token list is short
+// enough, else the stream form
+// (vb, vg: this workgroup among the vg that walk a list)
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false, bool BATCH = false>
+__device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S, const StateHead &H,
+                                                                    uint32_t vb, uint32_t vg) {
+    if (scan_list_dispatch<PROF>(A, S, H, vb, vg)) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
     scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH>(A, S);
 }
@@ -944,9 +1024,121 @@ __device__ inline bool plan_is_list(const ScanArgs &A, const StateHead &H) {
     const uint32_t len = lb < la ? lb : la;
     return len != NO_LIST && (uint64_t)len * A.list_ratio < (uint64_t)A.n;
 }
+// ------------------------------------------------------------------------------------------
+// Multi-merge rounds (option round_k; RoundHead, types.hpp). The scan of a round: the merge (member 0,
+// cur_key) and the tied keys its decision named in home-slot order (pr_key .. pr_key4: members 1..4 for
+// merges cur_x + 1 ..), each walked by its own share of the grid into its own delta buffer (fixed
+// layout: left at +0, right at +65536, tail at +131072) and records (arena_top + j * T: every member has
+// the top count T of occurrences). Member walks also test every occurrence against the earlier members'
+// pairs (occ_window RD: touching) and count their new pairs and top-count pairs (NeighbourHist::gadd);
+// the replace decides from those which members the reference's loop would merge next (round_valid).
+// RD_FREE_WGS extra workgroups bound the free Zig-map slots the members' order depends on, from the home
+// summaries the naming decision saw (as pair_slack_block does for one candidate).
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t RD_FREE_WGS = 2;
+constexpr uint32_t RD_INF = 0xFFFFFFFFu;
+__device__ inline uint32_t rd_delta_words() { return (uint32_t)(2 * 65536 + 64); }  // DELTA_WORDS (engine.hpp)
+__device__ __attribute__((always_inline)) inline int32_t wave_carry_block(const HomeView &V, const uint32_t *cs, uint32_t b);
+__device__ __attribute__((always_inline)) inline int64_t wave_homes_cover(const HomeView &V, uint32_t x, uint32_t y);
+// One wave per range: range 0 = after the largest tied home's block up to C (no tied run may wrap past C-1),
+// range j = after member j's home block up to the next tied home (member j stays first in slot order)
+__device__ inline void round_free(const ScanArgs &A0, uint32_t K, const PairTail &PT, uint32_t w) {
+    DevState *st = A0.st;
+    if (w >= ROUND_MAX || (w > 0 && w >= K)) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t H[ROUND_MAX + 1] = {0u, PT.h2, PT.h3, PT.h4, PT.h5, PT.h6};  // member j's home: H[j]; the next tied one: H[j + 1]
+    const HomeView &V = A0.hv;
+    const bool ok = A0.cs && V.C >= (uint32_t)(SUMM_SLOTS * SUPER_BLOCKS);
+    int64_t f = -1;
+    if (ok) {
+        const uint32_t x = w == 0 ? (PT.hmax / SUMM_SLOTS + 1) * SUMM_SLOTS : (H[w] / SUMM_SLOTS + 1) * SUMM_SLOTS;
+        const uint32_t y = w == 0 ? V.C : H[w + 1];
+        if (w > 0 && y == 0) {
+            f = -1;  // no next tied home (the member is the last tied key: the replace needs no bound)
+        } else if (x < y) {
+            const int64_t c = wave_carry_block(V, A0.cs, x / SUMM_SLOTS);
+            const int64_t h = wave_homes_cover(V, x, y);
+            f = max((int64_t)0, (int64_t)y - x - h - c);
+        } else {
+            f = 0;
+        }
+    }
+    if (lane == 0) st->rd.freeb[w] = (int32_t)min(f, (int64_t)0x7FFFFFFF);
+}
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool BATCH>
+__device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs &A0, const StateHead &H, ScanLds &S) {
+    DevState *st = A0.st;
+    const uint32_t X0 = H.cur_x, T = H.top_count, G = gridDim.x - RD_FREE_WGS;
+    ScanArgs A = scan_args_resolve(A0, H, X0);
+    // the members: merge X0 and the keys its decision named (pr_x == X0 + 1), while every one is a list walk
+    // with room in the arena and below the vocabulary's end
+    const PairHead P = *reinterpret_cast<const PairHead *>(&st->pr_x);
+    const PairTail PT = *reinterpret_cast<const PairTail *>(&st->pr_plan[0]);
+    const uint32_t keys[ROUND_MAX] = {pair_key(A.a, A.b), P.key, PT.key2, PT.key3, PT.key4};
+    uint32_t K = 1;
+    if (A0.round >= 2 && P.x == X0 + 1 && st->pr_full == X0 + 1 && plan_is_list(A, H) && T) {
+        const uint32_t kmax = min(min((uint32_t)A0.round, (uint32_t)ROUND_MAX), A0.x_end > X0 ? A0.x_end - X0 : 1u);
+        while (K < kmax && keys[K] != NO_ID && (uint64_t)(K + 1) * T <= (uint64_t)A.rec_cap) K++;
+    }
+    if (blockIdx.x >= G && K > 1) {  // the free-slot bounds: one wave per range
+        round_free(A0, K, PT, (blockIdx.x - G) * (SCAN_THREADS / 64) + (threadIdx.x >> 6));
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->rd.n = K;
+        st->rd.ties = P.ties;
+        st->rd.live0 = st->live;
+#pragma unroll
+        for (int e = 0; e < ROUND_MAX; e++) st->rd.key[e] = (uint32_t)e < K ? keys[e] : NO_ID;
+    }
+    A.rd_top = &st->rd.top[0];
+    A.rd_birth = &st->rd.birth[0];
+    A.ntk = 0;
+    if (K == 1) {  // a round of one: the merge's own scan (any form; the stream form strides over the whole grid)
+        scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, false, BATCH>(A, S, H, blockIdx.x, gridDim.x);
+        return;
+    }
+    const uint32_t g = G / K, j = min(blockIdx.x / g, K - 1), vb = blockIdx.x - j * g, vg = j == K - 1 ? G - j * g : g;
+    if (j == 0) {
+        scan_list_dispatch<false, true>(A, S, H, vb, vg);  // (a list walk: plan_is_list)
+        return;
+    }
+    // member j: merge X0 + j of pair keys[j]; its list plan (two dependent round trips), then a list walk
+    const uint32_t a = keys[j] & 0xFFFF, b = keys[j] >> 16, dw = rd_delta_words();
+    A.a = a;
+    A.b = b;
+    A.X = X0 + j;
+    A.left = A0.left + (size_t)j * dw;
+    A.right = A.left + 65536;
+    A.xx_out = A.left + 2 * 65536;
+    A.occ_out = A.xx_out + 1;
+    A.rec = A0.rec + H.arena_top + j * T;  // (rec_arena: records in the arena after the lists)
+    A.rec_cap = T;
+    A.rec_ctr = &st->rd.rec[j];
+    A.pres = nullptr;
+    uint32_t la = A.lst_len[a], lb = A.lst_len[b], oa = A.lst_off[a], ob = A.lst_off[b];
+    const uint32_t ra = A.dir_row && a < H.lists_x && b < H.lists_x ? A.dir_row[a] : NO_LIST;
+    uint32_t r0 = NO_LIST, r1 = NO_LIST;
+    if (ra != NO_LIST) {
+        const uint64_t rb = (uint64_t)ra * A.dir_w + b;
+        r0 = A.dir[rb];
+        r1 = A.dir[rb + 1];
+    }
+    A.plan_ok = 1;
+    A.pl[0] = la; A.pl[1] = lb; A.pl[2] = oa; A.pl[3] = ob; A.pl[4] = r0; A.pl[5] = r1;
+#pragma unroll
+    for (int e = 0; e < ROUND_MAX - 1; e++) A.tk[e] = (uint32_t)e < j ? keys[e] : 0u;
+    A.ntk = j;
+    A.rd_touch = &st->rd.touch[j];
+    A.rd_top = &st->rd.top[j];
+    A.rd_birth = &st->rd.birth[j];
+    if (scan_list_dispatch<false, true>(A, S, H, vb, vg) && vb == 0 && threadIdx.x == 0) st->rd.walk[j] = 1;
+}
 // PROF (option sel_prof): the pipeline probes; a separate instantiation, so the production kernel's
 // code and register allocation are untouched by them
-template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false, bool PROF = false, bool BATCH = false>
+// ROUND: the multi-merge round's scan (round_scan; batch mode, one GPU or replicas)
+template <int UNROLL, bool NT, bool FILTER, bool PIPE = true, bool COMPACT = false, bool PROF = false, bool BATCH = false,
+          bool ROUND = false>
 // stp == A0.st, as the leading pointer argument: a build with kernarg preloading (Makefile KP=1) has it in
 // SGPRs at entry, so the state head load needs no kernarg round trip first (aggregates are not preloaded)
 __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(4))) zbpe_scan_pairs_t(const DevState *stp, ScanArgs A0) {
@@ -967,7 +1159,11 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
                  "s"(H.plan_lb), "s"(H.plan_oa), "s"(H.plan_ob), "s"(H.plan_r0), "s"(H.plan_r1));
     if (A0.dyn && H.halt) return;
     __shared__ ScanLds S;
-    const ScanArgs A = scan_args_resolve(A0, H);
+    if (ROUND) {
+        round_scan<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH>(A0, H, S);
+        return;
+    }
+    const ScanArgs A = scan_args_resolve(A0, H, A0.X);
     scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, PROF, BATCH>(A, S, H, blockIdx.x, gridDim.x);
 }
 
@@ -1067,7 +1263,7 @@ constexpr int LIST_EPT = 16;  // the most entries a thread filters
 // (vb, vg: this workgroup's index among the vg workgroups that walk the list; NT threads each)
 // all: every entry of [off, off + len) is a candidate (a successor range, zbpe_list_sort_succ: no
 // neighbour words to filter), at most four per thread.
-template <bool PROF, int NT>
+template <bool PROF, int NT, bool RD>
 __device__ __attribute__((always_inline)) inline void scan_list_filtered(const ScanArgs A, bool by_b, uint32_t off, uint32_t len,
                                                                          ScanLds &S, uint32_t vb, uint32_t vg, bool all) {
     // entries per thread: about one match per two lanes (a wave resolves its matches 64 at a time, one
@@ -1083,10 +1279,11 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     const uint32_t *NB = A.nb, sh = by_b ? 16u : 0u;  // the build-time neighbour on the partner's side
     const uint32_t partner = by_b ? A.a : A.b, key = by_b ? A.b : A.a;
     scan_lds_clear(S);
-    if (threadIdx.x == 0) { S.any = 0; S.lrec_n = 0; }
+    if (threadIdx.x == 0) { S.any = 0; S.lrec_n = 0; S.rd[0] = S.rd[1] = 0; }
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{S.left, S.right, A.left, A.right, S.hleft, S.hright};
+    if (RD) { H.rd = S.rd; H.top = A.top_count; }
     const uint4 *tv = reinterpret_cast<const uint4 *>(A.tok);
     const int64_t nvec = (A.n + 7) / 8;
     const int lane = threadIdx.x & 63;
@@ -1178,17 +1375,17 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
                     const uint32_t nx = vi + 1 < nvec ? nv0.x : 0xffffffffu, ny = vi + 1 < nvec ? nv0.y : 0xffffffffu;
                     if (!by_b) {
                         pr = (uint32_t)p;
-                        hit = occ_window(A, H, vi, 1u << k, xx, pw, cv, nx, ny) != 0;
+                        hit = occ_window<RD>(A, H, vi, 1u << k, xx, pw, cv, nx, ny) != 0;
                     } else {
                         int jb = k - 1;  // the live token before p inside the vector
                         while (jb >= 0 && tok_at(cv, jb) == HOLE) jb--;
                         if (jb >= 0) {
-                            if (tok_at(cv, jb) == A.a && occ_window(A, H, vi, 1u << jb, xx, pw, cv, nx, ny)) {
+                            if (tok_at(cv, jb) == A.a && occ_window<RD>(A, H, vi, 1u << jb, xx, pw, cv, nx, ny)) {
                                 pr = (uint32_t)(vi * 8 + jb);
                                 hit = true;
                             }
                         } else {
-                            hit = resolve_candidate(A, H, p, by_b, nvec, xx, pr);
+                            hit = resolve_candidate<RD>(A, H, p, by_b, nvec, xx, pr);
                         }
                     }
                 }
@@ -1201,12 +1398,14 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     }
     xx = wave_sum(xx);
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
+    if (RD && lane == 0 && xx) atomicOr(A.rd_top, 2u);  // adjacent occurrences: (X, X) is new, (b, a) falls
     if (lane == 0 && any) S.any = 1;
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
     if (S.any) {
         lrec_flush(A, S);
-        scan_lds_flush(S, A.left, A.right);
+        if (RD) scan_lds_flush_rd(A, S, H);
+        else scan_lds_flush(S, A.left, A.right);
     }
     if (PROF) {
         __syncthreads();
@@ -1216,7 +1415,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
 
 // List scan: every entry of the key token's list is a position that held the key when it was
 // listed; entries overwritten since (merged or turned into holes) fail the token check.
-template <bool PROF, int NT>
+template <bool PROF, int NT, bool RD>
 __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanArgs A, bool by_b, const uint32_t *L,
                                                                      uint32_t len, ScanLds &S, const uint16_t *NB,
                                                                      uint32_t vb, uint32_t vg) {
@@ -1225,10 +1424,11 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     uint32_t *s_left = S.left, *s_right = S.right;
     uint32_t &s_any = S.any;
     scan_lds_clear(S);
-    if (threadIdx.x == 0) { s_any = 0; S.lrec_n = 0; }
+    if (threadIdx.x == 0) { s_any = 0; S.lrec_n = 0; S.rd[0] = S.rd[1] = 0; }
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{s_left, s_right, A.left, A.right, S.hleft, S.hright};
+    if (RD) { H.rd = S.rd; H.top = A.top_count; }
     const uint16_t *tok = A.tok;
     const uint32_t key = by_b ? A.b : A.a;
     uint32_t xx = 0, any = 0;
@@ -1307,17 +1507,17 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
                 {
                     if (!by_b) {
                         pr = (uint32_t)p;
-                        hit = occ_window(A, H, vi, 1u << k, xx, pw, cv, nx, ny) != 0;
+                        hit = occ_window<RD>(A, H, vi, 1u << k, xx, pw, cv, nx, ny) != 0;
                     } else {
                         int j = k - 1;  // the live token before p inside the vector
                         while (j >= 0 && tok_at(cv, j) == HOLE) j--;
                         if (j >= 0) {
-                            if (tok_at(cv, j) == A.a && occ_window(A, H, vi, 1u << j, xx, pw, cv, nx, ny)) {
+                            if (tok_at(cv, j) == A.a && occ_window<RD>(A, H, vi, 1u << j, xx, pw, cv, nx, ny)) {
                                 pr = (uint32_t)(vi * 8 + j);
                                 hit = true;
                             }
                         } else {
-                            hit = resolve_candidate(A, H, p, by_b, nvec, xx, pr);
+                            hit = resolve_candidate<RD>(A, H, p, by_b, nvec, xx, pr);
                         }
                     }
                 }
@@ -1330,12 +1530,14 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     }
     xx = wave_sum(xx);
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
+    if (RD && lane == 0 && xx) atomicOr(A.rd_top, 2u);
     if (lane == 0 && any) s_any = 1;
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
     if (s_any) {
         lrec_flush(A, S);
-        scan_lds_flush(S, A.left, A.right);
+        if (RD) scan_lds_flush_rd(A, S, H);
+        else scan_lds_flush(S, A.left, A.right);
     }
     if (PROF) {
         __syncthreads();
@@ -2170,6 +2372,27 @@ __global__ void __launch_bounds__(256) zbpe_apply(uint16_t *tok, int64_t n, cons
 // every shared counter (ids, live pairs, hot list, dirty home blocks) takes one atomic per block.
 constexpr int UPD_THREADS = 256;
 constexpr int UPD_MAX_PER = 8;
+// A multi-merge round's update blocks (zbpe_replace, round mode): member j of the round's members applied
+// (keys, their delta buffers at base + i * DELTA_WORDS). A pair tied at the round's start counts for the tie
+// count of the first member that decrements it (the reference's loop sees it tied only there): the one
+// decrement that finds the top count -- the first to land -- looks up which members decrement the pair (their
+// deltas) and credits the smallest (RoundHead::dec).
+struct RoundCtx {
+    const uint32_t *base;
+    uint32_t j;
+    const uint32_t *keys;  // RoundHead::key
+    uint32_t *dec;         // RoundHead::dec
+};
+__device__ inline void round_credit(const RoundCtx &rc, uint32_t key) {
+    const uint32_t x = key & 0xFFFF, y = key >> 16;
+    uint32_t m = rc.j;
+    for (uint32_t i = 0; i < rc.j; i++) {
+        const uint32_t *l = rc.base + (size_t)i * (2 * 65536 + 64);
+        const uint32_t ki = rc.keys[i], ai = ki & 0xFFFF, bi = ki >> 16;
+        if ((y == ai && l[x]) || (x == bi && l[65536 + y]) || (x == bi && y == ai && l[2 * 65536])) { m = i; break; }
+    }
+    atomicAdd(&rc.dec[m], 1u);
+}
 __host__ __device__ inline uint32_t update_chunks(uint32_t X, uint32_t per) { return (X + UPD_THREADS * per - 1) / (UPD_THREADS * per); }
 __host__ __device__ inline uint32_t update_blocks(uint32_t X, uint32_t per) { return 4 * update_chunks(X, per) + 1; }
 // t per thread: about 16 blocks per group (fewer, fatter blocks cut the shared atomics)
@@ -2182,7 +2405,10 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                                     uint32_t b, uint32_t X, uint32_t top_key, uint32_t ublk, uint32_t per,
                                     const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta, int prof = 0,
                                     uint32_t top_count = 0, uint32_t pr_key = NO_ID, uint32_t pr_key2 = NO_ID,
-                                    uint32_t pr_key3 = NO_ID, uint32_t pr_key4 = NO_ID) {
+                                    uint32_t pr_key3 = NO_ID, uint32_t pr_key4 = NO_ID, const RoundCtx *rc = nullptr,
+                                    uint32_t Xc = 0) {
+    // Xc: the bound the blocks' groups and ranges were laid out for (update_preload's X; 0: X itself -- a round's
+    // replace lays them out for the batch's bound on every member's X)
     // pr_key != NO_ID: merge X+1 has a pair-select candidate (DevState::pr_key): count the new pairs, the
     // tied pairs decremented (old count == top_count) and flag what rules the candidate out
     // option sel_prof: the latest stamp of each phase over the update blocks (st->pp_t[8..11])
@@ -2193,13 +2419,16 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
     __shared__ uint32_t s_hot[UPD_THREADS * UPD_MAX_PER];
     __shared__ uint32_t s_n, s_nhot, s_base, s_hbase;
     __shared__ int s_live;
-    const uint32_t nch = update_chunks(X, per);
+    const uint32_t nch = update_chunks(Xc ? Xc : X, per);
     const uint32_t tid = threadIdx.x;
     if (ublk >= 4 * nch) {  // specials: three independent chains
         if (tid >= 3) return;
         int live_delta = 0;
         const uint32_t xx = tail[0];
-        if (tid == 0 && xx) pair_dec(T, st, pair_key(b, a), xx);
+        if (tid == 0 && xx) {
+            const uint32_t old = pair_dec(T, st, pair_key(b, a), xx);
+            if (rc && old == top_count) round_credit(*rc, pair_key(b, a));
+        }
         if (tid == 0 && xx && pr_key != NO_ID) atomicOr(&st->pr_dt, 1u << 18);
         if (tid == 1 && xx) pair_new(T, st, pair_key(X, X), xx);
         if (tid == 2) {
@@ -2212,7 +2441,11 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 if (old < occ) atomicOr(&st->error, 2u);
                 if (old == occ) { live_delta--; home_add(T, st, top_key, false); }
             }
-            if (T.tok_cnt) {
+            if (T.tok_cnt && rc) {  // (a round's members may share tokens)
+                atomicAdd(&T.tok_cnt[X], (int32_t)occ);
+                atomicSub(&T.tok_cnt[a], (int32_t)occ);
+                atomicSub(&T.tok_cnt[b], (int32_t)occ);
+            } else if (T.tok_cnt) {
                 T.tok_cnt[X] += (int32_t)occ;
                 T.tok_cnt[a] -= (int32_t)occ;
                 T.tok_cnt[b] -= (int32_t)occ;
@@ -2289,6 +2522,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 if (old < c) atomicOr(&st->error, 2u);
                 if (old == c) { live_delta--; home_add(T, st, key, false); }
                 // (a pair's first decrement sees its count before the merge: each tied pair counts once)
+                if (rc && old == top_count) round_credit(*rc, key);
                 if (pr_key != NO_ID && old == top_count)
                     atomicAdd(&st->pr_dt, key == pr_key    ? 0x10001u
                                           : key == pr_key2 ? 0x80001u
@@ -2347,7 +2581,51 @@ struct ReplaceArgs {
     const uint32_t *dir_row, *dir;  // the candidate's scan plan (ScanArgs::dir_row, dir, dir_w)
     uint32_t dir_w, gen;
     int plan;
+    // multi-merge rounds (batch mode, one GPU or replicas): `round` member slots of per_member workgroups each
+    // (apply_blocks of them apply, the rest update), member j's deltas at left + j * DELTA_WORDS (fixed layout:
+    // right at +65536, tail at +131072); no member at or past token x_end (round_valid; C: the Zig capacity)
+    int round;
+    uint32_t per_member, x_end;
 };
+__device__ inline uint64_t dev_zig_cap_for(uint64_t D);
+__device__ inline bool dev_zig_at_max_load(uint64_t cap, uint64_t D);
+// Which members of a multi-merge round the reference's loop merges next, one after the other (every workgroup
+// of the round's replace evaluates it on the same words: the scan's RoundHead, final at this launch): the
+// longest prefix whose member j >= 1 was walked (a list form) with exactly T occurrences, none touching an
+// earlier member's (so its occurrences, its neighbours and its count are what they would be when its turn
+// comes: every touch -- a shared position or a neighbour -- is what a change of them needs), no earlier member
+// made a pair with the top count or adjacent occurrences (the tied set is the decision's less the merged and
+// the decremented: member j is its smallest home), the earlier members' new pairs are fewer than the free
+// Zig-map slots after member j's home block before the next tied home and after the largest tied home's
+// block (each new key fills at most one: member j's run still ends before the next tied home and no tied run
+// wraps, so it is first in slot order -- the pair-select argument of zbpe_select_next, per member), and the
+// Zig capacity is C and not at a max load for every live-pair count the earlier members can leave (each member
+// kills its own pair and at most one pair per new pair: D in [D0 - j, D0 + births - j]).
+__device__ inline uint32_t round_valid(const RoundHead &R, uint32_t T, uint32_t X0, uint32_t x_end, uint32_t C,
+                                       uint32_t arena_top, uint32_t rec_cap) {
+    uint32_t k = 1;
+    uint64_t births = R.birth[0];
+    uint32_t flags = R.top[0];
+    const uint32_t n = min(R.n, (uint32_t)ROUND_MAX);
+#pragma unroll
+    for (uint32_t j = 1; j < (uint32_t)ROUND_MAX; j++) {
+        if (j >= n) break;
+        if (flags || !R.walk[j] || R.touch[j] || R.rec[j] != T || X0 + j >= x_end) break;
+        if ((uint64_t)arena_top + (uint64_t)(j + 1) * T > rec_cap) break;
+        const uint64_t slack = R.ties == j + 1 ? ~0ull
+                               : (R.freeb[j] < 0 || R.freeb[0] < 0) ? 0ull
+                                                                    : (uint64_t)min(R.freeb[j], R.freeb[0]);
+        if (births >= slack) break;
+        const int64_t lo = (int64_t)R.live0 - (int64_t)j, hi = (int64_t)R.live0 + (int64_t)births - (int64_t)j;
+        if (lo < 1 || dev_zig_cap_for((uint64_t)lo) != C || dev_zig_cap_for((uint64_t)hi) != C ||
+            dev_zig_at_max_load(C, (uint64_t)hi))
+            break;
+        k = j + 1;
+        births += R.birth[j];
+        flags |= R.top[j];
+    }
+    return k;
+}
 // pair selects: merge X+1's candidate bound, by the replace's extra workgroup (defined with the home views below)
 __device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Summ *sup, uint32_t C, uint32_t nb,
                                         uint32_t nsb, const uint32_t *cs, uint32_t X, const uint32_t *lst_off,
@@ -2454,6 +2732,51 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
     }
+}
+
+// The replace of a multi-merge round (batch mode, one GPU or replicas): R.round member slots of R.per_member
+// workgroups, the first apply_blocks of each rewrite the stream at the member's records, the rest update the
+// counts from its deltas (update_block); every workgroup evaluates round_valid on the scan's RoundHead and the
+// slots of members past the valid prefix return at once. Members' occurrences touch none of each other's, so
+// their rewrites and count updates commute: applying them together is applying them in order.
+__global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const uint32_t *__restrict__ left, uint32_t Xp,
+                                                          uint32_t apply_blocks, ReplaceArgs R, Tables T) {
+    constexpr uint32_t DW = 2 * 65536 + 64;  // DELTA_WORDS
+    const uint32_t j = blockIdx.x / R.per_member, lb = blockIdx.x - j * R.per_member, per = update_per(Xp);
+    const uint32_t *lj = left + (size_t)j * DW;
+    uint32_t dv[UPD_MAX_PER];
+    if (lb >= apply_blocks) update_preload(lj, lj + 65536, Xp, lb - apply_blocks, per, dv);
+    const StateHead H = load_head(st);
+    const RoundHead &RH = st->rd;  // (read in place: a register copy indexed by the member went to scratch)
+    if (H.halt) return;
+    const uint32_t Tc = H.top_count;
+    const uint32_t k = round_valid(RH, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->rd_v = k;
+    if (j >= k) return;
+    const uint32_t X = H.cur_x + j, key = RH.key[j], a = key & 0xFFFF, b = key >> 16;
+    if (lb < apply_blocks) {
+        // X at each occurrence start, a hole at its b (one GPU: the b is always in the stream)
+        const uint32_t *rec = R.rec + H.arena_top + (size_t)j * Tc;
+        const uint32_t cnt = min(j ? RH.rec[j] : H.rec_count, Tc);
+        uint32_t made = 0;
+        for (uint32_t i = lb * 256 + threadIdx.x; i < cnt; i += apply_blocks * 256) {
+            const int64_t p = rec[i];
+            R.tok[p] = (uint16_t)X;
+            const int64_t q = next_live(R.tok, R.n, p);
+            if (q >= 0) {
+                R.tok[q] = HOLE;
+                made++;
+            }
+        }
+        made = wave_sum(made);
+        if ((threadIdx.x & 63) == 0 && made) atomicAdd(&st->holes_made, made);
+        return;
+    }
+    const uint32_t ublk = lb - apply_blocks;
+    const uint32_t *tj = lj + 2 * 65536;
+    if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc) atomicOr(&st->error, 64u);  // occurrences != count
+    const RoundCtx rc{left, j, &st->rd.key[0], &st->rd.dec[0]};
+    update_block(T, st, lj, lj + 65536, tj, a, b, X, key, ublk, per, dv, H.theta, 0, Tc, NO_ID, NO_ID, NO_ID, NO_ID, &rc, Xp);
 }
 
 // this shard's boundary record: first 3 / last 2 live tokens (holes skipped) and its live count
@@ -2661,7 +2984,7 @@ __global__ void zbpe_self_x0(const uint32_t *__restrict__ fns, int rank, uint8_t
     *x0 = x;
 }
 __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, const uint8_t *__restrict__ carry_in) {
-    const ScanArgs A = scan_args_resolve(A0, load_head(A0.st));
+    const ScanArgs A = scan_args_resolve(A0, load_head(A0.st), A0.X);
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
     __shared__ uint32_t s_rec[SELF_TILE / 2];
     __shared__ uint8_t s_wave[SELF_THREADS / 64];
@@ -2743,7 +3066,7 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
 // trailing a of an odd run or the token after the run. Two walks: count, then (after one atomic per
 // wave for the records) emit. O(list length) instead of three passes over the stream.
 __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_self_list(ScanArgs A0) {
-    const ScanArgs A = scan_args_resolve(A0, load_head(A0.st));
+    const ScanArgs A = scan_args_resolve(A0, load_head(A0.st), A0.X);
     const uint32_t a = A.a, len = A.lst_len[a];
     if (len == NO_LIST || (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len)) return;
     const uint32_t *L = A.lists + A.lst_off[a];
@@ -3409,11 +3732,6 @@ __device__ inline Summ ld_wt(const Summ *p) {
                                                    __HIP_MEMORY_SCOPE_AGENT);
     return Summ{(int32_t)(uint32_t)v, (int32_t)(uint32_t)(v >> 32)};
 }
-struct HomeView {
-    const uint32_t *hc;
-    const Summ *summ, *sup;
-    uint32_t C, nb, nsb;
-};
 // ordered composition by one wave of the slots [lo, hi) inside the summary block starting at
 // `base`: lane L owns slots base + 64L .. +63 and reads them as four 16-B vectors (the histogram
 // is allocated in whole 4096-slot blocks)
@@ -3750,9 +4068,10 @@ constexpr int DECIDE_THREADS = 256;
 // of the select while its other waves work (the decision's carries), so the scan starts walking after
 // one state round trip instead of three. Token xn (made by the merge this launch rolled) has its
 // records as its list: offset xoff, length xlen (select_finish stores them in this launch).
+// (a multi-merge round made xnum tokens xn, xn + 1, ..: token xn + i's list is at xoff + i * xlen, xlen long)
 struct PlanCtx {
     const uint32_t *lst_off, *lst_len, *dir_row, *dir;
-    uint32_t dir_w, lists_x, xn, xoff, xlen;
+    uint32_t dir_w, lists_x, xn, xoff, xlen, xnum = 1;
 };
 __device__ inline void plan_compute(const PlanCtx &P, uint32_t key, uint32_t *out) {
     const uint32_t a = key & 0xFFFF, b = key >> 16;
@@ -3764,8 +4083,8 @@ __device__ inline void plan_compute(const PlanCtx &P, uint32_t key, uint32_t *ou
         r0 = P.dir[rb];
         r1 = P.dir[rb + 1];
     }
-    if (a == P.xn) { la = P.xlen; oa = P.xoff; }
-    if (b == P.xn) { lb = P.xlen; ob = P.xoff; }
+    if (a - P.xn < P.xnum) { la = P.xlen; oa = P.xoff + (a - P.xn) * P.xlen; }
+    if (b - P.xn < P.xnum) { lb = P.xlen; ob = P.xoff + (b - P.xn) * P.xlen; }
     out[0] = la; out[1] = lb; out[2] = oa; out[3] = ob; out[4] = r0; out[5] = r1;
 }
 // the plan of merge x1 = key (after the state's cur_key for it is stored; the next kernel boundary orders both)
@@ -4060,6 +4379,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                 st->pr_key = k2;
                 st->pr_ties = total;
                 st->pr_x = pair_x;
+                st->pr_full = pair_x;
             }
         }
     }
@@ -4092,6 +4412,65 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
 // argmax workgroup spins. The grid is sized (launch bounds: 4 waves per SIMD) so that every workgroup
 // fits one dispatch round.
 // ------------------------------------------------------------------------------------------
+// The roll of a multi-merge round (the last argmax workgroup's thread 0, after select_finish without its roll):
+// every member's records become its new token's list (member j's at arena_top + j T, T of them), the stream and
+// arena counters advance by all of them, the members' merge-log rows get their pairs, counts, live tokens and
+// tie counts (member j's tied set is member j-1's less member j-1 and the tied pairs member j-1 decremented
+// first, RoundHead::dec), and the round's words are cleared for the next round's scan.
+__device__ inline void round_roll(const Tables &T, DevState *st, const StateHead &H0, MergeLog *log, const uint32_t *pre,
+                                  FinishOut *fo, uint32_t *rlog) {
+    const uint32_t k = H0.rd_v, X0 = H0.cur_x, Tc = H0.top_count;
+    RoundHead &R = st->rd;
+    uint32_t rec[ROUND_MAX], key[ROUND_MAX], dec[ROUND_MAX];
+#pragma unroll
+    for (int j = 0; j < ROUND_MAX; j++) {
+        rec[j] = R.rec[j];
+        key[j] = R.key[j];
+        dec[j] = R.dec[j];
+    }
+    rec[0] = pre[RI_REC];
+    const uint32_t holes = pre[RI_HOLES], arena_top = pre[RI_ARENA_TOP], arena_rep = pre[RI_ARENA_REP], total_occ = pre[RI_TOTAL_OCC];
+    const long long live_tokens = (long long)(((uint64_t)pre[RI_LIVE_TOK_HI] << 32) | pre[RI_LIVE_TOK_LO]);
+    uint32_t ties = log[X0 - 256].ties, sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < (uint32_t)ROUND_MAX; j++) {
+        if (j >= k) break;
+        if (T.lst_off) {
+            T.lst_off[X0 + j] = arena_top + j * Tc;
+            T.lst_len[X0 + j] = rec[j];
+        }
+        if (j) {
+            ties = ties - 1u - dec[j - 1];
+            MergeLog &L = log[X0 + j - 256];
+            L.key = key[j];
+            L.count = Tc;
+            L.live = (uint32_t)(live_tokens - (long long)j * Tc);
+            L.ties = ties;
+        }
+        sum += rec[j];
+    }
+    const uint32_t top = arena_top + (k - 1) * Tc + rec[k - 1];
+    if (T.lst_off) st->arena_top = top;
+    st->last_occ = sum;
+    st->total_occ = total_occ + sum;
+    st->last_gocc = sum;
+    st->arena_rep = arena_rep + sum;
+    st->last_holes = holes;
+    st->live_tokens = live_tokens - holes;
+    st->tie_len = 0;
+    st->holes_made = 0;
+    st->rec_count = 0;
+#pragma unroll
+    for (int j = 0; j < ROUND_MAX; j++) {
+        R.walk[j] = 0; R.touch[j] = 0; R.top[j] = 0; R.birth[j] = 0; R.rec[j] = 0; R.dec[j] = 0;
+    }
+    st->rd_v = 0;
+    st->rd_merges += k - 1;
+    fo->arena_top = T.lst_off ? top : arena_top;
+    fo->arena_rep = arena_rep + sum;
+    fo->live_tokens = live_tokens - holes;
+    *rlog = X0 | (k << 16);
+}
 constexpr int NEXT_THREADS = 512;  // launch bounds: 4 waves per SIMD (two workgroups per CU; the decision spills a little)
 constexpr int NEXT_CAND = 64;          // keys kept per argmax block at the block's max
 constexpr int NEXT_MAX_SEL = 1024;     // argmax blocks (the reducer keeps one LDS entry per block)
@@ -4128,6 +4507,14 @@ struct NextArgs {
     int skip_refresh;     // option pair_refresh 0: a pair select's refresh workgroups leave the dirty blocks to the next launch
     int m3_w4;            // option pair_m3w: the decision's third-smallest home by wave 4 (else wave 0)
     int chain;            // option pair_chain: a pair select names merge X+2's candidate (needs skip_refresh, m3_w4); 2: and X+3's; 3: X+4's
+    // multi-merge rounds (option round_k; batch mode, one GPU or replicas): `round` member slots. The merges this
+    // launch rolls are the state's (cur_x .. cur_x + rd_v - 1; the kernel's X is the host's bound on them, for the
+    // clearing of the members' delta buffers `delta`, fixed layout); no pair selects (every select is a full
+    // one). par: the refresh counters' parity (launch order); seq: a launch id (ref_noprefix); rlog[rlog_i] =
+    // the round's first merge | its members << 16.
+    int round;
+    uint32_t par, seq, rlog_i;
+    uint32_t *rlog;
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -4206,12 +4593,21 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // written by the launch before); then the last workgroup to arrive is elected (returning
         // atomics, per-XCD counters, then the top one) and arrives once more when done. Else a
         // workgroup's arrival is one non-returning add to its XCD's counter.
-        const bool pfx = N.cs && N.B.log[X - 256].ties > 1;
+        // (rounds: ties come in streaks, a round is one; the carries are always precomputed)
+        const bool pfx = N.round ? N.cs != nullptr : N.cs && N.B.log[X - 256].ties > 1;
         // merge X's neighbour deltas, cleared for merge X + 2 by these workgroups (off the argmax's
         // critical path: the argmax grid is sized by the hot list alone; nothing in this launch reads
         // [0, 2X) -- the roll reads the tail words past it)
-        for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
-        if (N.pair && N.skip_refresh) {  // a pair select: no decision in this launch reads the summaries
+        if (N.round) {  // every member buffer: left [0, X), right [65536, 65536 + X), the tail's two words
+            const uint32_t per = 2 * X + 2;
+            for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < (uint32_t)N.round * per; t += nref * NEXT_THREADS) {
+                const uint32_t m = t / per, o = t - m * per;
+                delta[(size_t)m * (2 * 65536 + 64) + (o < X ? o : o < 2 * X ? 65536 + (o - X) : 2 * 65536 + (o - 2 * X))] = 0;
+            }
+        } else {
+            for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
+        }
+        if (N.pair && N.skip_refresh && !N.round) {  // a pair select: no decision in this launch reads the summaries
             const PairHead P0 = *reinterpret_cast<const PairHead *>(&st->pr_x);
             if (pair_light(N.pair, N.B.X, N.x_end, N.V.C, P0, st->live)) return;
         }
@@ -4229,14 +4625,14 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
             atomicAdd(&st->sel_prof[16], 1ull);
         }
         __shared__ uint32_t s_rlast;
-        uint32_t *rtk = N.rtk + (X & 1) * RTK_SET;
+        uint32_t *rtk = N.rtk + (N.round ? N.par : X & 1) * RTK_SET;
         if (!pfx) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through summaries drained
             __syncthreads();
             if (tid == 0) __hip_atomic_fetch_add(rtk + (blockIdx.x & 7) * RTK_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
-        if (block_ticket_last_x(rtk, nref, &s_rlast) && ld_wt(&st->ref_noprefix) != X) {
+        if (block_ticket_last_x(rtk, nref, &s_rlast) && ld_wt(&st->ref_noprefix) != (N.round ? N.seq : X)) {
             if (N.prof && tid == 0)
                 __hip_atomic_store(&st->sel_prof_pq, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             refresh_prefix(N.V, N.cs);
@@ -4262,6 +4658,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     const bool lp_wave = bx == 0 && tid >= 64 && tid < 128 && N.world == 1 && !N.lp_lazy;
     const uint32_t t_tail = lp_wave && n - 1 - (int64_t)(tid - 64) >= 0 ? tok[n - 1 - (int64_t)(tid - 64)] : HOLE;
     const StateHead H0 = load_head(st);
+    // multi-merge rounds: this launch rolls the round's members, merges cur_x .. Xr, and begins merge Xr + 1
+    const uint32_t Xr = N.round && H0.rd_v ? H0.cur_x + H0.rd_v - 1 : X;
+    BeginArgs NB = N.B;
+    if (N.round) NB.X = Xr + 1;
     // pair select: merge X+1's candidate from merge X's tie decision and what merge X's replace counted (in
     // the head's round trip)
     PairHead P0{};
@@ -4301,7 +4701,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     // tied run wraps: it is the first tied key in slot order) and (d) the Zig capacity is the same and not
     // at a max load (the stream's last pair is not needed). Then the Zig order is the one the decision saw.
     // (one roll and begin below serve both: a second inlined copy of them pushed the kernel into spills)
-    const bool light = pair_light(N.pair, N.B.X, N.x_end, N.V.C, P0, live0);
+    const bool light = !N.round && pair_light(N.pair, N.B.X, N.x_end, N.V.C, P0, live0);
     if (light && bx != 0) return;
     // the candidate's words wait in LDS (kept in registers across the argmax and decision code, they pushed
     // the kernel's scalar registers into spills)
@@ -4425,9 +4825,9 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     if (N.prof && tid == 0) atomicMax(&st->sel_ta, (unsigned long long)wall_clock64());
     if (!single && !block_ticket_last(&st->ticket, sel_blocks, &s_flag)) return;
-    const bool pfx = nref && N.cs && N.B.log[X - 256].ties > 1;  // the refresh precomputes the carries (its predicate)
+    const bool pfx = nref && N.cs && (N.round || N.B.log[X - 256].ties > 1);  // the refresh precomputes the carries (its predicate)
     // the next launch's refresh count (the launch before this one used it and has ended)
-    if (tid < 9) st_wt(N.rtk + ((X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
+    if (tid < 9) st_wt(N.rtk + (N.round ? N.par ^ 1u : (X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
     unsigned long long pt = 0;
     if (N.prof && tid == 0 && !light) {
         pt = st->sel_t0;
@@ -4483,7 +4883,11 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     // the next merge's scan plan: its list loads (one lane of wave 1) overlap the roll and begin below;
     // for an untied next merge the key is known now, a tied one's comes from the decision (decide_body)
     __shared__ uint32_t s_plan[6];
-    const PlanCtx plan{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, X, H0.arena_top, H0.rec_count};  // (X's list: the roll's lst_off / lst_len, from the same words)
+    // (X's list: the roll's lst_off / lst_len, from the same words; a round's members: T records each)
+    const PlanCtx plan = N.round && H0.rd_v ? PlanCtx{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, H0.cur_x, H0.arena_top,
+                                                      H0.top_count, H0.rd_v}
+                                            : PlanCtx{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, X, H0.arena_top,
+                                                      H0.rec_count, 1u};
     const bool plan_on = N.plan && T.lst_off && H0.lists_valid;
     if (plan_on && tid == 64) {
         if (light) {  // the candidate's plan, by merge X's replace (pair_slack_block), unless the layout changed since
@@ -4499,13 +4903,15 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     if (N.prof && tid == 0 && !light) sel_tick(st, 1, &pt);
     if (tid == 0) {
         FinishOut fo;
-        select_finish(T, st, Q, tok, n, delta, X, 1, N.bnd, N.world, light || (Q.ties == 1 && Q.cnt) ? s_key[0] : NO_ID,
+        const bool rnd = N.round && H0.rd_v;
+        select_finish(T, st, Q, tok, n, delta, X, rnd ? 0 : 1, N.bnd, N.world, light || (Q.ties == 1 && Q.cnt) ? s_key[0] : NO_ID,
                       lastpair_wt, &fo, s_pre, Q.ties > 1 && !light, N.lp_lazy != 0 || light);
+        if (rnd) round_roll(T, st, H0, N.B.log, s_pre, &fo, N.rlog + N.rlog_i);
         s_h = HALT_DONE;
         s_tie = 0;
-        if (N.B.X < N.x_end) {
+        if (NB.X < N.x_end) {
             bool tie;
-            const uint32_t h = merge_begin_eval_v(T, fo, N.B, &tie);
+            const uint32_t h = merge_begin_eval_v(T, fo, NB, &tie);
             if (light && !h && tie) {  // a pair select: the decision's commit, with its winner
                 st->cur_x = N.B.X;
                 st->tie_on = 0;
@@ -4513,7 +4919,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 N.B.log[N.B.X - 256] = MergeLog{s_key[0], fo.top_count, (uint32_t)fo.live_tokens, fo.tie_count};
                 tie = false;
             } else {
-                merge_begin_commit_v(st, N.B, h, tie, fo);
+                merge_begin_commit_v(st, NB, h, tie, fo);
             }
             if (light) {
                 // chain: merge X+2's candidate is the next tied key by home, once this pair select is committed;
@@ -4544,13 +4950,16 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
             }
             s_h = h;
             s_tie = tie ? 1u : 0u;
+        } else if (N.round) {  // the round reached the vocabulary's end: the launches after it have nothing to do
+            st->halt = HALT_DONE;
+            st->halt_at = NB.X;
         }
         s_len = 0;
         s_ovf = 0;
     }
     __syncthreads();
     // merge X+1 needs no tie decision: the last refresh workgroup may skip its carries
-    if (tid == 0 && (s_h || !s_tie)) st_wt(&st->ref_noprefix, X);
+    if (tid == 0 && (s_h || !s_tie)) st_wt(&st->ref_noprefix, N.round ? N.seq : X);
     if (N.prof && tid == 0 && !light) sel_tick(st, 2, &pt);
     // the tied top pair's key, deferred by select_finish (stored on every way out below)
     auto put_key = [&]() {
@@ -4560,7 +4969,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     };
     if (s_h || !s_tie) {
-        if (plan_on && tid == 64 && !s_h && (light || (Q.ties == 1 && Q.cnt))) plan_store(st, N.B.X, s_key[0], N.gen, s_plan);
+        if (plan_on && tid == 64 && !s_h && (light || (Q.ties == 1 && Q.cnt))) plan_store(st, NB.X, s_key[0], N.gen, s_plan);
         if (N.prof && tid == 0) {
             const unsigned long long now = wall_clock64();
             st->pp_t[7] = now;
@@ -4582,7 +4991,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     __syncthreads();
     if (total > N.tie_cap) {  // the host path decides (replicated state: every rank takes it)
-        if (tid == 0) { st->halt = HALT_TIE; st->halt_at = N.B.X; }
+        if (tid == 0) { st->halt = HALT_TIE; st->halt_at = NB.X; }
         put_key();
         return;
     }
@@ -4661,7 +5070,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // Bounded: a wait past SPIN_LIMIT_TICKS (a broken dispatch-order assumption) reads the counters once
         // more and, still short, sets error bit 1024 (sync_state fails the train); the decision goes on with
         // whatever summaries it reads.
-        const uint32_t *rtk = N.rtk + (X & 1) * RTK_SET;
+        const uint32_t *rtk = N.rtk + (N.round ? N.par : X & 1) * RTK_SET;
         const unsigned long long t_spin = wall_clock64();
         if (pfx) {
             const uint32_t want = min(nref, 8u) + 1u;
@@ -4706,7 +5115,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
-                              plan_on, plan, N.gen, N.pair && N.B.X + 1 < N.x_end ? N.B.X + 1 : 0u, N.m3_w4 != 0,
+                              plan_on, plan, N.gen, N.pair && NB.X + 1 < N.x_end ? NB.X + 1 : 0u, N.m3_w4 != 0,
                               N.skip_refresh != 0 && N.chain != 0, N.chain >= 2, N.chain >= 3);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();

@@ -22,6 +22,29 @@ constexpr int PRES_GROUP = 32;       // presence blocks per bitmap word
 
 __host__ __device__ constexpr inline uint32_t pair_key(uint32_t first, uint32_t second) { return first | (second << 16); }
 
+// Multi-merge rounds (option round_k). A tied merge's decision names the tied keys by
+// home slot order (DevState::pr_key .. pr_key4); a round applies the merge and up to ROUND_MAX - 1 of those
+// keys in one scan, one replace and one select launch. The round's scan walks every member's occurrences
+// (member j -> merge cur_x + j, new token cur_x + j) into its own delta buffer and records; the replace
+// applies the longest prefix of members that the reference's loop would merge next, one after the other
+// (each member j >= 1: still tied and first in Zig slot order, no occurrence touching an earlier member's);
+// the select rolls them all and starts the merge after the round.
+constexpr int ROUND_MAX = 5;
+struct RoundHead {
+    uint32_t n;                  // members the scan took (1 .. ROUND_MAX; written by its block 0)
+    uint32_t ties;               // tied keys at the decision that named them (pr_ties)
+    int32_t live0;               // live pairs at the round's start (DevState::live as the scan saw it)
+    uint32_t key[ROUND_MAX];     // member keys (key[0] = cur_key)
+    uint32_t walk[ROUND_MAX];    // member j >= 1 walked by a list form (a stream scan is never a member)
+    uint32_t touch[ROUND_MAX];   // an occurrence of member j touches one of an earlier member's
+    uint32_t top[ROUND_MAX];     // bit 0: a new pair of member j has the top count; bit 1: adjacent occurrences
+    uint32_t birth[ROUND_MAX];   // new pairs of member j: its distinct neighbour tokens
+    uint32_t rec[ROUND_MAX];     // records of member j >= 1 (member 0's: DevState::rec_count)
+    int32_t freeb[ROUND_MAX];    // free Zig-map slots: [0] after the largest tied home's block, [j] after member j's
+                                 // home block and before the next tied home (j >= 1); -1: no bound
+    uint32_t dec[ROUND_MAX];     // tied pairs member j decremented first (the replace), for the tie counts
+};
+static_assert(sizeof(RoundHead) == 4 * (3 + 8 * ROUND_MAX), "round head: packed words");
 // Device-resident state. Host reads a copy after each merge (one small D2H per merge).
 struct DevState {
     // ---- hot header (the first 96 B): the words the merge kernels read first, loaded together in one
@@ -44,7 +67,9 @@ struct DevState {
     // the stream's last pair (zbpe_select_next): its key and pair id when last looked up, so that the
     // count is one load beside the tail tokens' (the key only changes when a merge reaches the tail)
     uint32_t lp_key, lp_id;
-    uint32_t head_pad[4];
+    uint32_t cur_x;          // merge token X being processed (the first member of a multi-merge round)
+    uint32_t rd_v;           // multi-merge rounds: members the round's replace applied (0: not a round; RoundHead)
+    uint32_t head_pad[2];
     // ---- the rest
     uint32_t num_ids;        // pair ids allocated
     int32_t live;            // D_t: pairs with count > 0
@@ -73,7 +98,6 @@ struct DevState {
     // device-resident merge loop (Engine::run_batch): the host enqueues a batch of merges whose
     // kernels read the pair from here; a merge the device cannot finish alone halts the batch
     uint32_t halt_at;        // merge token X of the halted merge
-    uint32_t cur_x;          // merge token X being processed
     uint32_t tie_on;         // 1: this merge's top count is tied (the tie kernels run)
     long long live_tokens;   // live tokens of this shard (rolled by zbpe_select)
     uint32_t arena_rep;      // sum of the merges' global occurrence counts since the arena was emptied: the same on
@@ -110,7 +134,14 @@ struct DevState {
     uint32_t pr_key2, pr_key3;        // (pr_key3: merge X+3's, option pair_chain 2; bit 20 of pr_dt: decremented)
     uint32_t pr_h2, pr_h3, pr_h4, pr_hmax, pr_h5;
     uint32_t pr_key4, pr_h6;          // (merge X+4's, option pair_chain 3; bit 21)
-    uint32_t pr_pad2[9];
+    // pr_x as a tie decision set it (a pair select's chain shift leaves it): a multi-merge round takes the named
+    // keys only from the decision itself (the chain state past a pair select counts what that merge did)
+    uint32_t pr_full;
+    uint32_t pr_pad2[8];
+    // multi-merge rounds (option round_k, one GPU or replicas): see RoundHead; rd_merges counts the merges
+    // rounds applied beyond their first members
+    alignas(128) RoundHead rd;
+    uint32_t rd_merges;
 };
 struct PairHead {  // what the light test reads (the kernel entry's round trip)
     uint32_t x, key, slack, ties, births, dt, hits, plan_gen;
@@ -126,11 +157,12 @@ struct StateHead {
     uint32_t halt, cur_key, arena_top, lists_valid, lists_x, top_count, theta, hot_len, rec_count;
     uint32_t plan_x, plan_key, plan_gen, plan_la, plan_lb, plan_oa, plan_ob, plan_r0, plan_r1;
     uint32_t lp_key, lp_id;
-    uint32_t pad[4];
+    uint32_t cur_x, rd_v;
+    uint32_t pad[2];
 };
 static_assert(sizeof(StateHead) == 96, "state head: 24 words");
 static_assert(offsetof(DevState, rec_count) == 32 && offsetof(DevState, plan_r1) == 68 && offsetof(DevState, hot_len) == 28 &&
-                  offsetof(DevState, lp_id) == 76,
+                  offsetof(DevState, lp_id) == 76 && offsetof(DevState, rd_v) == 84,
               "StateHead mirrors DevState's first words");
 // zbpe_select_next's refresh arrival counters (a device buffer): per launch parity X & 1, eight
 // per-XCD counters (workgroup i counts in i % 8) and a top counter, each on its own 128-B line. The
@@ -183,6 +215,12 @@ constexpr int SUPER_BLOCKS = 64;          // block summaries per super-block sum
 // carry function c -> max(m, c + q) of a run of slots; |q|, m <= Zig capacity < 2^31, so 32-bit
 // arithmetic (half the VALU chain and shuffles of the tie decision)
 struct Summ { int32_t q, m; };
+// the Zig-map home histogram as the tie decision reads it: per-slot counts, block and super-block summaries
+struct HomeView {
+    const uint32_t *hc;
+    const Summ *summ, *sup;
+    uint32_t C, nb, nsb;
+};
 
 // Live tokens just outside this rank's shard (multi-GPU): left token 0 is the last live token before
 // the shard, left 1 the one before it; right 0..2 the first live tokens after it. Packed 16 bits per

@@ -75,6 +75,9 @@ pub const BasicTokenizer = struct {
         self.timeStats.replace_pair_calls += st.replace_pair_calls;
         self.timeStats.just_count_pairs_time += @intFromFloat(st.count_pairs_s * 1000.0);
         self.timeStats.just_count_pairs_calls += st.count_pairs_calls;
+        // generateCodePointPairs runs once per count (basic_tokenizer.zig:185-186); the device never materialises
+        // the pairs, so its time is 0 over as many calls (zbpe_format_time_stats prints the same line), not 0 / 0
+        self.timeStats.generate_pairs_calls += st.count_pairs_calls;
     }
 
     pub fn encode(self: *@This(), text: []const u8) !std.ArrayList(u16) {
