@@ -107,7 +107,7 @@ def analyse(d, logp):
             continue
         t1 = first[hi] if hi is not None else ks[-1][1]
         n = (hi if hi is not None else len(ties)) - lo
-        wall[b] = ((t1 - first[lo]) / 1e3, n)
+        wall[b] = ((t1 - first[lo]) / 1e6, n)  # (trace timestamps in ns)
     # halted batches: reason -> count and host-path microseconds, by bucket
     names = {2: "hot_list_rebuild", 3: "zig_capacity", 4: "undecided_tie", 5: "self_pair", 6: "arena"}
     halts = {b: {} for b in buckets}

@@ -1138,15 +1138,22 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                 P[17] * us / calls, P[18] * us / calls, P[19] / calls);
         fprintf(stderr, "sel_prof: pair selects %llu, average %.2f us from the first argmax block's start to their commit\n", P[20],
                 P[21] * us / std::max(1.0, (double)P[20]));
+        const uint32_t *W = h_st->rd_why;
+        fprintf(stderr, "sel_prof: rounds with named keys ended by: all walked %u, an earlier member's top/adjacent pairs %u, not walked %u, "
+                        "touch %u, records %u, vocabulary end %u, arena %u, free slots %u, capacity %u\n",
+                W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8]);
+        const unsigned long long nw = (P[23] & 0xFFFFFFFFull) + (P[23] >> 32);
+        fprintf(stderr, "sel_prof: round member walks %llu (%llu with the decision's plan), average %.2f us from the workgroup's state words in (round_scan) to the walk's start\n",
+                nw, P[23] & 0xFFFFFFFFull, P[22] * us / std::max(1.0, (double)nw));
         static const char *bucket[3] = {"merges < 7936", "merges 7936-19743", "merges >= 19744"};
         for (int k = 0; k < 3; k++) {
             const unsigned long long *Q = h_st->pipe_prof[k];
             const double nl = std::max(1.0, (double)Q[4]), nr = std::max(1.0, (double)Q[7]), ns = std::max(1.0, (double)Q[9]);
             fprintf(stderr, "pipe_prof %s: list scans %llu: avg us from the launch's block-0 start: LDS clear done %.2f, walk "
                             "done %.2f, flush done %.2f, replace starts %.2f; replace (%llu): work done %.2f, select starts %.2f; "
-                            "select end -> scan start (%llu) %.2f\n",
+                            "select end -> scan start (%llu) %.2f; round scans' bound workgroups done %.2f\n",
                     bucket[k], Q[4], Q[0] * us / nl, Q[1] * us / nl, Q[2] * us / nl, Q[3] * us / nl, Q[7], Q[5] * us / nr,
-                    Q[6] * us / nr, Q[9], Q[8] * us / ns);
+                    Q[6] * us / nr, Q[9], Q[8] * us / ns, Q[15] * us / nl);
             fprintf(stderr, "pipe_prof %s: replace phases, avg us from its block-0 start (latest block): deltas in %.2f, "
                             "gathered %.2f, ids/hot reserved %.2f, table updated %.2f; apply blocks done %.2f\n",
                     bucket[k], Q[10] * us / nr, Q[11] * us / nr, Q[12] * us / nr, Q[13] * us / nr, Q[14] * us / nr);
@@ -1205,8 +1212,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // one GPU or replicas, with the naming decisions of the pair selects; a launch triple then does 1 .. round_k
     // merges, which the device decides (round_valid), so the kernels take the merge index from the state and
     // the batch's merges are counted after it
+    // (and in tie streaks: a round of one costs more than a plain merge -- the members' walks, the full selects)
     const bool rounds = round_k >= 2 && !dist() && fused_select && pair_select && refresh_prefix && lists_on && list_streak &&
-                        !replace_split && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS;
+                        last_tied_pct >= round_ties && !replace_split && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS;
     const uint32_t KM = rounds ? std::min<uint32_t>(K * (uint32_t)round_k, run.vocab - X0) : K;  // merges the batch may do
     // headroom for KM merges: ids, occurrence records (counts never grow), tie list; compaction
     CHECK(maybe_grow_tables(X0, KM));
@@ -1412,6 +1420,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     uint32_t nlist = 0;
     for (uint32_t i = 0; i < m; i++) nlist += h_log[X0 - 256 + i].mode;
     list_streak = m > 0 && nlist == m;
+    uint32_t ntied = 0;
+    for (uint32_t i = 0; i < m; i++) ntied += h_log[X0 - 256 + i].ties > 1 ? 1u : 0u;
+    last_tied_pct = m ? 100u * ntied / m : 0u;
     n_live = h_st->live_tokens;
     if (dist()) halo_from_boundaries();
     *done = m;
@@ -1447,8 +1458,13 @@ zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_
     A.hv = HomeView{nullptr, d_summ, d_sup, (uint32_t)C, V.nb, V.nsb};
     A.cs = cs;
     const int g = list_streak && list_grid > 0 ? list_grid : scan_grid(n_slots);
-    hipLaunchKernelGGL((zbpe_scan_pairs_t<4, true, true, true, true, false, false, true>), dim3(g + RD_FREE_WGS), dim3(SCAN_THREADS),
-                       0, stream, (const DevState *)d_st, A);
+    A.prof = (int)sel_prof;
+    if (sel_prof)  // (the probed instantiation)
+        hipLaunchKernelGGL((zbpe_scan_pairs_t<4, true, true, true, true, true, false, true>), dim3(g + RD_FREE_WGS), dim3(SCAN_THREADS),
+                           RD_QUEUE * sizeof(uint32_t), stream, (const DevState *)d_st, A);
+    else
+        hipLaunchKernelGGL((zbpe_scan_pairs_t<4, true, true, true, true, false, false, true>), dim3(g + RD_FREE_WGS), dim3(SCAN_THREADS),
+                           RD_QUEUE * sizeof(uint32_t), stream, (const DevState *)d_st, A);  // (dynamic LDS: rd_queue)
     LAUNCH_OK();
     if (timed) {
         HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 2], stream));
@@ -1457,7 +1473,7 @@ zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_
     const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top0 / 256 + 1);
     const uint32_t pm = ab + update_blocks(Xmax, update_per(Xmax));
     ReplaceArgs R{d_tok[cur], n_slots, d_lists, (uint32_t)lists_cap, base, base + 65536, base + 2 * 65536, 0, 0, Xmax, 0, ab, halo,
-                  nullptr, 1, nullptr, 1, 0, 0, d_summ, d_sup, (uint32_t)C, V.nb, V.nsb, cs, nullptr, nullptr, 0, layout_gen, 0};
+                  nullptr, 1, nullptr, 1, (int)sel_prof, 0, d_summ, d_sup, (uint32_t)C, V.nb, V.nsb, cs, nullptr, nullptr, 0, layout_gen, 0};
     R.round = round_k;
     R.per_member = pm;
     R.x_end = run.vocab;

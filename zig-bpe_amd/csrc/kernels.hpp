@@ -381,18 +381,13 @@ struct NeighbourHist {
     uint32_t *h_left = nullptr, *h_right = nullptr;  // nullptr: no hash (large tokens go to HBM)
     // multi-merge rounds: every add to the global deltas returns the old value, so that the workgroup counts the
     // new pairs (a delta word leaving 0: one per distinct neighbour token, whichever workgroup adds first) and
-    // sees a new pair reaching the top count (the add that completes it); rd = its LDS words {new pairs, top}
+    // sees a new pair reaching the top count (the add that completes it); rd = its LDS words {new pairs, top,
+    // queued adds}. The walk's adds past the LDS bins and hash are queued in LDS (rd_queue, the round scan's
+    // dynamic LDS) and made by the flush, all in flight together: a returning add here held its thread for a
+    // memory round trip per occurrence.
     uint32_t *rd = nullptr;
     uint32_t top = 0;
-    __device__ inline void gadd(uint32_t *g, uint32_t t, uint32_t v) const {
-        if (!rd) {
-            atomicAdd(&g[t], v);
-            return;
-        }
-        const uint32_t old = atomicAdd(&g[t], v);
-        if (old == 0) atomicAdd(&rd[0], 1u);
-        if (old + v >= top) rd[1] = 1u;
-    }
+    __device__ inline void gadd(uint32_t *g, uint32_t t, uint32_t v) const;
     __device__ inline void add(uint32_t *lds, uint32_t *h, uint32_t *g, uint16_t t) const {
         if (t < LDS_BINS) {
             atomicAdd(&lds[t], 1u);
@@ -423,6 +418,26 @@ struct NeighbourHist {
     __device__ inline void right(uint16_t t) { add(lds_right, h_right, g_right, t); }
 };
 
+constexpr uint32_t RD_QUEUE = 2048;  // queued adds of a round member walk's workgroup (rd_queue entries)
+__device__ inline uint32_t *rd_queue() {
+    extern __shared__ uint32_t rd_dyn[];
+    return rd_dyn;
+}
+// a queued add: token | right << 16 | (v == 0x8000) << 17
+__device__ inline void NeighbourHist::gadd(uint32_t *g, uint32_t t, uint32_t v) const {
+    if (!rd) {
+        atomicAdd(&g[t], v);
+        return;
+    }
+    const uint32_t j = atomicAdd(&rd[2], 1u);
+    if (j < RD_QUEUE) {
+        rd_queue()[j] = t | (g == g_right ? 1u << 16 : 0u) | (v == 1u ? 0u : 1u << 17);
+        return;
+    }
+    const uint32_t old = atomicAdd(&g[t], v);  // (queue full: added here)
+    if (old == 0) atomicAdd(&rd[0], 1u);
+    if (old + v >= top) rd[1] = 1u;
+}
 // option sel_prof: merge-index bucket of the pipeline probes (DevState::pipe_prof)
 __device__ inline int pp_bucket(uint32_t X) { return X < 8192 ? 0 : X < 20000 ? 1 : 2; }
 
@@ -852,7 +867,7 @@ struct ScanLds {
     unsigned long long scanned;
     uint32_t lrec[LREC_CAP];
     uint32_t lrec_n, lrec_base;
-    uint32_t rd[2];  // multi-merge rounds: {new pairs, a new pair reached the top count} (NeighbourHist::rd)
+    uint32_t rd[3];  // multi-merge rounds: {new pairs, a new pair reached the top count, queued adds} (NeighbourHist::rd)
 };
 // A list walk's wave with hit lanes: stage their record starts `pr` in the workgroup's LDS buffer; lanes
 // past its capacity reserve in the arena directly (one atomic per wave). Every lane of the wave calls it.
@@ -900,16 +915,64 @@ __device__ inline void scan_lds_clear(ScanLds &S) {
 }
 // the same through a round member walk's returning adds (NeighbourHist::gadd), then the workgroup's counts of
 // new pairs and top-count pairs into the member's RoundHead words (every thread calls it)
+// (every returning add of a thread is issued before the first one's value is used: a loop that tested each
+// add's return before the next add waited one memory round trip per bin)
 __device__ inline void scan_lds_flush_rd(const ScanArgs &A, ScanLds &S, const NeighbourHist &H) {
-    for (int i = threadIdx.x; i < LDS_BINS; i += blockDim.x) {
-        const uint32_t l = S.left[i], r = S.right[i];
-        if (l) H.gadd(A.left, i, l);
-        if (r) H.gadd(A.right, i, r);
+    static_assert(LDS_BINS % SCAN_THREADS == 0 && HASH_BINS % SCAN_THREADS == 0, "whole bins per thread");
+    constexpr int NL = LDS_BINS / SCAN_THREADS, NH = HASH_BINS / SCAN_THREADS, NB = 2 * (NL + NH);
+    uint32_t *g[NB];
+    uint32_t v[NB], old[NB];
+#pragma unroll
+    for (int k = 0; k < NL; k++) {
+        const uint32_t i = threadIdx.x + k * SCAN_THREADS;
+        g[2 * k] = A.left + i;
+        v[2 * k] = S.left[i];
+        g[2 * k + 1] = A.right + i;
+        v[2 * k + 1] = S.right[i];
     }
-    for (int i = threadIdx.x; i < HASH_BINS; i += blockDim.x) {
-        const uint32_t l = S.hleft[i], r = S.hright[i];
-        if (l) H.gadd(A.left, l >> 16, l & 0xffffu);
-        if (r) H.gadd(A.right, r >> 16, r & 0xffffu);
+#pragma unroll
+    for (int k = 0; k < NH; k++) {
+        const uint32_t i = threadIdx.x + k * SCAN_THREADS, l = S.hleft[i], r = S.hright[i];
+        g[2 * NL + 2 * k] = A.left + (l >> 16);
+        v[2 * NL + 2 * k] = l & 0xffffu;
+        g[2 * NL + 2 * k + 1] = A.right + (r >> 16);
+        v[2 * NL + 2 * k + 1] = r & 0xffffu;
+    }
+    // the walk's queued adds (RD_QUEUE / SCAN_THREADS per thread) join the bins' adds: every add of the thread is
+    // in flight before the first value is used (one memory round trip)
+    constexpr int NQ = RD_QUEUE / SCAN_THREADS;
+    const uint32_t nq = min(S.rd[2], RD_QUEUE);
+    const uint32_t *q = rd_queue();
+    uint32_t e[NQ], oq[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const uint32_t i = k * SCAN_THREADS + threadIdx.x;
+        e[k] = i < nq ? q[i] : ~0u;
+    }
+#pragma unroll
+    for (int k = 0; k < NB; k++) old[k] = v[k] ? atomicAdd(g[k], v[k]) : 1u;
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const uint32_t vk = (e[k] >> 17) & 1u ? 0x8000u : 1u;
+        oq[k] = e[k] != ~0u ? atomicAdd(((e[k] >> 16) & 1u ? A.right : A.left) + (e[k] & 0xFFFFu), vk) : 1u;
+    }
+    uint32_t births = 0, top = 0;
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        births += v[k] && old[k] == 0 ? 1u : 0u;
+        top |= v[k] && old[k] + v[k] >= H.top ? 1u : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const uint32_t vk = (e[k] >> 17) & 1u ? 0x8000u : 1u;
+        births += e[k] != ~0u && oq[k] == 0 ? 1u : 0u;
+        top |= e[k] != ~0u && oq[k] + vk >= H.top ? 1u : 0u;
+    }
+    births = wave_sum(births);
+    top = __ballot(top) ? 1u : 0u;
+    if ((threadIdx.x & 63) == 0) {
+        if (births) atomicAdd(&S.rd[0], births);
+        if (top) S.rd[1] = 1u;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1065,42 +1128,57 @@ __device__ inline void round_free(const ScanArgs &A0, uint32_t K, const PairTail
     }
     if (lane == 0) st->rd.freeb[w] = (int32_t)min(f, (int64_t)0x7FFFFFFF);
 }
-template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool BATCH>
-__device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs &A0, const StateHead &H, ScanLds &S) {
+// (P, PT, pr_full: the naming decision's words, loaded by the kernel's entry with the state head)
+// (PROF: the pipeline probes, st->pp_t: the member walks' phases as a list scan's, the bound workgroups' end in pp_t[13])
+template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool BATCH, bool PROF = false>
+__device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs &A0, const StateHead &H, ScanLds &S, const PairHead &P,
+                                                                 const PairTail &PT, const RoundPlans &RPL, uint32_t pr_full) {
     DevState *st = A0.st;
+    const unsigned long long t_in = PROF ? wall_clock64() : 0ull;
     const uint32_t X0 = H.cur_x, T = H.top_count, G = gridDim.x - RD_FREE_WGS;
     ScanArgs A = scan_args_resolve(A0, H, X0);
     // the members: merge X0 and the keys its decision named (pr_x == X0 + 1), while every one is a list walk
     // with room in the arena and below the vocabulary's end
-    const PairHead P = *reinterpret_cast<const PairHead *>(&st->pr_x);
-    const PairTail PT = *reinterpret_cast<const PairTail *>(&st->pr_plan[0]);
     const uint32_t keys[ROUND_MAX] = {pair_key(A.a, A.b), P.key, PT.key2, PT.key3, PT.key4};
     uint32_t K = 1;
-    if (A0.round >= 2 && P.x == X0 + 1 && st->pr_full == X0 + 1 && plan_is_list(A, H) && T) {
+    if (A0.round >= 2 && P.x == X0 + 1 && pr_full == X0 + 1 && plan_is_list(A, H) && T) {
         const uint32_t kmax = min(min((uint32_t)A0.round, (uint32_t)ROUND_MAX), A0.x_end > X0 ? A0.x_end - X0 : 1u);
         while (K < kmax && keys[K] != NO_ID && (uint64_t)(K + 1) * T <= (uint64_t)A.rec_cap) K++;
     }
-    if (blockIdx.x >= G && K > 1) {  // the free-slot bounds: one wave per range
-        round_free(A0, K, PT, (blockIdx.x - G) * (SCAN_THREADS / 64) + (threadIdx.x >> 6));
+    // Workgroups [0, RD_FREE_WGS) bound the free slots (one wave per range) and store the round's words; the
+    // members' walks take the others in turn (member j: every K-th from RD_FREE_WGS + j), so that every member's
+    // first workgroups are among the grid's first: the dispatcher starts workgroups in order, ~1000 of them
+    // took several microseconds, and a member (or bound) placed after them started that much later.
+    if (K == 1) {  // a round of one: the merge's own scan (any form; the stream form strides over the whole grid)
+        if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the replace reads the round's member keys)
+            st->rd.n = 1;
+            st->rd.key[0] = keys[0];
+        }
+        scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, false, BATCH>(A, S, H, blockIdx.x, gridDim.x);
         return;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->rd.n = K;
-        st->rd.ties = P.ties;
-        st->rd.live0 = st->live;
+    if (blockIdx.x < RD_FREE_WGS) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->rd.n = K;
+            st->rd.ties = P.ties;
+            st->rd.live0 = st->live;
+            st->rd.ties0 = st->tie_count;  // (merge X0's tied pairs, as its begin logged them)
 #pragma unroll
-        for (int e = 0; e < ROUND_MAX; e++) st->rd.key[e] = (uint32_t)e < K ? keys[e] : NO_ID;
+            for (int e = 0; e < ROUND_MAX; e++) st->rd.key[e] = (uint32_t)e < K ? keys[e] : NO_ID;
+        }
+        round_free(A0, K, PT, blockIdx.x * (SCAN_THREADS / 64) + (threadIdx.x >> 6));
+        if (PROF) {
+            __syncthreads();
+            if (threadIdx.x == 0) atomicMax(&st->pp_t[13], (unsigned long long)wall_clock64());
+        }
+        return;
     }
     A.rd_top = &st->rd.top[0];
     A.rd_birth = &st->rd.birth[0];
     A.ntk = 0;
-    if (K == 1) {  // a round of one: the merge's own scan (any form; the stream form strides over the whole grid)
-        scan_dispatch<UNROLL, NT, FILTER, PIPE, COMPACT, false, BATCH>(A, S, H, blockIdx.x, gridDim.x);
-        return;
-    }
-    const uint32_t g = G / K, j = min(blockIdx.x / g, K - 1), vb = blockIdx.x - j * g, vg = j == K - 1 ? G - j * g : g;
+    const uint32_t bi = blockIdx.x - RD_FREE_WGS, j = bi % K, vb = bi / K, vg = (G - j + K - 1) / K;
     if (j == 0) {
-        scan_list_dispatch<false, true>(A, S, H, vb, vg);  // (a list walk: plan_is_list)
+        scan_list_dispatch<PROF, true>(A, S, H, vb, vg);  // (a list walk: plan_is_list)
         return;
     }
     // member j: merge X0 + j of pair keys[j]; its list plan (two dependent round trips), then a list walk
@@ -1116,23 +1194,40 @@ __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs 
     A.rec_cap = T;
     A.rec_ctr = &st->rd.rec[j];
     A.pres = nullptr;
-    uint32_t la = A.lst_len[a], lb = A.lst_len[b], oa = A.lst_off[a], ob = A.lst_off[b];
-    const uint32_t ra = A.dir_row && a < H.lists_x && b < H.lists_x ? A.dir_row[a] : NO_LIST;
-    uint32_t r0 = NO_LIST, r1 = NO_LIST;
-    if (ra != NO_LIST) {
-        const uint64_t rb = (uint64_t)ra * A.dir_w + b;
-        r0 = A.dir[rb];
-        r1 = A.dir[rb + 1];
+    // the plan the naming decision loaded (RoundPlans, entry words), else two dependent round trips
+    uint32_t kj = 0;
+#pragma unroll
+    for (int e = 0; e < ROUND_MAX - 1; e++) kj = (uint32_t)e == j - 1 ? RPL.key[e] : kj;
+    const bool planned = RPL.gen == A0.gen && kj == keys[j];
+    if (planned) {
+#pragma unroll
+        for (int e = 0; e < ROUND_MAX - 1; e++)
+            if ((uint32_t)e == j - 1)
+#pragma unroll
+                for (int k = 0; k < 6; k++) A.pl[k] = RPL.plan[e][k];
+    } else {
+        const uint32_t la = A.lst_len[a], lb = A.lst_len[b], oa = A.lst_off[a], ob = A.lst_off[b];
+        const uint32_t ra = A.dir_row && a < H.lists_x && b < H.lists_x ? A.dir_row[a] : NO_LIST;
+        uint32_t r0 = NO_LIST, r1 = NO_LIST;
+        if (ra != NO_LIST) {
+            const uint64_t rb = (uint64_t)ra * A.dir_w + b;
+            r0 = A.dir[rb];
+            r1 = A.dir[rb + 1];
+        }
+        A.pl[0] = la; A.pl[1] = lb; A.pl[2] = oa; A.pl[3] = ob; A.pl[4] = r0; A.pl[5] = r1;
     }
     A.plan_ok = 1;
-    A.pl[0] = la; A.pl[1] = lb; A.pl[2] = oa; A.pl[3] = ob; A.pl[4] = r0; A.pl[5] = r1;
+    if (PROF && vb == 0 && threadIdx.x == 0) {  // member j's walk starts (its plan in): sel_prof[22] from the launch's start
+        atomicAdd(&st->sel_prof[22], wall_clock64() - t_in);
+        atomicAdd(&st->sel_prof[23], planned ? 1ull : 1ull << 32);
+    }
 #pragma unroll
     for (int e = 0; e < ROUND_MAX - 1; e++) A.tk[e] = (uint32_t)e < j ? keys[e] : 0u;
     A.ntk = j;
     A.rd_touch = &st->rd.touch[j];
     A.rd_top = &st->rd.top[j];
     A.rd_birth = &st->rd.birth[j];
-    if (scan_list_dispatch<false, true>(A, S, H, vb, vg) && vb == 0 && threadIdx.x == 0) st->rd.walk[j] = 1;
+    if (scan_list_dispatch<PROF, true>(A, S, H, vb, vg) && vb == 0 && threadIdx.x == 0) st->rd.walk[j] = 1;
 }
 // PROF (option sel_prof): the pipeline probes; a separate instantiation, so the production kernel's
 // code and register allocation are untouched by them
@@ -1152,6 +1247,24 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
     // the state head and the argument words a list walk needs, fetched together (one round trip, not a
     // chain of kernarg cache misses in the order the code first uses them): one asm consumes them all
     const StateHead H = *reinterpret_cast<const StateHead *>(stp);
+    // a round's scan: the naming decision's words in the same round trip
+    PairHead P{};
+    PairTail PT{};
+    RoundPlans RPL{};
+    uint32_t pr_full = 0;
+    if (ROUND) {
+        P = *reinterpret_cast<const PairHead *>(&stp->pr_x);
+        PT = *reinterpret_cast<const PairTail *>(&stp->pr_plan[0]);
+        RPL = stp->rp;
+        pr_full = stp->pr_full;
+        asm volatile("" ::"s"(P.x), "s"(P.key), "s"(P.ties), "s"(PT.key2), "s"(PT.key3), "s"(PT.key4), "s"(PT.h2), "s"(PT.h3),
+                     "s"(PT.h4), "s"(PT.h5), "s"(PT.h6), "s"(PT.hmax), "s"(pr_full), "s"(RPL.gen), "s"(RPL.key[0]),
+                     "s"(RPL.key[1]), "s"(RPL.key[2]), "s"(RPL.key[3]));
+        // the round's argument words (a kernarg word first used deep in the walk's setup cost a cache-miss round trip)
+        asm volatile("" ::"s"(A0.round), "s"(A0.x_end), "s"(A0.lst_len), "s"(A0.lst_off), "s"(A0.dir), "s"(A0.dir_w),
+                     "s"(A0.log), "s"(A0.list_ratio), "s"(A0.nb), "s"(A0.tokcnt), "s"(A0.cs), "s"(A0.hv.summ), "s"(A0.hv.sup),
+                     "s"(A0.hv.C), "s"(A0.hv.nb), "s"(A0.hv.nsb), "s"(A0.prof));
+    }
     asm volatile("" ::"s"(A0.dyn), "s"(A0.X), "s"(A0.gen), "s"(A0.rec_arena), "s"(A0.rec_cap), "s"(A0.count_deltas),
                  "s"(A0.tok), "s"(A0.lists), "s"(A0.rec), "s"(A0.left), "s"(A0.right), "s"(A0.dir_row), "s"(A0.xx_out),
                  "s"(A0.occ_out), "s"(A0.n), "s"(H.halt), "s"(H.cur_key), "s"(H.arena_top), "s"(H.lists_valid),
@@ -1160,7 +1273,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
     if (A0.dyn && H.halt) return;
     __shared__ ScanLds S;
     if (ROUND) {
-        round_scan<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH>(A0, H, S);
+        round_scan<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH, PROF>(A0, H, S, P, PT, RPL, pr_full);
         return;
     }
     const ScanArgs A = scan_args_resolve(A0, H, A0.X);
@@ -1279,7 +1392,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     const uint32_t *NB = A.nb, sh = by_b ? 16u : 0u;  // the build-time neighbour on the partner's side
     const uint32_t partner = by_b ? A.a : A.b, key = by_b ? A.b : A.a;
     scan_lds_clear(S);
-    if (threadIdx.x == 0) { S.any = 0; S.lrec_n = 0; S.rd[0] = S.rd[1] = 0; }
+    if (threadIdx.x == 0) { S.any = 0; S.lrec_n = 0; S.rd[0] = S.rd[1] = S.rd[2] = 0; }
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{S.left, S.right, A.left, A.right, S.hleft, S.hright};
@@ -1424,7 +1537,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     uint32_t *s_left = S.left, *s_right = S.right;
     uint32_t &s_any = S.any;
     scan_lds_clear(S);
-    if (threadIdx.x == 0) { s_any = 0; S.lrec_n = 0; S.rd[0] = S.rd[1] = 0; }
+    if (threadIdx.x == 0) { s_any = 0; S.lrec_n = 0; S.rd[0] = S.rd[1] = S.rd[2] = 0; }
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{s_left, s_right, A.left, A.right, S.hleft, S.hright};
@@ -2601,29 +2714,35 @@ __device__ inline bool dev_zig_at_max_load(uint64_t cap, uint64_t D);
 // wraps, so it is first in slot order -- the pair-select argument of zbpe_select_next, per member), and the
 // Zig capacity is C and not at a max load for every live-pair count the earlier members can leave (each member
 // kills its own pair and at most one pair per new pair: D in [D0 - j, D0 + births - j]).
+// (*why: what ended the round -- RoundWhy)
+enum RoundWhy : uint32_t { RW_ALL, RW_FLAGS, RW_WALK, RW_TOUCH, RW_REC, RW_END, RW_ARENA, RW_SLACK, RW_CAP, RW_N };
 __device__ inline uint32_t round_valid(const RoundHead &R, uint32_t T, uint32_t X0, uint32_t x_end, uint32_t C,
-                                       uint32_t arena_top, uint32_t rec_cap) {
-    uint32_t k = 1;
+                                       uint32_t arena_top, uint32_t rec_cap, uint32_t *why = nullptr) {
+    uint32_t k = 1, w = RW_ALL;
     uint64_t births = R.birth[0];
     uint32_t flags = R.top[0];
     const uint32_t n = min(R.n, (uint32_t)ROUND_MAX);
 #pragma unroll
     for (uint32_t j = 1; j < (uint32_t)ROUND_MAX; j++) {
         if (j >= n) break;
-        if (flags || !R.walk[j] || R.touch[j] || R.rec[j] != T || X0 + j >= x_end) break;
-        if ((uint64_t)arena_top + (uint64_t)(j + 1) * T > rec_cap) break;
+        w = flags ? RW_FLAGS : !R.walk[j] ? RW_WALK : R.touch[j] ? RW_TOUCH : R.rec[j] != T ? RW_REC : X0 + j >= x_end ? RW_END : RW_ALL;
+        if (w != RW_ALL) break;
+        if ((uint64_t)arena_top + (uint64_t)(j + 1) * T > rec_cap) { w = RW_ARENA; break; }
         const uint64_t slack = R.ties == j + 1 ? ~0ull
                                : (R.freeb[j] < 0 || R.freeb[0] < 0) ? 0ull
                                                                     : (uint64_t)min(R.freeb[j], R.freeb[0]);
-        if (births >= slack) break;
+        if (births >= slack) { w = RW_SLACK; break; }
         const int64_t lo = (int64_t)R.live0 - (int64_t)j, hi = (int64_t)R.live0 + (int64_t)births - (int64_t)j;
         if (lo < 1 || dev_zig_cap_for((uint64_t)lo) != C || dev_zig_cap_for((uint64_t)hi) != C ||
-            dev_zig_at_max_load(C, (uint64_t)hi))
+            dev_zig_at_max_load(C, (uint64_t)hi)) {
+            w = RW_CAP;
             break;
+        }
         k = j + 1;
         births += R.birth[j];
         flags |= R.top[j];
     }
+    if (why) *why = w;
     return k;
 }
 // pair selects: merge X+1's candidate bound, by the replace's extra workgroup (defined with the home views below)
@@ -2748,10 +2867,29 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     if (lb >= apply_blocks) update_preload(lj, lj + 65536, Xp, lb - apply_blocks, per, dv);
     const StateHead H = load_head(st);
     const RoundHead &RH = st->rd;  // (read in place: a register copy indexed by the member went to scratch)
+    if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the round scan's stamps (as zbpe_replace)
+        const unsigned long long now = wall_clock64();
+        if (st->pp_t[4]) {
+            unsigned long long *P = st->pipe_prof[pp_bucket(H.cur_x)];
+            const unsigned long long t0 = st->pp_t[0];
+            P[0] += st->pp_t[1] - t0;
+            P[1] += st->pp_t[2] - t0;
+            P[2] += st->pp_t[3] - t0;
+            P[3] += now - t0;
+            P[4]++;
+            if (st->pp_t[13] > t0) P[15] += st->pp_t[13] - t0;
+        }
+        st->pp_t[1] = st->pp_t[2] = st->pp_t[3] = st->pp_t[4] = st->pp_t[13] = 0;
+        st->pp_t[5] = now;
+    }
     if (H.halt) return;
     const uint32_t Tc = H.top_count;
-    const uint32_t k = round_valid(RH, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap);
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->rd_v = k;
+    uint32_t why;
+    const uint32_t k = round_valid(RH, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap, &why);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->rd_v = k;
+        if (RH.n > 1) atomicAdd(&st->rd_why[why], 1u);  // (rounds with named keys: what ended them)
+    }
     if (j >= k) return;
     const uint32_t X = H.cur_x + j, key = RH.key[j], a = key & 0xFFFF, b = key >> 16;
     if (lb < apply_blocks) {
@@ -3265,8 +3403,16 @@ enum RollIn : int { RI_REC, RI_TOTAL_OCC, RI_HOLES, RI_ARENA_TOP, RI_ARENA_REP, 
 // The fused select's roll words, loaded at kernel start straight into LDS by lanes [0, RI_WORDS) of
 // wave 0 (global_load_lds: no registers held across the kernel); they are stable until the last
 // block rolls, and block_ticket_last's vmcnt(0) + barrier publishes them to the block.
-__device__ inline void roll_preload(const DevState *st, const uint32_t *delta, uint32_t X, uint32_t *s_pre) {
+// (rd: a multi-merge round's select -- lanes [RI_WORDS, RI_WORDS + RD_WORDS) load the RoundHead words too)
+constexpr uint32_t RD_WORDS = sizeof(RoundHead) / 4;
+static_assert(RI_WORDS + RD_WORDS <= 64, "one wave loads the roll words");
+__device__ inline void roll_preload(const DevState *st, const uint32_t *delta, uint32_t X, uint32_t *s_pre, bool rd = false) {
     const uint32_t lane = threadIdx.x;
+    if (rd && lane >= RI_WORDS && lane < RI_WORDS + RD_WORDS) {
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(&st->rd) + (lane - RI_WORDS),
+                                         (__attribute__((address_space(3))) void *)s_pre, 4, 0, 0);
+        return;
+    }
     if (lane >= RI_WORDS) return;
     const uint32_t *w = lane == RI_REC ? &st->rec_count : lane == RI_TOTAL_OCC ? &st->total_occ
                         : lane == RI_HOLES ? &st->holes_made : lane == RI_ARENA_TOP ? &st->arena_top
@@ -4247,7 +4393,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
                                    uint32_t plan_gen = 0, uint32_t pair_x = 0, bool m3_w4 = false,
-                                   bool chain = false, bool chain2 = false, bool chain3 = false) {
+                                   bool chain = false, bool chain2 = false, bool chain3 = false, bool rplan = false) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
     // plan (NT >= 256): wave 3 finds the smallest home's key itself and loads its scan plan during the
     // carries; the commit below stores it with cur_key
@@ -4313,6 +4459,22 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) m1 = min(m1, (uint64_t)__shfl_xor(m1, off));
         if (lane == 0) plan_compute(plan, (uint32_t)m1, s_plan);
+    }
+    // rplan (a multi-merge round's select): wave 5 finds the next tied keys by home itself and loads their scan
+    // plans, one lane each, beside the carries (the round's scan then walks them without a plan round trip)
+    if (NT >= 512 && rplan && plan_on && w == 5 && len >= 2) {
+        uint64_t q[ROUND_MAX];
+        uint32_t hmx;
+        wave_minK<ROUND_MAX>(list, len, q, hmx);
+        if (lane >= 1 && lane < (uint32_t)ROUND_MAX && q[lane] != ~0ull) {
+            const uint32_t key = (uint32_t)q[lane];
+            uint32_t pl[6];
+            plan_compute(plan, key, pl);
+#pragma unroll
+            for (int k = 0; k < 6; k++) st->rp.plan[lane - 1][k] = pl[k];
+            st->rp.key[lane - 1] = key;
+        }
+        if (lane == 0) st->rp.gen = plan_gen;
     }
     __syncthreads();
     if (!ws && !cs) {  // a map of at most 4096 slots: the last free slot needs the carry into slot 0
@@ -4421,17 +4583,19 @@ __device__ inline void round_roll(const Tables &T, DevState *st, const StateHead
                                   FinishOut *fo, uint32_t *rlog) {
     const uint32_t k = H0.rd_v, X0 = H0.cur_x, Tc = H0.top_count;
     RoundHead &R = st->rd;
+    // the RoundHead words, preloaded into LDS at the kernel's entry (roll_preload rd)
+    const RoundHead &RP = *reinterpret_cast<const RoundHead *>(pre + RI_WORDS);
     uint32_t rec[ROUND_MAX], key[ROUND_MAX], dec[ROUND_MAX];
 #pragma unroll
     for (int j = 0; j < ROUND_MAX; j++) {
-        rec[j] = R.rec[j];
-        key[j] = R.key[j];
-        dec[j] = R.dec[j];
+        rec[j] = RP.rec[j];
+        key[j] = RP.key[j];
+        dec[j] = RP.dec[j];
     }
     rec[0] = pre[RI_REC];
     const uint32_t holes = pre[RI_HOLES], arena_top = pre[RI_ARENA_TOP], arena_rep = pre[RI_ARENA_REP], total_occ = pre[RI_TOTAL_OCC];
     const long long live_tokens = (long long)(((uint64_t)pre[RI_LIVE_TOK_HI] << 32) | pre[RI_LIVE_TOK_LO]);
-    uint32_t ties = log[X0 - 256].ties, sum = 0;
+    uint32_t ties = RP.ties0, sum = 0;
 #pragma unroll
     for (uint32_t j = 0; j < (uint32_t)ROUND_MAX; j++) {
         if (j >= k) break;
@@ -4593,8 +4757,8 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // written by the launch before); then the last workgroup to arrive is elected (returning
         // atomics, per-XCD counters, then the top one) and arrives once more when done. Else a
         // workgroup's arrival is one non-returning add to its XCD's counter.
-        // (rounds: ties come in streaks, a round is one; the carries are always precomputed)
-        const bool pfx = N.round ? N.cs != nullptr : N.cs && N.B.log[X - 256].ties > 1;
+        // (rounds: the round's first merge was tied -- its scan stored the count -- ties come in streaks)
+        const bool pfx = N.cs && (N.round ? ld_wt(&st->rd.ties0) > 1 : N.B.log[X - 256].ties > 1);
         // merge X's neighbour deltas, cleared for merge X + 2 by these workgroups (off the argmax's
         // critical path: the argmax grid is sized by the hot list alone; nothing in this launch reads
         // [0, 2X) -- the roll reads the tail words past it)
@@ -4676,7 +4840,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     __shared__ uint32_t s_key[NEXT_CAND];
     __shared__ uint32_t s_pc[NEXT_MAX_SEL], s_pt[NEXT_MAX_SEL], s_pk[NEXT_MAX_SEL];
     __shared__ uint32_t s_pre[64];
-    roll_preload(st, delta, X, s_pre);
+    roll_preload(st, delta, X, s_pre, N.round != 0);
     if (N.prof && blockIdx.x == nref && tid == 0) {  // the first argmax block
         const unsigned long long now = wall_clock64();
         st->sel_t0 = now;
@@ -4825,7 +4989,12 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     if (N.prof && tid == 0) atomicMax(&st->sel_ta, (unsigned long long)wall_clock64());
     if (!single && !block_ticket_last(&st->ticket, sel_blocks, &s_flag)) return;
-    const bool pfx = nref && N.cs && (N.round || N.B.log[X - 256].ties > 1);  // the refresh precomputes the carries (its predicate)
+    if (N.round) {  // roll_preload's LDS words (wave 0) landed (a single argmax block took no ticket)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // the refresh precomputes the carries (its predicate; a round's RoundHead words are in s_pre: roll_preload)
+    const bool pfx = nref && N.cs && (N.round ? reinterpret_cast<const RoundHead *>(s_pre + RI_WORDS)->ties0 > 1 : N.B.log[X - 256].ties > 1);
     // the next launch's refresh count (the launch before this one used it and has ended)
     if (tid < 9) st_wt(N.rtk + (N.round ? N.par ^ 1u : (X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
     unsigned long long pt = 0;
@@ -5116,7 +5285,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
                               plan_on, plan, N.gen, N.pair && NB.X + 1 < N.x_end ? NB.X + 1 : 0u, N.m3_w4 != 0,
-                              N.skip_refresh != 0 && N.chain != 0, N.chain >= 2, N.chain >= 3);
+                              N.skip_refresh != 0 && N.chain != 0, N.chain >= 2, N.chain >= 3, N.round != 0);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }

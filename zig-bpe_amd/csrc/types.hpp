@@ -34,6 +34,7 @@ struct RoundHead {
     uint32_t n;                  // members the scan took (1 .. ROUND_MAX; written by its block 0)
     uint32_t ties;               // tied keys at the decision that named them (pr_ties)
     int32_t live0;               // live pairs at the round's start (DevState::live as the scan saw it)
+    uint32_t ties0;              // merge cur_x's tied pairs (DevState::tie_count as the scan saw it)
     uint32_t key[ROUND_MAX];     // member keys (key[0] = cur_key)
     uint32_t walk[ROUND_MAX];    // member j >= 1 walked by a list form (a stream scan is never a member)
     uint32_t touch[ROUND_MAX];   // an occurrence of member j touches one of an earlier member's
@@ -44,7 +45,14 @@ struct RoundHead {
                                  // home block and before the next tied home (j >= 1); -1: no bound
     uint32_t dec[ROUND_MAX];     // tied pairs member j decremented first (the replace), for the tie counts
 };
-static_assert(sizeof(RoundHead) == 4 * (3 + 8 * ROUND_MAX), "round head: packed words");
+static_assert(sizeof(RoundHead) == 4 * (4 + 8 * ROUND_MAX), "round head: packed words");
+struct RoundPlans {
+    uint32_t key[ROUND_MAX - 1];
+    uint32_t gen;
+    uint32_t pad[3];
+    uint32_t plan[ROUND_MAX - 1][6];
+};
+static_assert(sizeof(RoundPlans) == 4 * (8 + 6 * (ROUND_MAX - 1)), "round plans: packed words");
 // Device-resident state. Host reads a copy after each merge (one small D2H per merge).
 struct DevState {
     // ---- hot header (the first 96 B): the words the merge kernels read first, loaded together in one
@@ -142,6 +150,10 @@ struct DevState {
     // rounds applied beyond their first members
     alignas(128) RoundHead rd;
     uint32_t rd_merges;
+    uint32_t rd_why[10];     // rounds that walked named keys, by what ended them (RoundWhy, kernels.hpp)
+    // the named keys' scan plans (ScanArgs::pl), by a spare wave of the naming decision (zbpe_select_next, round
+    // mode), valid for layout generation rp.gen: a member walk then starts without loading its lists' words
+    alignas(16) RoundPlans rp;
 };
 struct PairHead {  // what the light test reads (the kernel entry's round trip)
     uint32_t x, key, slack, ties, births, dt, hits, plan_gen;
