@@ -28,7 +28,7 @@ for s in $STEPS; do
           python3 tools/merge_timeline.py --analyse $O/tl $O/tl_log.json > $O/merge_timeline.json || exit 7
           find $O/tl -name "*kernel_trace.csv" -size +20M -delete ;;
     probes) timeout -k 10 300 python3 tools/trace_run.py --opt sel_prof=1 $OPT > $O/sel_prof.txt 2>&1 || { tail $O/sel_prof.txt; exit 8; } ;;
-    dist) timeout -k 10 1500 python -u -m pytest tests/test_dist.py -m gpu -v -s --durations=20 --timeout 1100 --timeout-method thread > $O/pytest_dist.log 2>&1 || { tail -30 $O/pytest_dist.log; exit 9; }
+    dist) ZBPE_LONG=1 timeout -k 10 1500 python -u -m pytest tests/test_dist.py -m gpu -v -s --durations=20 --timeout 1100 --timeout-method thread > $O/pytest_dist.log 2>&1 || { tail -30 $O/pytest_dist.log; exit 9; }
           grep HANDOVER $O/pytest_dist.log; tail -3 $O/pytest_dist.log ;;
   esac
 done

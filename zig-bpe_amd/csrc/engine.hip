@@ -199,8 +199,11 @@ zbpe_status Engine::sync_state() {
     if (h_st->error & 512u)
         return fail(ZBPE_INVALID_ARGUMENT, "a byte pair occurs 2^32 times or more in the corpus: pair counts are u32 on the device");
     if (h_st->error)
-        return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow, 16 home count range, 32 dirty list overflow, 64 occurrences != count, 128 tie collection, 1024 select wait timed out)",
-                    h_st->error);
+        return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow, 16 home count range, 32 dirty list overflow, 64 occurrences != count, 128 tie collection, 1024 select wait timed out)%s",
+                    h_st->error,
+                    (h_st->error & 64u) ? (" [first 64: merge " + std::to_string(h_st->err_x) + " found " + std::to_string(h_st->err_occ) +
+                                           " occurrences of a pair counted " + std::to_string(h_st->err_cnt) + ", rank " + std::to_string(rank) + "]").c_str()
+                                        : "");
     return ZBPE_OK;
 }
 
@@ -421,11 +424,15 @@ zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio, bool ranges) {
     const uint32_t max_len = (uint32_t)std::min<uint64_t>(0xFFFFFFFEu, (uint64_t)n / ratio);
     zbpe_list_offsets<<<1, 1024, 0, stream>>>(d_list_total, pres_vp, max_len, T.lst_off, T.lst_len, d_st, lists_x);
     LAUNCH_OK();
-    if (list_nb) {  // the build-time neighbours of every list entry (the filtered list walk)
+    // the build-time neighbours of every list entry (the filtered list walk). Sharded, the successor of the shard's
+    // last token is the next shard's first live token (the halo): an occurrence across the edge is this shard's,
+    // found from a's list; the predecessor of its first token stays HOLE (that occurrence is the left shard's)
+    if (list_nb) {
         CHECK(ensure(&d_nb, nb_cap, (size_t)n + 64, "list neighbours"));
     }
     zbpe_list_scatter<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt, T.lst_off,
-                                                                       T.lst_len, d_lists, list_nb ? d_nb : nullptr);
+                                                                       T.lst_len, d_lists, list_nb ? d_nb : nullptr,
+                                                                       dist() && halo.nright > 0 ? halo_right(halo, 0) : (uint32_t)HOLE);
     LAUNCH_OK();
     // successor ranges: training on one stream (a shard's edge entries have no successor in it)
     dirs_built = false;

@@ -1364,6 +1364,19 @@ __global__ void __launch_bounds__(256) zbpe_encode_apply_batch(uint16_t *tok, in
     st->ticket = 0;
 }
 
+// A walk of b's list (sharded): the occurrence leaving the shard -- its a this shard's last live token, its b the next
+// shard's first (the halo), in no list here -- is this shard's; one thread checks and records it. Returns 1 if found.
+__device__ inline uint32_t list_edge_occurrence(const ScanArgs &A, NeighbourHist &H, uint32_t &xx) {
+    if (A.halo.nright == 0 || halo_right(A.halo, 0) != A.b) return 0;
+    const int64_t p = prev_live(A.tok, A.n);
+    if (p < 0 || A.tok[p] != A.a || !occ_slow(A, H, p, xx)) return 0;
+    const uint32_t j = atomicAdd(A.rec_ctr, 1u);
+    atomicAdd(A.occ_out, 1u);
+    if (j < A.rec_cap) A.rec[j] = (uint32_t)p;
+    else atomicOr(&A.st->error, 8u);
+    return 1;
+}
+
 // Filtered list scan (scan_dispatch: both tokens existed at the list build). Each thread reads the
 // build-time neighbours of LIST_EPT consecutive entries (two 16-B loads of the u16 neighbour array,
 // coalesced); only entries whose neighbour was the pair's other token can be occurrences (about the
@@ -1401,6 +1414,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     const int64_t nvec = (A.n + 7) / 8;
     const int lane = threadIdx.x & 63;
     uint32_t xx = 0, any = 0;
+    if (by_b && vb == 0 && threadIdx.x == 0) any = list_edge_occurrence(A, H, xx);
     const uint32_t gstride = vg * per_block;
     // block-uniform trip count (every lane of a wave takes part in the shuffles and ballots)
     for (uint32_t b0 = vb * per_block; b0 < span; b0 += gstride) {
@@ -1546,17 +1560,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     const uint32_t key = by_b ? A.b : A.a;
     uint32_t xx = 0, any = 0;
     const int lane = threadIdx.x & 63;
-    if (by_b && vb == 0 && threadIdx.x == 0 && A.halo.nright > 0 && halo_right(A.halo, 0) == A.b) {
-        // the occurrence leaving the shard: its b is the next shard's, in no list here
-        const int64_t p = prev_live(tok, A.n);
-        if (p >= 0 && tok[p] == A.a && occ_slow(A, H, p, xx)) {
-            const uint32_t j = atomicAdd(A.rec_ctr, 1u);
-            atomicAdd(A.occ_out, 1u);
-            if (j < A.rec_cap) A.rec[j] = (uint32_t)p;
-            else atomicOr(&A.st->error, 8u);
-            any = 1;
-        }
-    }
+    if (by_b && vb == 0 && threadIdx.x == 0) any = list_edge_occurrence(A, H, xx);
     const uint32_t stride = vg * NT;
     const int64_t nvec = (A.n + 7) / 8;
     const uint32_t len64 = (len + 63) & ~63u;  // wave-uniform trip count (wave_append)
@@ -2240,7 +2244,8 @@ __global__ void __launch_bounds__(LIST_THREADS) zbpe_list_scatter(const uint16_t
                                                                   const uint32_t *__restrict__ colpre,
                                                                   const uint32_t *__restrict__ lst_off,
                                                                   const uint32_t *__restrict__ lst_len,
-                                                                  uint32_t *__restrict__ lists, uint32_t *__restrict__ nb) {
+                                                                  uint32_t *__restrict__ lists, uint32_t *__restrict__ nb,
+                                                                  uint32_t tail_succ) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
     for (uint32_t t = threadIdx.x; t < vp; t += LIST_THREADS)
         cur[t] = lst_len[t] == NO_LIST ? NO_LIST : lst_off[t] + colpre[(uint64_t)blockIdx.x * vp + t];
@@ -2257,7 +2262,8 @@ __global__ void __launch_bounds__(LIST_THREADS) zbpe_list_scatter(const uint16_t
                 const uint32_t j = atomicAdd(&cur[t], 1u);
                 lists[j] = (uint32_t)(p + k);
                 if (nb) {
-                    const uint32_t sc = k < 7 ? (p + k + 1 < n ? tok_at(v, k + 1) : HOLE) : (p + 8 < n ? after : HOLE);
+                    // (the last position's successor: tail_succ, the next shard's first live token, or HOLE)
+                    const uint32_t sc = k < 7 ? (p + k + 1 < n ? tok_at(v, k + 1) : tail_succ) : (p + 8 < n ? after : tail_succ);
                     const uint32_t pd = k > 0 ? tok_at(v, k - 1) : before;
                     nb[j] = pd << 16 | sc;
                 }
@@ -2672,6 +2678,14 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
 // recorded occurrences (X at the start, a hole at the consumed b), the rest update the counts
 // (identical on every rank: the deltas were summed), and one thread checks whether this shard's
 // first live token is the b of an occurrence owned by the left rank (then it becomes a hole).
+// error 64 (the occurrences a merge found != its pair's count): the first one's merge and numbers, for the message
+__device__ inline void occ_check_failed(DevState *st, uint32_t X, uint32_t occ, uint32_t cnt) {
+    if (atomicCAS(&st->err_x, 0u, X) == 0u) {
+        st->err_occ = occ;
+        st->err_cnt = cnt;
+    }
+    atomicOr(&st->error, 64u);
+}
 struct ReplaceArgs {
     uint16_t *tok;
     int64_t n;
@@ -2844,7 +2858,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
         return;
     }
     const uint32_t ublk = blockIdx.x - apply_blocks;
-    if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) atomicOr(&st->error, 64u);  // occurrences != count
+    if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) occ_check_failed(st, R.X, R.tail[1], H.top_count);
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof, H.top_count,
                  R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2, pr_key3, pr_key4);
     if (R.prof) {
@@ -2912,7 +2926,7 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     }
     const uint32_t ublk = lb - apply_blocks;
     const uint32_t *tj = lj + 2 * 65536;
-    if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc) atomicOr(&st->error, 64u);  // occurrences != count
+    if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc) occ_check_failed(st, X, tj[1], Tc);
     const RoundCtx rc{left, j, &st->rd.key[0], &st->rd.dec[0]};
     update_block(T, st, lj, lj + 65536, tj, a, b, X, key, ublk, per, dv, H.theta, 0, Tc, NO_ID, NO_ID, NO_ID, NO_ID, &rc, Xp);
 }

@@ -94,14 +94,13 @@ struct DevState {
     uint32_t mismatches;
     uint32_t last_occ;       // occurrences merged by the last merge (copied by zbpe_reset_merge)
     uint32_t total_occ;      // running sum of last_occ (encode bookkeeping)
-    uint32_t pad_dirty;
+    uint32_t err_x;          // the first failed occurrence check (error 64): merge X, occurrences found, count
     uint32_t ticket;         // zbpe_select: blocks done (the last one reduces), reset by it
     uint32_t last_gocc;      // occurrences merged by the last merge on all ranks
     uint32_t consumed;       // 1: this shard's first live token was the b of the left rank's last occurrence
     uint32_t holes_made;     // slots of this shard turned into holes by the current merge
     uint32_t last_holes;     // holes_made of the last merge (rolled by zbpe_select)
-    int32_t pad_by_b;
-    uint32_t pad3;
+    uint32_t err_occ, err_cnt;
     unsigned long long scanned_slots;  // stream slots the scans actually streamed (block skipping)
     // device-resident merge loop (Engine::run_batch): the host enqueues a batch of merges whose
     // kernels read the pair from here; a merge the device cannot finish alone halts the batch
