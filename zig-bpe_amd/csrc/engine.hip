@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -21,6 +22,22 @@
 #include "zig_order.hpp"
 
 namespace zbpe {
+
+// Device allocations. ZBPE_POISON=1 (diagnostics) fills every new buffer with 0xA5 bytes, so that a read of
+// memory no kernel wrote fails the same way on every run instead of depending on what the allocator hands back.
+static hipError_t dev_alloc_raw(void **p, size_t bytes) {
+    static const bool poison = getenv("ZBPE_POISON") && atoi(getenv("ZBPE_POISON")) != 0;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess && poison) {
+        e = hipMemset(*p, 0xA5, bytes);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+    }
+    return e;
+}
+template <class T_>
+static hipError_t dev_alloc(T_ **p, size_t bytes) {
+    return dev_alloc_raw(reinterpret_cast<void **>(p), bytes);
+}
 
 #define HIP_OK(expr)                                                                       \
     do {                                                                                   \
@@ -97,29 +114,29 @@ zbpe_status Engine::init(int dev) {
     HIP_OK(hipSetDevice(dev));
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIP_OK(hipHostMalloc((void **)&h_st, sizeof(DevState), hipHostMallocDefault));
-    HIP_OK(hipMalloc(&d_st, sizeof(DevState)));
-    HIP_OK(hipMalloc(&d_delta, 2 * DELTA_WORDS * sizeof(uint32_t)));  // two: merges alternate (delta_of)
+    HIP_OK(dev_alloc(&d_st, sizeof(DevState)));
+    HIP_OK(dev_alloc(&d_delta, 2 * DELTA_WORDS * sizeof(uint32_t)));  // two: merges alternate (delta_of)
     HIP_OK(hipMemset(d_delta, 0, 2 * DELTA_WORDS * sizeof(uint32_t)));
-    HIP_OK(hipMalloc(&d_rdelta, (size_t)ROUND_MAX * DELTA_WORDS * sizeof(uint32_t)));
+    HIP_OK(dev_alloc(&d_rdelta, (size_t)ROUND_MAX * DELTA_WORDS * sizeof(uint32_t)));
     HIP_OK(hipMemset(d_rdelta, 0, (size_t)ROUND_MAX * DELTA_WORDS * sizeof(uint32_t)));
-    HIP_OK(hipMalloc(&d_rlog, MAX_BATCH * sizeof(uint32_t)));
+    HIP_OK(dev_alloc(&d_rlog, MAX_BATCH * sizeof(uint32_t)));
     h_rlog.resize(MAX_BATCH);
-    HIP_OK(hipMalloc(&d_hist, 65536 * sizeof(uint32_t)));
-    HIP_OK(hipMalloc(&T.tok_cnt, 65536 * sizeof(int32_t)));
-    HIP_OK(hipMalloc(&d_log, 65536 * sizeof(MergeLog)));
-    HIP_OK(hipMalloc(&T.lst_off, 65536 * sizeof(uint32_t)));
-    HIP_OK(hipMalloc(&T.lst_len, 65536 * sizeof(uint32_t)));
-    HIP_OK(hipMalloc(&d_list_total, 65536 * sizeof(uint32_t)));
+    HIP_OK(dev_alloc(&d_hist, 65536 * sizeof(uint32_t)));
+    HIP_OK(dev_alloc(&T.tok_cnt, 65536 * sizeof(int32_t)));
+    HIP_OK(dev_alloc(&d_log, 65536 * sizeof(MergeLog)));
+    HIP_OK(dev_alloc(&T.lst_off, 65536 * sizeof(uint32_t)));
+    HIP_OK(dev_alloc(&T.lst_len, 65536 * sizeof(uint32_t)));
+    HIP_OK(dev_alloc(&d_list_total, 65536 * sizeof(uint32_t)));
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_list_hist, hipFuncAttributeMaxDynamicSharedMemorySize, PRES_MAX_VP * 4));
     HIP_OK(hipFuncSetAttribute((const void *)zbpe_list_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, PRES_MAX_VP * 4));
-    HIP_OK(hipMalloc(&d_halo, sizeof(Halo)));
+    HIP_OK(dev_alloc(&d_halo, sizeof(Halo)));
     h_log.resize(65536);
     bev.resize(BEV_PER_MERGE * MAX_BATCH + 2);  // per timed merge + the batch's first and last
     for (auto &e : bev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no L2 writeback
-    HIP_OK(hipMalloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
-    HIP_OK(hipMalloc(&d_cand, ((size_t)NEXT_MAX_SEL * (NEXT_CAND + 1) + 64) * sizeof(uint32_t)));  // keys | pkey | lastpair
-    HIP_OK(hipMalloc(&d_rtk, RTK_WORDS * sizeof(uint32_t)));
-    HIP_OK(hipMalloc(&d_count_hist, COUNT_BINS * sizeof(uint32_t)));
+    HIP_OK(dev_alloc(&d_partial, ARGMAX_MAX_BLOCKS * sizeof(MaxRec)));
+    HIP_OK(dev_alloc(&d_cand, ((size_t)NEXT_MAX_SEL * (NEXT_CAND + 1) + 64) * sizeof(uint32_t)));  // keys | pkey | lastpair
+    HIP_OK(dev_alloc(&d_rtk, RTK_WORDS * sizeof(uint32_t)));
+    HIP_OK(dev_alloc(&d_count_hist, COUNT_BINS * sizeof(uint32_t)));
     HIP_OK(hipHostMalloc((void **)&h_count_hist, COUNT_BINS * sizeof(uint32_t), hipHostMallocDefault));
     for (auto &e : ev) HIP_OK(hipEventCreate(&e));
     // the initial byte-pair histogram keeps 128 KiB of bins in LDS
@@ -140,7 +157,7 @@ zbpe_status Engine::ensure(T_ **p, size_t &cap, size_t need, const char *what) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     size_t c = std::max(need, cap * 2);
-    if (hipMalloc((void **)p, c * sizeof(T_)) != hipSuccess) {
+    if (dev_alloc((void **)p, c * sizeof(T_)) != hipSuccess) {
         (void)hipGetLastError();
         *p = nullptr;
         cap = 0;
@@ -184,12 +201,12 @@ zbpe_status Engine::init_dist(int r, int w, std::unique_ptr<Comm> c) {
     world = w;
     comm = std::move(c);
     HIP_OK(hipSetDevice(device));
-    HIP_OK(hipMalloc(&d_bnd_mine, sizeof(Boundary)));
-    HIP_OK(hipMalloc(&d_bnd_all, (size_t)w * sizeof(Boundary)));
+    HIP_OK(dev_alloc(&d_bnd_mine, sizeof(Boundary)));
+    HIP_OK(dev_alloc(&d_bnd_all, (size_t)w * sizeof(Boundary)));
     HIP_OK(hipHostMalloc((void **)&h_bnd, (size_t)w * sizeof(Boundary), hipHostMallocDefault));
-    HIP_OK(hipMalloc(&d_x0, 16));
-    HIP_OK(hipMalloc(&d_shard_fn, 16));
-    HIP_OK(hipMalloc(&d_fns_all, (size_t)w * 4 + 16));
+    HIP_OK(dev_alloc(&d_x0, 16));
+    HIP_OK(dev_alloc(&d_shard_fn, 16));
+    HIP_OK(dev_alloc(&d_fns_all, (size_t)w * 4 + 16));
     return ZBPE_OK;
 }
 
@@ -202,7 +219,9 @@ zbpe_status Engine::sync_state() {
         return fail(ZBPE_INTERNAL, "device consistency check failed (flags 0x%x: 1 id overflow, 2 count underflow, 4 missing key, 8 record overflow, 16 home count range, 32 dirty list overflow, 64 occurrences != count, 128 tie collection, 1024 select wait timed out)%s",
                     h_st->error,
                     (h_st->error & 64u) ? (" [first 64: merge " + std::to_string(h_st->err_x) + " found " + std::to_string(h_st->err_occ) +
-                                           " occurrences of a pair counted " + std::to_string(h_st->err_cnt) + ", rank " + std::to_string(rank) + "]").c_str()
+                                           " occurrences of (" + std::to_string(h_st->err_key & 0xFFFF) + "," + std::to_string(h_st->err_key >> 16) +
+                                           ") counted " + std::to_string(h_st->err_cnt) + ", " + (h_st->err_mode ? "list" : "stream") +
+                                           " scan, rank " + std::to_string(rank) + "]").c_str()
                                         : "");
     return ZBPE_OK;
 }
@@ -217,8 +236,8 @@ zbpe_status Engine::alloc_tables(size_t id_cap_new) {
     N.tok_cnt = T.tok_cnt; N.lst_off = T.lst_off; N.lst_len = T.lst_len;
     N.id_cap = (uint32_t)id_cap_new;
     N.ht_mask = (uint32_t)(ht_cap_new - 1);
-    if (hipMalloc(&N.ht, ht_cap_new * 8) != hipSuccess || hipMalloc(&N.id_key, id_cap_new * 4) != hipSuccess ||
-        hipMalloc(&N.id_cnt, id_cap_new * 4) != hipSuccess || hipMalloc(&N.hpos, id_cap_new * 4) != hipSuccess) {
+    if (dev_alloc(&N.ht, ht_cap_new * 8) != hipSuccess || dev_alloc(&N.id_key, id_cap_new * 4) != hipSuccess ||
+        dev_alloc(&N.id_cnt, id_cap_new * 4) != hipSuccess || dev_alloc(&N.hpos, id_cap_new * 4) != hipSuccess) {
         (void)hipGetLastError();
         for (void *p : {(void *)N.ht, (void *)N.id_key, (void *)N.id_cnt, (void *)N.hpos}) if (p) (void)hipFree(p);
         return fail(ZBPE_OUT_OF_MEMORY, "pair table allocation (%zu ids) failed", id_cap_new);
@@ -344,7 +363,7 @@ zbpe_status Engine::replicate() {
     zbpe_fill_u16<<<64, 256, 0, stream>>>(d_tok[cur], n_live, (int64_t)M, HOLE);
     LAUNCH_OK();
     uint16_t *full = nullptr;
-    if (hipMalloc(&full, need * 2) != hipSuccess) { (void)hipGetLastError(); return fail(ZBPE_OUT_OF_MEMORY, "replicated stream (%zu slots)", need); }
+    if (dev_alloc(&full, need * 2) != hipSuccess) { (void)hipGetLastError(); return fail(ZBPE_OUT_OF_MEMORY, "replicated stream (%zu slots)", need); }
     zbpe_fill_u16<<<256, 256, 0, stream>>>(full, 0, (int64_t)need, HOLE);
     LAUNCH_OK();
     if (!comm->allgather(d_tok[cur], full, (size_t)M * 2, stream)) { (void)hipFree(full); return fail(ZBPE_COMM_ERROR, "all-gather of the shards failed"); }
@@ -375,7 +394,7 @@ zbpe_status Engine::grow_arena(uint64_t need) {
     if (need > 0xFFFFFFF0u) return fail(ZBPE_OUT_OF_MEMORY, "occurrence arena of %llu entries exceeds 2^32", (unsigned long long)need);
     if (need > lists_cap) {
         uint32_t *grown = nullptr;
-        if (hipMalloc(&grown, need * 4) != hipSuccess) {
+        if (dev_alloc(&grown, need * 4) != hipSuccess) {
             (void)hipGetLastError();
             return fail(ZBPE_OUT_OF_MEMORY, "occurrence arena (%llu entries)", (unsigned long long)need);
         }
@@ -519,7 +538,7 @@ zbpe_status Engine::rebuild_hot() {
         if (T.hcnt) (void)hipFree(T.hcnt);
         T.hot = nullptr;
         T.hcnt = nullptr;
-        if (hipMalloc(&T.hot, need * 8) != hipSuccess || hipMalloc(&T.hcnt, need * 4) != hipSuccess) {
+        if (dev_alloc(&T.hot, need * 8) != hipSuccess || dev_alloc(&T.hcnt, need * 4) != hipSuccess) {
             (void)hipGetLastError();
             hot_cap_alloc = 0;
             return fail(ZBPE_OUT_OF_MEMORY, "hot list allocation (%zu ids) failed", need);
@@ -561,7 +580,7 @@ zbpe_status Engine::select_ready() {
         if (!overflow && !exhausted) {
             if (debug_checks) {  // cross-check the hot list against a full argmax over every id
                 DevState *dbg = nullptr;
-                HIP_OK(hipMalloc(&dbg, sizeof(DevState)));
+                HIP_OK(dev_alloc(&dbg, sizeof(DevState)));
                 HIP_OK(hipMemcpyAsync(dbg, d_st, sizeof(DevState), hipMemcpyDeviceToDevice, stream));
                 const uint32_t nid = h_st->num_ids;
                 const int blocks = (int)std::min<uint64_t>(ARGMAX_MAX_BLOCKS, nid / (4 * ARGMAX_THREADS) + 1);
@@ -591,7 +610,7 @@ zbpe_status Engine::rebuild_home(uint64_t cap) {
     if (!T.home_cnt || home_words_cap < words) {
         if (T.home_cnt) (void)hipFree(T.home_cnt);
         T.home_cnt = nullptr;
-        if (hipMalloc(&T.home_cnt, words * 4) != hipSuccess) {
+        if (dev_alloc(&T.home_cnt, words * 4) != hipSuccess) {
             (void)hipGetLastError();
             home_words_cap = 0;
             home_slots = 0;
@@ -1149,6 +1168,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         fprintf(stderr, "sel_prof: rounds with named keys ended by: all walked %u, an earlier member's top/adjacent pairs %u, not walked %u, "
                         "touch %u, records %u, vocabulary end %u, arena %u, free slots %u, capacity %u\n",
                 W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8]);
+        fprintf(stderr, "sel_prof: the ending touches: a shared token %u, a neighbour occurrence %u, one past the window %u, "
+                        "unresolved (slow path) %u\n", W[9], W[10], W[11], W[12]);
         const unsigned long long nw = (P[23] & 0xFFFFFFFFull) + (P[23] >> 32);
         fprintf(stderr, "sel_prof: round member walks %llu (%llu with the decision's plan), average %.2f us from the workgroup's state words in (round_scan) to the walk's start\n",
                 nw, P[23] & 0xFFFFFFFFull, P[22] * us / std::max(1.0, (double)nw));
@@ -1711,7 +1732,7 @@ zbpe_status Engine::recount_check(uint64_t *mismatches, uint32_t *first_bad_key)
         return ZBPE_OK;
     }
     uint32_t *d_dump = nullptr;
-    HIP_OK(hipMalloc(&d_dump, (size_t)nid * 12 + 16));
+    HIP_OK(dev_alloc(&d_dump, (size_t)nid * 12 + 16));
     zbpe_recount_dump<<<std::min<uint32_t>(4096, nid / 256 + 1), 256, 0, stream>>>(T, d_recount, d_st, d_dump);
     LAUNCH_OK();
     std::vector<uint32_t> dump((size_t)nid * 3);

@@ -759,20 +759,22 @@ __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64
                 // a token with one (its a is the tb after a ta, its b the ta before a tb). Any of them is also
                 // what a decrement of this pair by that member needs, so an untouched member keeps its count.
                 const uint32_t tl = win(l), tr = win(r), tll = win(ll < 0 ? 0 : ll), trn = win(rn > 13 ? 13 : rn);
-                bool t = false;
+                // (bits: 1 a shared token, 2 a neighbour occurrence, 4 one that reaches past the window)
+                uint32_t t = 0;
 #pragma unroll
                 for (int e = 0; e < ROUND_MAX - 1; e++) {
                     if ((uint32_t)e < A.ntk) {
                         const uint32_t ta = A.tk[e] & 0xFFFFu, tb = A.tk[e] >> 16;
-                        t |= (tl == tb && (ll < 0 || tll == ta)) || (tr == ta && (rn >= 14 || trn == tb)) || (A.a == tb && tl == ta) ||
-                             (A.b == ta && tr == tb);
+                        t |= ((A.a == tb && tl == ta) || (A.b == ta && tr == tb)) ? 1u : 0u;
+                        t |= ((tl == tb && ll >= 0 && tll == ta) || (tr == ta && rn < 14 && trn == tb)) ? 2u : 0u;
+                        t |= ((tl == tb && ll < 0) || (tr == ta && rn >= 14)) ? 4u : 0u;
                     }
                 }
-                if (t) atomicOr(A.rd_touch, 1u);
+                if (t) atomicOr(A.rd_touch, t);
             }
         } else {
             hit = occ_slow(A, H, p, xx);
-            if (RD && hit && A.ntk) atomicOr(A.rd_touch, 1u);  // (not resolved here: counted as touching)
+            if (RD && hit && A.ntk) atomicOr(A.rd_touch, 8u);  // (not resolved here: counted as touching)
         }
         if (hit) hits |= 1u << k;
     }
@@ -2679,10 +2681,12 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
 // (identical on every rank: the deltas were summed), and one thread checks whether this shard's
 // first live token is the b of an occurrence owned by the left rank (then it becomes a hole).
 // error 64 (the occurrences a merge found != its pair's count): the first one's merge and numbers, for the message
-__device__ inline void occ_check_failed(DevState *st, uint32_t X, uint32_t occ, uint32_t cnt) {
+__device__ inline void occ_check_failed(DevState *st, uint32_t X, uint32_t occ, uint32_t cnt, uint32_t key) {
     if (atomicCAS(&st->err_x, 0u, X) == 0u) {
         st->err_occ = occ;
         st->err_cnt = cnt;
+        st->err_key = key;
+        st->err_mode = st->scan_mode;
     }
     atomicOr(&st->error, 64u);
 }
@@ -2858,7 +2862,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
         return;
     }
     const uint32_t ublk = blockIdx.x - apply_blocks;
-    if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) occ_check_failed(st, R.X, R.tail[1], H.top_count);
+    if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) occ_check_failed(st, R.X, R.tail[1], H.top_count, R.top_key);
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof, H.top_count,
                  R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2, pr_key3, pr_key4);
     if (R.prof) {
@@ -2903,6 +2907,11 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->rd_v = k;
         if (RH.n > 1) atomicAdd(&st->rd_why[why], 1u);  // (rounds with named keys: what ended them)
+        if (RH.n > 1 && why == RW_TOUCH) {  // (and the ending touch's kinds: occ_window's bits)
+            const uint32_t tb = RH.touch[k];
+            for (int i = 0; i < 4; i++)
+                if (tb >> i & 1u) atomicAdd(&st->rd_why[RW_N + i], 1u);
+        }
     }
     if (j >= k) return;
     const uint32_t X = H.cur_x + j, key = RH.key[j], a = key & 0xFFFF, b = key >> 16;
@@ -2926,7 +2935,7 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     }
     const uint32_t ublk = lb - apply_blocks;
     const uint32_t *tj = lj + 2 * 65536;
-    if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc) occ_check_failed(st, X, tj[1], Tc);
+    if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc) occ_check_failed(st, X, tj[1], Tc, key);
     const RoundCtx rc{left, j, &st->rd.key[0], &st->rd.dec[0]};
     update_block(T, st, lj, lj + 65536, tj, a, b, X, key, ublk, per, dv, H.theta, 0, Tc, NO_ID, NO_ID, NO_ID, NO_ID, &rc, Xp);
 }
@@ -4354,6 +4363,12 @@ __device__ __attribute__((always_inline)) inline int64_t wave_homes_cover(const 
 // candidate's home (free slots there end its run before the third-smallest home h3) and after the largest
 // tied home's block (a free slot there: no tied key's run wraps past slot C-1). Four waves: the carry into
 // each range (the super-block carry cs composed with the block summaries before it) and its homes.
+// Mixed states: a refresh workgroup of a light launch may refresh some summaries after merge X
+// changed the key set (S -> S - R + B) while cs is the decision's. The bound stays a lower bound for the set
+// merge X+1 sees: carries and occupied slots are monotone in the key set, so cs (from S) >= the carries of
+// S - R, and the mixed homes (S with some of R gone and some of B in) >= the homes of S - R; the bound is then
+// <= the free slots of S - R. Every birth of merge X is compared against it (pr_births counts all of B, also
+// those a refreshed summary already holds), and S - R + B has at least free(S - R) - |B| free slots.
 __device__ __attribute__((always_inline)) inline int32_t wave_carry_block(const HomeView &V, const uint32_t *cs, uint32_t b) {
     const uint32_t lane = threadIdx.x & 63, sb = b / SUPER_BLOCKS, bi = sb * SUPER_BLOCKS + lane;
     const Summ bs = bi < b ? ld_wt(V.summ + bi) : Summ{0, 0};

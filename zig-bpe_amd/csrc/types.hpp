@@ -149,10 +149,11 @@ struct DevState {
     // rounds applied beyond their first members
     alignas(128) RoundHead rd;
     uint32_t rd_merges;
-    uint32_t rd_why[10];     // rounds that walked named keys, by what ended them (RoundWhy, kernels.hpp)
+    uint32_t rd_why[14];     // rounds that walked named keys, by what ended them (RoundWhy, kernels.hpp)
     // the named keys' scan plans (ScanArgs::pl), by a spare wave of the naming decision (zbpe_select_next, round
     // mode), valid for layout generation rp.gen: a member walk then starts without loading its lists' words
     alignas(16) RoundPlans rp;
+    uint32_t err_key, err_mode;  // (error 64: the pair, and its scan's form -- scan_mode)
 };
 struct PairHead {  // what the light test reads (the kernel entry's round trip)
     uint32_t x, key, slack, ties, births, dt, hits, plan_gen;
