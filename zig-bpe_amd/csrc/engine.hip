@@ -1168,8 +1168,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         fprintf(stderr, "sel_prof: rounds with named keys ended by: all walked %u, an earlier member's top/adjacent pairs %u, not walked %u, "
                         "touch %u, records %u, vocabulary end %u, arena %u, free slots %u, capacity %u\n",
                 W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8]);
-        fprintf(stderr, "sel_prof: the ending touches: a shared token %u, a neighbour occurrence %u, one past the window %u, "
-                        "unresolved (slow path) %u\n", W[9], W[10], W[11], W[12]);
+        fprintf(stderr, "sel_prof: the ending touches: a neighbour occurrence %u, one past the window %u, unresolved (slow path) %u; "
+                        "members skipped (decremented by a merged member) %u\n", W[9], W[10], W[11], W[12]);
         const unsigned long long nw = (P[23] & 0xFFFFFFFFull) + (P[23] >> 32);
         fprintf(stderr, "sel_prof: round member walks %llu (%llu with the decision's plan), average %.2f us from the workgroup's state words in (round_scan) to the walk's start\n",
                 nw, P[23] & 0xFFFFFFFFull, P[22] * us / std::max(1.0, (double)nw));

@@ -682,6 +682,10 @@ __device__ inline void wave_flush_records(const ScanArgs &A, const uint32_t *rec
 // next vector's first two dwords nx, ny (holes outside the stream); returns the hit mask.
 // RD: a multi-merge round's member walk -- every occurrence is also tested against the earlier members' pairs
 // (A.tk): does it touch one of their occurrences (share a token with one, or sit next to one)? Then A.rd_touch.
+// RoundHead::touch of member j: bit e (RT_SHARED << e) an occurrence shares a token with one of earlier member e's
+// (merging e decrements member j's pair: it leaves the tied set), bit 8 + e (RT_NEIGHBOUR << e) one sits next to
+// one of e's (its neighbour pairs would differ), RT_WINDOW / RT_SLOW such a test could not be made
+enum RoundTouch : uint32_t { RT_SHARED = 1u, RT_NEIGHBOUR = 1u << 8, RT_WINDOW = 1u << 16, RT_SLOW = 1u << 17 };
 template <bool RD = false>
 __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64_t vi, uint32_t m, uint32_t &xx,
                                       uint32_t pw, uint4 cv, uint32_t nx, uint32_t ny);
@@ -759,22 +763,23 @@ __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64
                 // a token with one (its a is the tb after a ta, its b the ta before a tb). Any of them is also
                 // what a decrement of this pair by that member needs, so an untouched member keeps its count.
                 const uint32_t tl = win(l), tr = win(r), tll = win(ll < 0 ? 0 : ll), trn = win(rn > 13 ? 13 : rn);
-                // (bits: 1 a shared token, 2 a neighbour occurrence, 4 one that reaches past the window)
+                // (RoundTouch bits, per earlier member e: a shared token -- merging e decrements this pair --, a
+                // neighbour occurrence, or one that may reach past the window)
                 uint32_t t = 0;
 #pragma unroll
                 for (int e = 0; e < ROUND_MAX - 1; e++) {
                     if ((uint32_t)e < A.ntk) {
                         const uint32_t ta = A.tk[e] & 0xFFFFu, tb = A.tk[e] >> 16;
-                        t |= ((A.a == tb && tl == ta) || (A.b == ta && tr == tb)) ? 1u : 0u;
-                        t |= ((tl == tb && ll >= 0 && tll == ta) || (tr == ta && rn < 14 && trn == tb)) ? 2u : 0u;
-                        t |= ((tl == tb && ll < 0) || (tr == ta && rn >= 14)) ? 4u : 0u;
+                        t |= ((A.a == tb && tl == ta) || (A.b == ta && tr == tb)) ? RT_SHARED << e : 0u;
+                        t |= ((tl == tb && ll >= 0 && tll == ta) || (tr == ta && rn < 14 && trn == tb)) ? RT_NEIGHBOUR << e : 0u;
+                        t |= ((tl == tb && ll < 0) || (tr == ta && rn >= 14)) ? RT_WINDOW : 0u;
                     }
                 }
                 if (t) atomicOr(A.rd_touch, t);
             }
         } else {
             hit = occ_slow(A, H, p, xx);
-            if (RD && hit && A.ntk) atomicOr(A.rd_touch, 8u);  // (not resolved here: counted as touching)
+            if (RD && hit && A.ntk) atomicOr(A.rd_touch, RT_SLOW);  // (not resolved here: counted as touching every one)
         }
         if (hit) hits |= 1u << k;
     }
@@ -1145,7 +1150,8 @@ __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs 
     uint32_t K = 1;
     if (A0.round >= 2 && P.x == X0 + 1 && pr_full == X0 + 1 && plan_is_list(A, H) && T) {
         const uint32_t kmax = min(min((uint32_t)A0.round, (uint32_t)ROUND_MAX), A0.x_end > X0 ? A0.x_end - X0 : 1u);
-        while (K < kmax && keys[K] != NO_ID && (uint64_t)(K + 1) * T <= (uint64_t)A.rec_cap) K++;
+        // (a self pair's occurrences overlap in runs: the touch tests assume none do, so one ends the members)
+        while (K < kmax && keys[K] != NO_ID && (keys[K] & 0xFFFF) != (keys[K] >> 16) && (uint64_t)(K + 1) * T <= (uint64_t)A.rec_cap) K++;
     }
     // Workgroups [0, RD_FREE_WGS) bound the free slots (one wave per range) and store the round's words; the
     // members' walks take the others in turn (member j: every K-th from RD_FREE_WGS + j), so that every member's
@@ -2503,11 +2509,13 @@ struct RoundCtx {
     uint32_t j;
     const uint32_t *keys;  // RoundHead::key
     uint32_t *dec;         // RoundHead::dec
+    uint32_t mask;         // the members merged (round_valid)
 };
 __device__ inline void round_credit(const RoundCtx &rc, uint32_t key) {
     const uint32_t x = key & 0xFFFF, y = key >> 16;
     uint32_t m = rc.j;
     for (uint32_t i = 0; i < rc.j; i++) {
+        if (!(rc.mask >> i & 1u)) continue;  // (a skipped member's deltas are not applied)
         const uint32_t *l = rc.base + (size_t)i * (2 * 65536 + 64);
         const uint32_t ki = rc.keys[i], ai = ki & 0xFFFF, bi = ki >> 16;
         if ((y == ai && l[x]) || (x == bi && l[65536 + y]) || (x == bi && y == ai && l[2 * 65536])) { m = i; break; }
@@ -2721,47 +2729,65 @@ struct ReplaceArgs {
 __device__ inline uint64_t dev_zig_cap_for(uint64_t D);
 __device__ inline bool dev_zig_at_max_load(uint64_t cap, uint64_t D);
 // Which members of a multi-merge round the reference's loop merges next, one after the other (every workgroup
-// of the round's replace evaluates it on the same words: the scan's RoundHead, final at this launch): the
-// longest prefix whose member j >= 1 was walked (a list form) with exactly T occurrences, none touching an
-// earlier member's (so its occurrences, its neighbours and its count are what they would be when its turn
-// comes: every touch -- a shared position or a neighbour -- is what a change of them needs), no earlier member
-// made a pair with the top count or adjacent occurrences (the tied set is the decision's less the merged and
-// the decremented: member j is its smallest home), the earlier members' new pairs are fewer than the free
-// Zig-map slots after member j's home block before the next tied home and after the largest tied home's
-// block (each new key fills at most one: member j's run still ends before the next tied home and no tied run
-// wraps, so it is first in slot order -- the pair-select argument of zbpe_select_next, per member), and the
-// Zig capacity is C and not at a max load for every live-pair count the earlier members can leave (each member
-// kills its own pair and at most one pair per new pair: D in [D0 - j, D0 + births - j]).
-// (*why: what ended the round -- RoundWhy)
+// of the round's replace evaluates it on the same words: the scan's RoundHead, final at this launch). The named
+// keys are the decision's tied pairs in home order; member j >= 1 is
+//   - skipped when an occurrence of it shares a token with one of a merged member's (RT_SHARED): merging that
+//     member decrements its pair, which leaves the tied set, so the loop never takes it (tied pairs only fall);
+//   - else merged next (merge X0 + the members merged before it) when it was walked (a list form) with exactly
+//     T occurrences, none next to a merged member's (RT_NEIGHBOUR; so its occurrences, its neighbours and its
+//     count are what they would be when its turn comes), no merged member made a pair with the top count or
+//     adjacent occurrences (the tied set is the decision's less the merged and the decremented: member j is its
+//     smallest home), the merged members' new pairs are fewer than the free Zig-map slots after member j's home
+//     block before the next tied home and after the largest tied home's block (each new key fills at most one:
+//     member j's run still ends before the next tied home and no tied run wraps, so it is first in slot order
+//     -- the pair-select argument of zbpe_select_next, per member), and the Zig capacity is C and not at a max
+//     load for every live-pair count the merged members can leave (each kills its own pair and at most one pair
+//     per new pair: D in [D0 - k, D0 + births - k] after k merges);
+//   - else the round ends.
 enum RoundWhy : uint32_t { RW_ALL, RW_FLAGS, RW_WALK, RW_TOUCH, RW_REC, RW_END, RW_ARENA, RW_SLACK, RW_CAP, RW_N };
-__device__ inline uint32_t round_valid(const RoundHead &R, uint32_t T, uint32_t X0, uint32_t x_end, uint32_t C,
-                                       uint32_t arena_top, uint32_t rec_cap, uint32_t *why = nullptr) {
-    uint32_t k = 1, w = RW_ALL;
+struct RoundVerdict {
+    uint32_t mask;   // members merged (bit j: member j; bit 0 always)
+    uint32_t k;      // how many
+    uint32_t why;    // what ended the round (RoundWhy), at member jend
+    uint32_t jend;
+};
+__device__ inline RoundVerdict round_valid(const RoundHead &R, uint32_t T, uint32_t X0, uint32_t x_end, uint32_t C,
+                                           uint32_t arena_top, uint32_t rec_cap) {
+    RoundVerdict v{1u, 1u, RW_ALL, 0u};
     uint64_t births = R.birth[0];
     uint32_t flags = R.top[0];
     const uint32_t n = min(R.n, (uint32_t)ROUND_MAX);
 #pragma unroll
     for (uint32_t j = 1; j < (uint32_t)ROUND_MAX; j++) {
         if (j >= n) break;
-        w = flags ? RW_FLAGS : !R.walk[j] ? RW_WALK : R.touch[j] ? RW_TOUCH : R.rec[j] != T ? RW_REC : X0 + j >= x_end ? RW_END : RW_ALL;
-        if (w != RW_ALL) break;
-        if ((uint64_t)arena_top + (uint64_t)(j + 1) * T > rec_cap) { w = RW_ARENA; break; }
+        v.jend = j;
+        if (flags) { v.why = RW_FLAGS; break; }
+        const uint32_t tch = R.touch[j];
+        if (tch & v.mask * RT_SHARED) continue;  // decremented: no longer tied
+        v.why = !R.walk[j]                                                ? RW_WALK
+                : (tch & (v.mask * RT_NEIGHBOUR | RT_WINDOW | RT_SLOW))   ? RW_TOUCH
+                : R.rec[j] != T                                           ? RW_REC
+                : X0 + v.k >= x_end                                       ? RW_END
+                : (uint64_t)arena_top + (uint64_t)(j + 1) * T > rec_cap   ? RW_ARENA
+                                                                          : RW_ALL;
+        if (v.why != RW_ALL) break;
         const uint64_t slack = R.ties == j + 1 ? ~0ull
                                : (R.freeb[j] < 0 || R.freeb[0] < 0) ? 0ull
                                                                     : (uint64_t)min(R.freeb[j], R.freeb[0]);
-        if (births >= slack) { w = RW_SLACK; break; }
-        const int64_t lo = (int64_t)R.live0 - (int64_t)j, hi = (int64_t)R.live0 + (int64_t)births - (int64_t)j;
+        if (births >= slack) { v.why = RW_SLACK; break; }
+        const int64_t lo = (int64_t)R.live0 - (int64_t)v.k, hi = (int64_t)R.live0 + (int64_t)births - (int64_t)v.k;
         if (lo < 1 || dev_zig_cap_for((uint64_t)lo) != C || dev_zig_cap_for((uint64_t)hi) != C ||
             dev_zig_at_max_load(C, (uint64_t)hi)) {
-            w = RW_CAP;
+            v.why = RW_CAP;
             break;
         }
-        k = j + 1;
+        v.mask |= 1u << j;
+        v.k++;
         births += R.birth[j];
         flags |= R.top[j];
     }
-    if (why) *why = w;
-    return k;
+    if (v.why == RW_ALL) v.jend = n;
+    return v;
 }
 // pair selects: merge X+1's candidate bound, by the replace's extra workgroup (defined with the home views below)
 __device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Summ *sup, uint32_t C, uint32_t nb,
@@ -2902,19 +2928,25 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     }
     if (H.halt) return;
     const uint32_t Tc = H.top_count;
-    uint32_t why;
-    const uint32_t k = round_valid(RH, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap, &why);
+    const RoundVerdict v = round_valid(RH, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->rd_v = k;
-        if (RH.n > 1) atomicAdd(&st->rd_why[why], 1u);  // (rounds with named keys: what ended them)
-        if (RH.n > 1 && why == RW_TOUCH) {  // (and the ending touch's kinds: occ_window's bits)
-            const uint32_t tb = RH.touch[k];
-            for (int i = 0; i < 4; i++)
-                if (tb >> i & 1u) atomicAdd(&st->rd_why[RW_N + i], 1u);
+        st->rd_v = v.k;
+        st->rd_mask = v.mask;
+        if (RH.n > 1) {  // (rounds with named keys: what ended them, the ending touch's kinds, the members skipped)
+            atomicAdd(&st->rd_why[v.why], 1u);
+            if (v.why == RW_TOUCH) {
+                const uint32_t tb = RH.touch[v.jend];
+                if (tb & RT_NEIGHBOUR * 0x1Fu) atomicAdd(&st->rd_why[RW_N], 1u);
+                if (tb & RT_WINDOW) atomicAdd(&st->rd_why[RW_N + 1], 1u);
+                if (tb & RT_SLOW) atomicAdd(&st->rd_why[RW_N + 2], 1u);
+            }
+            const uint32_t skipped = ((1u << v.jend) - 1u) & ~v.mask;
+            if (skipped) atomicAdd(&st->rd_why[RW_N + 3], (uint32_t)__popc(skipped));
         }
     }
-    if (j >= k) return;
-    const uint32_t X = H.cur_x + j, key = RH.key[j], a = key & 0xFFFF, b = key >> 16;
+    if (!(v.mask >> j & 1u)) return;
+    // member j is merge X0 + (the members merged before it)
+    const uint32_t X = H.cur_x + (uint32_t)__popc(v.mask & ((1u << j) - 1u)), key = RH.key[j], a = key & 0xFFFF, b = key >> 16;
     if (lb < apply_blocks) {
         // X at each occurrence start, a hole at its b (one GPU: the b is always in the stream)
         const uint32_t *rec = R.rec + H.arena_top + (size_t)j * Tc;
@@ -2936,7 +2968,7 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     const uint32_t ublk = lb - apply_blocks;
     const uint32_t *tj = lj + 2 * 65536;
     if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc) occ_check_failed(st, X, tj[1], Tc, key);
-    const RoundCtx rc{left, j, &st->rd.key[0], &st->rd.dec[0]};
+    const RoundCtx rc{left, j, &st->rd.key[0], &st->rd.dec[0], v.mask};
     update_block(T, st, lj, lj + 65536, tj, a, b, X, key, ublk, per, dv, H.theta, 0, Tc, NO_ID, NO_ID, NO_ID, NO_ID, &rc, Xp);
 }
 
@@ -4241,7 +4273,21 @@ constexpr int DECIDE_THREADS = 256;
 struct PlanCtx {
     const uint32_t *lst_off, *lst_len, *dir_row, *dir;
     uint32_t dir_w, lists_x, xn, xoff, xlen, xnum = 1;
+    uint32_t xmask = 0;  // (a round that skipped members: token xn + i is member m_i, the i-th set bit; list at xoff + m_i * xlen)
 };
+// the member of a round's i-th merge (the i-th set bit of the mask; the identity without one)
+__device__ inline uint32_t round_member(uint32_t mask, uint32_t i) {
+    if (!mask) return i;
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < (uint32_t)ROUND_MAX; e++) {
+        if (mask >> e & 1u) {
+            if (i == 0) m = e;
+            i--;
+        }
+    }
+    return m;
+}
 __device__ inline void plan_compute(const PlanCtx &P, uint32_t key, uint32_t *out) {
     const uint32_t a = key & 0xFFFF, b = key >> 16;
     uint32_t la = P.lst_len[a], lb = P.lst_len[b], oa = P.lst_off[a], ob = P.lst_off[b];
@@ -4252,8 +4298,8 @@ __device__ inline void plan_compute(const PlanCtx &P, uint32_t key, uint32_t *ou
         r0 = P.dir[rb];
         r1 = P.dir[rb + 1];
     }
-    if (a - P.xn < P.xnum) { la = P.xlen; oa = P.xoff + (a - P.xn) * P.xlen; }
-    if (b - P.xn < P.xnum) { lb = P.xlen; ob = P.xoff + (b - P.xn) * P.xlen; }
+    if (a - P.xn < P.xnum) { la = P.xlen; oa = P.xoff + round_member(P.xmask, a - P.xn) * P.xlen; }
+    if (b - P.xn < P.xnum) { lb = P.xlen; ob = P.xoff + round_member(P.xmask, b - P.xn) * P.xlen; }
     out[0] = la; out[1] = lb; out[2] = oa; out[3] = ob; out[4] = r0; out[5] = r1;
 }
 // the plan of merge x1 = key (after the state's cur_key for it is stored; the next kernel boundary orders both)
@@ -4610,7 +4656,7 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
 // first, RoundHead::dec), and the round's words are cleared for the next round's scan.
 __device__ inline void round_roll(const Tables &T, DevState *st, const StateHead &H0, MergeLog *log, const uint32_t *pre,
                                   FinishOut *fo, uint32_t *rlog) {
-    const uint32_t k = H0.rd_v, X0 = H0.cur_x, Tc = H0.top_count;
+    const uint32_t k = H0.rd_v, X0 = H0.cur_x, Tc = H0.top_count, mask = H0.rd_mask;
     RoundHead &R = st->rd;
     // the RoundHead words, preloaded into LDS at the kernel's entry (roll_preload rd)
     const RoundHead &RP = *reinterpret_cast<const RoundHead *>(pre + RI_WORDS);
@@ -4624,25 +4670,30 @@ __device__ inline void round_roll(const Tables &T, DevState *st, const StateHead
     rec[0] = pre[RI_REC];
     const uint32_t holes = pre[RI_HOLES], arena_top = pre[RI_ARENA_TOP], arena_rep = pre[RI_ARENA_REP], total_occ = pre[RI_TOTAL_OCC];
     const long long live_tokens = (long long)(((uint64_t)pre[RI_LIVE_TOK_HI] << 32) | pre[RI_LIVE_TOK_LO]);
-    uint32_t ties = RP.ties0, sum = 0;
+    // merge X0 + x is member m (the x-th set bit of mask); member m's records are at arena_top + m Tc
+    uint32_t ties = RP.ties0, sum = 0, x = 0, prev = 0, last = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < (uint32_t)ROUND_MAX; j++) {
-        if (j >= k) break;
+    for (uint32_t m = 0; m < (uint32_t)ROUND_MAX; m++) {
+        if (!(mask >> m & 1u)) continue;
         if (T.lst_off) {
-            T.lst_off[X0 + j] = arena_top + j * Tc;
-            T.lst_len[X0 + j] = rec[j];
+            T.lst_off[X0 + x] = arena_top + m * Tc;
+            T.lst_len[X0 + x] = rec[m];
         }
-        if (j) {
-            ties = ties - 1u - dec[j - 1];
-            MergeLog &L = log[X0 + j - 256];
-            L.key = key[j];
+        if (x) {
+            ties = ties - 1u - dec[prev];
+            MergeLog &L = log[X0 + x - 256];
+            L.key = key[m];
             L.count = Tc;
-            L.live = (uint32_t)(live_tokens - (long long)j * Tc);
+            L.live = (uint32_t)(live_tokens - (long long)x * Tc);
             L.ties = ties;
+            L.mode = 1;
         }
-        sum += rec[j];
+        sum += rec[m];
+        prev = last = m;
+        x++;
     }
-    const uint32_t top = arena_top + (k - 1) * Tc + rec[k - 1];
+    (void)k;
+    const uint32_t top = arena_top + last * Tc + rec[last];
     if (T.lst_off) st->arena_top = top;
     st->last_occ = sum;
     st->total_occ = total_occ + sum;
@@ -5083,7 +5134,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     __shared__ uint32_t s_plan[6];
     // (X's list: the roll's lst_off / lst_len, from the same words; a round's members: T records each)
     const PlanCtx plan = N.round && H0.rd_v ? PlanCtx{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, H0.cur_x, H0.arena_top,
-                                                      H0.top_count, H0.rd_v}
+                                                      H0.top_count, H0.rd_v, H0.rd_mask}
                                             : PlanCtx{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, X, H0.arena_top,
                                                       H0.rec_count, 1u};
     const bool plan_on = N.plan && T.lst_off && H0.lists_valid;

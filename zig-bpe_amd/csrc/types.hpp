@@ -77,7 +77,8 @@ struct DevState {
     uint32_t lp_key, lp_id;
     uint32_t cur_x;          // merge token X being processed (the first member of a multi-merge round)
     uint32_t rd_v;           // multi-merge rounds: members the round's replace applied (0: not a round; RoundHead)
-    uint32_t head_pad[2];
+    uint32_t rd_mask;        // multi-merge rounds: which members the replace applied (RoundVerdict)
+    uint32_t head_pad;
     // ---- the rest
     uint32_t num_ids;        // pair ids allocated
     int32_t live;            // D_t: pairs with count > 0
@@ -169,8 +170,8 @@ struct StateHead {
     uint32_t halt, cur_key, arena_top, lists_valid, lists_x, top_count, theta, hot_len, rec_count;
     uint32_t plan_x, plan_key, plan_gen, plan_la, plan_lb, plan_oa, plan_ob, plan_r0, plan_r1;
     uint32_t lp_key, lp_id;
-    uint32_t cur_x, rd_v;
-    uint32_t pad[2];
+    uint32_t cur_x, rd_v, rd_mask;
+    uint32_t pad;
 };
 static_assert(sizeof(StateHead) == 96, "state head: 24 words");
 static_assert(offsetof(DevState, rec_count) == 32 && offsetof(DevState, plan_r1) == 68 && offsetof(DevState, hot_len) == 28 &&
