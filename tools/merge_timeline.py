@@ -116,7 +116,33 @@ def analyse(d, logp):
         h = halts[b].setdefault(names.get(reason, str(reason)), [0, 0.0])
         h[0] += 1
         h[1] += us
+    # what a halt's host path runs: the kernels between the previous merge's select and the next merge's first
+    # scan (the halted merge on the synchronous path, compactions, rebuilds), by reason: window wall and kernel time
+    scan_at = {}
+    for j, x in enumerate(slog):
+        if x >= 0:
+            scan_at.setdefault(x >> 1, scans[j])
+    hwin = {}
+    for x, reason, us in L.get("halts", []):
+        m = x - 256
+        if m - 1 not in scan_at or m + 1 not in first:
+            continue
+        i0 = scan_at[m - 1]
+        t_lo = ks[min(i0 + 2, len(ks) - 1)][1]
+        t_hi = first[m + 1]
+        h = hwin.setdefault(names.get(reason, str(reason)), {"n": 0, "window_us": 0.0, "kernels": {}})
+        h["n"] += 1
+        h["window_us"] += (t_hi - t_lo) / 1e3
+        for a0, a1, name in ks[i0 + 3:]:
+            if a0 >= t_hi:
+                break
+            if a0 >= t_lo:
+                short = name.split("(")[0].replace("void ", "").replace("zbpe::", "")[:40]
+                h["kernels"][short] = h["kernels"].get(short, 0.0) + (a1 - a0) / 1e3
     out = {}
+    out["halt_windows"] = {k: {"n": v["n"], "window_us_avg": round(v["window_us"] / v["n"], 1),
+                               "kernel_us_avg": {kk: round(vv / v["n"], 1) for kk, vv in sorted(v["kernels"].items(), key=lambda kv: -kv[1])[:8]}}
+                           for k, v in hwin.items()}
     for b in buckets:
         key = f"merges [{b[0]}, {b[1] if b[1] < 1 << 30 else 'end'})"
         if b in wall:

@@ -606,22 +606,26 @@ zbpe_status Engine::select_ready() {
 
 zbpe_status Engine::rebuild_home(uint64_t cap) {
     // whole 4096-slot blocks (the tie kernels read a block's slots as 16-B vectors)
-    const size_t words = (std::max<uint64_t>(cap, SUMM_SLOTS) + SUMM_SLOTS - 1) / SUMM_SLOTS * (SUMM_SLOTS / 4);
+    const auto words_for = [](uint64_t c) { return (std::max<uint64_t>(c, SUMM_SLOTS) + SUMM_SLOTS - 1) / SUMM_SLOTS * (SUMM_SLOTS / 4); };
+    const size_t words = words_for(cap);
     if (!T.home_cnt || home_words_cap < words) {
         if (T.home_cnt) (void)hipFree(T.home_cnt);
         T.home_cnt = nullptr;
-        if (dev_alloc(&T.home_cnt, words * 4) != hipSuccess) {
+        // room for two more doublings: a capacity step halts the batch, and a free + allocation took most of
+        // its host path (~4 ms each at C4 merges 500-2000, profiles/r05_c4_merge_timeline.json)
+        const size_t alloc = words_for(std::min<uint64_t>(cap * 4, 1ull << 31));
+        if (dev_alloc(&T.home_cnt, alloc * 4) != hipSuccess) {
             (void)hipGetLastError();
             home_words_cap = 0;
             home_slots = 0;
             return fail(ZBPE_OUT_OF_MEMORY, "home histogram allocation (%llu slots) failed", (unsigned long long)cap);
         }
-        home_words_cap = words;
+        home_words_cap = alloc;
     }
     const size_t nb = (cap + SUMM_SLOTS - 1) / SUMM_SLOTS, nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
-    CHECK(ensure(&d_summ, summ_cap, nb, "home summaries"));
-    CHECK(ensure(&d_sup, sup_cap, nsb, "home super-block summaries"));
-    CHECK(ensure(&T.home_dirty, dirty_bits_cap, 2 * nsb, "home dirty bits"));
+    if (summ_cap < nb) CHECK(ensure(&d_summ, summ_cap, 4 * nb, "home summaries"));  // (headroom as above)
+    if (sup_cap < nsb) CHECK(ensure(&d_sup, sup_cap, 4 * nsb, "home super-block summaries"));
+    if (dirty_bits_cap < 2 * nsb) CHECK(ensure(&T.home_dirty, dirty_bits_cap, 8 * nsb, "home dirty bits"));
     HIP_OK(hipMemsetAsync(T.home_cnt, 0, words * 4, stream));
     HIP_OK(hipMemsetAsync(T.home_dirty, 0, 2 * nsb * 4, stream));
     T.home_mask = (uint32_t)(cap - 1);
@@ -1169,7 +1173,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                         "touch %u, records %u, vocabulary end %u, arena %u, free slots %u, capacity %u\n",
                 W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8]);
         fprintf(stderr, "sel_prof: the ending touches: a neighbour occurrence %u, one past the window %u, unresolved (slow path) %u; "
-                        "members skipped (decremented by a merged member) %u\n", W[9], W[10], W[11], W[12]);
+                        "members skipped (decremented by a merged member) %u; ending flags: a new pair at the top count %u, "
+                        "only adjacent occurrences %u\n", W[9], W[10], W[11], W[12], W[13], W[14]);
         const unsigned long long nw = (P[23] & 0xFFFFFFFFull) + (P[23] >> 32);
         fprintf(stderr, "sel_prof: round member walks %llu (%llu with the decision's plan), average %.2f us from the workgroup's state words in (round_scan) to the walk's start\n",
                 nw, P[23] & 0xFFFFFFFFull, P[22] * us / std::max(1.0, (double)nw));

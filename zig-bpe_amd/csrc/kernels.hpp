@@ -2750,10 +2750,11 @@ struct RoundVerdict {
     uint32_t k;      // how many
     uint32_t why;    // what ended the round (RoundWhy), at member jend
     uint32_t jend;
+    uint32_t flags;  // (RW_FLAGS: the merged members' RoundHead::top bits)
 };
 __device__ inline RoundVerdict round_valid(const RoundHead &R, uint32_t T, uint32_t X0, uint32_t x_end, uint32_t C,
                                            uint32_t arena_top, uint32_t rec_cap) {
-    RoundVerdict v{1u, 1u, RW_ALL, 0u};
+    RoundVerdict v{1u, 1u, RW_ALL, 0u, 0u};
     uint64_t births = R.birth[0];
     uint32_t flags = R.top[0];
     const uint32_t n = min(R.n, (uint32_t)ROUND_MAX);
@@ -2761,7 +2762,7 @@ __device__ inline RoundVerdict round_valid(const RoundHead &R, uint32_t T, uint3
     for (uint32_t j = 1; j < (uint32_t)ROUND_MAX; j++) {
         if (j >= n) break;
         v.jend = j;
-        if (flags) { v.why = RW_FLAGS; break; }
+        if (flags) { v.why = RW_FLAGS; v.flags = flags; break; }
         const uint32_t tch = R.touch[j];
         if (tch & v.mask * RT_SHARED) continue;  // decremented: no longer tied
         v.why = !R.walk[j]                                                ? RW_WALK
@@ -2940,6 +2941,7 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
                 if (tb & RT_WINDOW) atomicAdd(&st->rd_why[RW_N + 1], 1u);
                 if (tb & RT_SLOW) atomicAdd(&st->rd_why[RW_N + 2], 1u);
             }
+            if (v.why == RW_FLAGS) atomicAdd(&st->rd_why[RW_N + 4 + (v.flags & 1u ? 0 : 1)], 1u);
             const uint32_t skipped = ((1u << v.jend) - 1u) & ~v.mask;
             if (skipped) atomicAdd(&st->rd_why[RW_N + 3], (uint32_t)__popc(skipped));
         }

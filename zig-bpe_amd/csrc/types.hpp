@@ -150,7 +150,7 @@ struct DevState {
     // rounds applied beyond their first members
     alignas(128) RoundHead rd;
     uint32_t rd_merges;
-    uint32_t rd_why[14];     // rounds that walked named keys, by what ended them (RoundWhy, kernels.hpp)
+    uint32_t rd_why[16];     // rounds that walked named keys, by what ended them (RoundWhy, kernels.hpp)
     // the named keys' scan plans (ScanArgs::pl), by a spare wave of the naming decision (zbpe_select_next, round
     // mode), valid for layout generation rp.gen: a member walk then starts without loading its lists' words
     alignas(16) RoundPlans rp;
