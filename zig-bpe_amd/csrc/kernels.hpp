@@ -2752,11 +2752,16 @@ struct RoundVerdict {
     uint32_t jend;
     uint32_t flags;  // (RW_FLAGS: the merged members' RoundHead::top bits)
 };
-__device__ inline RoundVerdict round_valid(const RoundHead &R, uint32_t T, uint32_t X0, uint32_t x_end, uint32_t C,
-                                           uint32_t arena_top, uint32_t rec_cap) {
+// (dbase: the members' delta buffers, DELTA_WORDS apart. A member's adjacent occurrences (xx, its tail word) make
+// (X, X), one more new pair, with count xx: a flag only at the top count; the (b, a) they decrement is a tied
+// pair leaving the set, or a later member that shares their tokens and is skipped.)
+__device__ inline RoundVerdict round_valid(const RoundHead &R, const uint32_t *dbase, uint32_t T, uint32_t X0, uint32_t x_end,
+                                           uint32_t C, uint32_t arena_top, uint32_t rec_cap) {
+    constexpr uint32_t DW = 2 * 65536 + 64;
     RoundVerdict v{1u, 1u, RW_ALL, 0u, 0u};
-    uint64_t births = R.birth[0];
-    uint32_t flags = R.top[0];
+    const uint32_t xx0 = dbase[2 * 65536];
+    uint64_t births = R.birth[0] + (xx0 ? 1u : 0u);
+    uint32_t flags = (R.top[0] & 1u) | (xx0 >= T ? 2u : 0u);
     const uint32_t n = min(R.n, (uint32_t)ROUND_MAX);
 #pragma unroll
     for (uint32_t j = 1; j < (uint32_t)ROUND_MAX; j++) {
@@ -2784,8 +2789,9 @@ __device__ inline RoundVerdict round_valid(const RoundHead &R, uint32_t T, uint3
         }
         v.mask |= 1u << j;
         v.k++;
-        births += R.birth[j];
-        flags |= R.top[j];
+        const uint32_t xxj = dbase[(size_t)j * DW + 2 * 65536];
+        births += R.birth[j] + (xxj ? 1u : 0u);
+        flags |= (R.top[j] & 1u) | (xxj >= T ? 2u : 0u);
     }
     if (v.why == RW_ALL) v.jend = n;
     return v;
@@ -2929,7 +2935,7 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     }
     if (H.halt) return;
     const uint32_t Tc = H.top_count;
-    const RoundVerdict v = round_valid(RH, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap);
+    const RoundVerdict v = round_valid(RH, left, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->rd_v = v.k;
         st->rd_mask = v.mask;
