@@ -173,7 +173,7 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * merge's winner, whose select then skips the argmax and the decision), "pair_chain"
  * (0-3, default 2: a pair select passes that on to up to this many further merges), "pair_refresh"
  * (0/1, default 0: a pair select's home refresh is left to the next full select; 1 disables chains),
- * "pair_m3w" (0/1: the decision's further tied homes by a wave of their own), "round_k" (1-5, default 4:
+ * "pair_m3w" (0/1: the decision's further tied homes by a wave of their own), "round_k" (1-5, default 5:
  * members of a multi-merge round -- a tied merge and the tied keys its decision named, applied in one scan,
  * replace and select launch when the reference's loop would merge them next; 1: no rounds), "round_ties" (0-100,
  * default 50: rounds in batches after one with at least this many percent tied merges), "lp_lazy" (0/1,

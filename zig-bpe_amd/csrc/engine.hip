@@ -1169,12 +1169,12 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         fprintf(stderr, "sel_prof: pair selects %llu, average %.2f us from the first argmax block's start to their commit\n", P[20],
                 P[21] * us / std::max(1.0, (double)P[20]));
         const uint32_t *W = h_st->rd_why;
-        fprintf(stderr, "sel_prof: rounds with named keys ended by: all walked %u, an earlier member's top/adjacent pairs %u, not walked %u, "
-                        "touch %u, records %u, vocabulary end %u, arena %u, free slots %u, capacity %u\n",
-                W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8]);
-        fprintf(stderr, "sel_prof: the ending touches: a neighbour occurrence %u, one past the window %u, unresolved (slow path) %u; "
-                        "members skipped (decremented by a merged member) %u; ending flags: a new pair at the top count %u, "
-                        "only adjacent occurrences %u\n", W[9], W[10], W[11], W[12], W[13], W[14]);
+        fprintf(stderr, "sel_prof: rounds with named keys ended by: all walked %u, a merged member's pair at the top count %u, not walked %u, "
+                        "touch %u, records %u, vocabulary end %u, arena %u, free slots %u, capacity %u, junction counts differ %u\n",
+                W[0], W[1], W[2], W[3], W[4], W[5], W[6], W[7], W[8], W[9]);
+        fprintf(stderr, "sel_prof: merged members with a junction to an earlier one %u; members skipped (decremented by a merged member) %u; "
+                        "ending flags: a new pair (or junction pair) at the top count %u, only adjacent occurrences %u\n",
+                W[10], W[13], W[14], W[15]);
         const unsigned long long nw = (P[23] & 0xFFFFFFFFull) + (P[23] >> 32);
         fprintf(stderr, "sel_prof: round member walks %llu (%llu with the decision's plan), average %.2f us from the workgroup's state words in (round_scan) to the walk's start\n",
                 nw, P[23] & 0xFFFFFFFFull, P[22] * us / std::max(1.0, (double)nw));

@@ -54,7 +54,7 @@ struct Engine {
     std::vector<uint32_t> h_rlog;
     uint32_t rpar = 0, launch_seq = 1u << 20;
     bool last_rounds = false;
-    int round_k = 4;            // option "round_k": members of a multi-merge round (1: no rounds; at most ROUND_MAX)
+    int round_k = 5;            // option "round_k": members of a multi-merge round (1: no rounds; at most ROUND_MAX)
     uint32_t round_ties = 50;   // option "round_ties": rounds once this many percent of the last batch's merges were tied
     uint32_t last_tied_pct = 0; // (the last batch's)
 

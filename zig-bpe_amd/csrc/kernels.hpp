@@ -493,11 +493,11 @@ struct ScanArgs {
     uint32_t x_end;
     HomeView hv;  // (hc unused)
     const uint32_t *cs;
-    // a member walk (filled by the round scan): the earlier members' keys its occurrences must not touch, and
-    // its RoundHead words
-    uint32_t tk[ROUND_MAX - 1];
-    uint32_t ntk;
-    uint32_t *rd_touch, *rd_top, *rd_birth;
+    // a member walk (filled by the round scan): every member's key (tk[tkj] its own; ntk members), its RoundHead
+    // words and the round's junction counts (DevState::rd_jn)
+    uint32_t tk[ROUND_MAX];
+    uint32_t ntk, tkj;
+    uint32_t *rd_touch, *rd_top, *rd_birth, *rd_jn;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // batching pays below about one occurrence per 400 slots and costs above it (tools/scan_bands.py:
@@ -559,11 +559,56 @@ __device__ inline int64_t prev_live_h(const ScanArgs &A, int64_t p) {
     return i < A.halo.nleft ? -(i + 1) : NONE_POS;
 }
 
+// RoundHead::touch of member j: bit e (RT_SHARED << e) an occurrence shares a token with one of earlier member e's
+// (merging e decrements member j's pair: it leaves the tied set), bit 8 + e (RT_NEIGHBOUR << e) one sits next to
+// one of member e's (a junction)
+enum RoundTouch : uint32_t { RT_SHARED = 1u, RT_NEIGHBOUR = 1u << 8 };
+// Junctions: an occurrence of member L immediately followed (holes aside) by one of member R. Merged one after the
+// other they make (X_L, X_R) and their shared neighbour pair (b_L, a_R) falls once; the first of them to merge
+// sees the other's original token, the second the first's new one. The walks leave a junction's side out of
+// their neighbour counts and count it instead -- rd_jn[L * RJ + R] by L's walk (its right neighbour),
+// rd_jn[RJ_R + L * RJ + R] by R's walk (its left neighbour) -- and the replace applies what the merged members
+// make of it (round_junction_adjust; a member merged without its partner takes its side back as a neighbour).
+constexpr uint32_t RJ = ROUND_MAX, RJ_R = 32;
+// a round member's occurrence against the other members (tl, tll: its left neighbour and the token before it,
+// tr, trn: its right neighbour and the one after it; HOLE where none): RT bits, and its junction sides
+__device__ __attribute__((always_inline)) inline uint32_t round_touch(const ScanArgs &A, uint32_t tl, uint32_t tll, uint32_t tr,
+                                                                      uint32_t trn, int &jl, int &jr) {
+    const uint32_t j = A.tkj;
+    uint32_t t = 0;
+    jl = jr = -1;
+#pragma unroll
+    for (int e = 0; e < ROUND_MAX; e++) {
+        if ((uint32_t)e < A.ntk && (uint32_t)e != j) {
+            const uint32_t ta = A.tk[e] & 0xFFFFu, tb = A.tk[e] >> 16;
+            // a shared token: its a is the tb after a ta, or its b the ta before a tb (an earlier e decrements it)
+            if ((uint32_t)e < j) t |= ((A.a == tb && tl == ta) || (A.b == ta && tr == tb)) ? RT_SHARED << e : 0u;
+            if (tl == tb && tll == ta) { jl = e; t |= RT_NEIGHBOUR << e; }
+            if (tr == ta && trn == tb) { jr = e; t |= RT_NEIGHBOUR << e; }
+        }
+    }
+    return t;
+}
+__device__ __attribute__((always_inline)) inline void round_touch_commit(const ScanArgs &A, uint32_t t, int jl, int jr) {
+    if (t) atomicOr(A.rd_touch, t);
+    if (jl >= 0) atomicAdd(&A.rd_jn[RJ_R + (uint32_t)jl * RJ + A.tkj], 1u);
+    if (jr >= 0) atomicAdd(&A.rd_jn[A.tkj * RJ + (uint32_t)jr], 1u);
+    if (jl >= 0 || jr >= 0) atomicOr(A.rd_top, 16u);  // (the roll clears rd_jn)
+}
 // General occurrence handler (any holes, any position, shard boundaries through the halo).
 // Returns 1 if (p, next live) == (a, b).
+// RD: a multi-merge round's member walk (round_touch on the exact neighbours; a junction side is not counted)
+template <bool RD = false>
 __device__ inline int occ_slow(const ScanArgs &A, NeighbourHist &H, int64_t p, uint32_t &xx) {
     const int64_t q = next_live_h(A, p);
     if (q == NONE_POS || tok_h(A, q) != A.b) return 0;
+    int jl = -1, jr = -1;
+    if (RD && A.ntk > 1) {
+        const int64_t l = prev_live_h(A, p), r = next_live_h(A, q);
+        const int64_t ll = l != NONE_POS ? prev_live_h(A, l) : NONE_POS, rn = r != NONE_POS ? next_live_h(A, r) : NONE_POS;
+        const auto tk = [&](int64_t x) { return x != NONE_POS ? tok_h(A, x) : (uint32_t)HOLE; };
+        round_touch_commit(A, round_touch(A, tk(l), tk(ll), tk(r), tk(rn), jl, jr), jl, jr);
+    }
     if (A.count_deltas) {
         const int64_t l = prev_live_h(A, p);
         if (l != NONE_POS) {
@@ -573,7 +618,7 @@ __device__ inline int occ_slow(const ScanArgs &A, NeighbourHist &H, int64_t p, u
                 const int64_t pl = prev_live_h(A, l);
                 merged_end = pl != NONE_POS && tok_h(A, pl) == A.a;
             }
-            if (!merged_end) H.left((uint16_t)tl);
+            if (!merged_end && jl < 0) H.left((uint16_t)tl);
         }
         const int64_t r = next_live_h(A, q);
         if (r != NONE_POS) {
@@ -584,7 +629,7 @@ __device__ inline int occ_slow(const ScanArgs &A, NeighbourHist &H, int64_t p, u
                 r_occ = rn != NONE_POS && tok_h(A, rn) == A.b;
             }
             if (r_occ) xx++;
-            else H.right((uint16_t)tr);
+            else if (jr < 0) H.right((uint16_t)tr);
         }
     }
     return 1;
@@ -682,10 +727,6 @@ __device__ inline void wave_flush_records(const ScanArgs &A, const uint32_t *rec
 // next vector's first two dwords nx, ny (holes outside the stream); returns the hit mask.
 // RD: a multi-merge round's member walk -- every occurrence is also tested against the earlier members' pairs
 // (A.tk): does it touch one of their occurrences (share a token with one, or sit next to one)? Then A.rd_touch.
-// RoundHead::touch of member j: bit e (RT_SHARED << e) an occurrence shares a token with one of earlier member e's
-// (merging e decrements member j's pair: it leaves the tied set), bit 8 + e (RT_NEIGHBOUR << e) one sits next to
-// one of e's (its neighbour pairs would differ), RT_WINDOW / RT_SLOW such a test could not be made
-enum RoundTouch : uint32_t { RT_SHARED = 1u, RT_NEIGHBOUR = 1u << 8, RT_WINDOW = 1u << 16, RT_SLOW = 1u << 17 };
 template <bool RD = false>
 __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64_t vi, uint32_t m, uint32_t &xx,
                                       uint32_t pw, uint4 cv, uint32_t nx, uint32_t ny);
@@ -747,39 +788,34 @@ __device__ inline uint32_t occ_window(const ScanArgs &A, NeighbourHist &H, int64
             // every token the delta rules may look at must be inside the window
             fast = r < 14 && (win(r) != A.a || rn < 14) && (win(l) != A.b || ll >= 0);
         }
+        int jl = -1, jr = -1;
+        if (RD && fast && A.ntk > 1 && win(q) == A.b) {
+            // against every other member (round_touch); a neighbour occurrence that may reach past the window
+            // sends the occurrence to the slow path
+            const uint32_t tl = win(l), tr = win(r), tll = ll < 0 ? (uint32_t)HOLE : win(ll), trn = rn >= 14 ? (uint32_t)HOLE : win(rn);
+            bool edge = false;
+#pragma unroll
+            for (int e = 0; e < ROUND_MAX; e++) {
+                if ((uint32_t)e < A.ntk && (uint32_t)e != A.tkj) {
+                    const uint32_t ta = A.tk[e] & 0xFFFFu, tb = A.tk[e] >> 16;
+                    edge |= (tl == tb && ll < 0) || (tr == ta && rn >= 14);
+                }
+            }
+            if (edge) fast = false;
+            else round_touch_commit(A, round_touch(A, tl, tll, tr, trn, jl, jr), jl, jr);
+        }
         if (fast) {
             hit = win(q) == A.b;
             if (hit && A.count_deltas) {
                 const uint32_t tl = win(l), tr = win(r);
                 const bool merged_end = (tl == A.b) && (win(ll < 0 ? 0 : ll) == A.a);
-                if (!merged_end) H.left((uint16_t)tl);
+                if (!merged_end && jl < 0) H.left((uint16_t)tl);
                 const bool r_occ = (tr == A.a) && (win(rn > 13 ? 13 : rn) == A.b);
                 if (r_occ) xx++;
-                else H.right((uint16_t)tr);
-            }
-            if (RD && hit) {
-                // against each earlier member (ta, tb): the left neighbour ends an occurrence of it (unknown before
-                // the window: yes), the right neighbour starts one (unknown past it: yes), or this occurrence shares
-                // a token with one (its a is the tb after a ta, its b the ta before a tb). Any of them is also
-                // what a decrement of this pair by that member needs, so an untouched member keeps its count.
-                const uint32_t tl = win(l), tr = win(r), tll = win(ll < 0 ? 0 : ll), trn = win(rn > 13 ? 13 : rn);
-                // (RoundTouch bits, per earlier member e: a shared token -- merging e decrements this pair --, a
-                // neighbour occurrence, or one that may reach past the window)
-                uint32_t t = 0;
-#pragma unroll
-                for (int e = 0; e < ROUND_MAX - 1; e++) {
-                    if ((uint32_t)e < A.ntk) {
-                        const uint32_t ta = A.tk[e] & 0xFFFFu, tb = A.tk[e] >> 16;
-                        t |= ((A.a == tb && tl == ta) || (A.b == ta && tr == tb)) ? RT_SHARED << e : 0u;
-                        t |= ((tl == tb && ll >= 0 && tll == ta) || (tr == ta && rn < 14 && trn == tb)) ? RT_NEIGHBOUR << e : 0u;
-                        t |= ((tl == tb && ll < 0) || (tr == ta && rn >= 14)) ? RT_WINDOW : 0u;
-                    }
-                }
-                if (t) atomicOr(A.rd_touch, t);
+                else if (jr < 0) H.right((uint16_t)tr);
             }
         } else {
-            hit = occ_slow(A, H, p, xx);
-            if (RD && hit && A.ntk) atomicOr(A.rd_touch, RT_SLOW);  // (not resolved here: counted as touching every one)
+            hit = occ_slow<RD>(A, H, p, xx);
         }
         if (hit) hits |= 1u << k;
     }
@@ -1183,7 +1219,12 @@ __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs 
     }
     A.rd_top = &st->rd.top[0];
     A.rd_birth = &st->rd.birth[0];
-    A.ntk = 0;
+    A.rd_touch = &st->rd.touch[0];
+    A.rd_jn = &st->rd_jn[0];
+#pragma unroll
+    for (int e = 0; e < ROUND_MAX; e++) A.tk[e] = (uint32_t)e < K ? keys[e] : 0u;
+    A.ntk = K;
+    A.tkj = 0;
     const uint32_t bi = blockIdx.x - RD_FREE_WGS, j = bi % K, vb = bi / K, vg = (G - j + K - 1) / K;
     if (j == 0) {
         scan_list_dispatch<PROF, true>(A, S, H, vb, vg);  // (a list walk: plan_is_list)
@@ -1229,9 +1270,7 @@ __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs 
         atomicAdd(&st->sel_prof[22], wall_clock64() - t_in);
         atomicAdd(&st->sel_prof[23], planned ? 1ull : 1ull << 32);
     }
-#pragma unroll
-    for (int e = 0; e < ROUND_MAX - 1; e++) A.tk[e] = (uint32_t)e < j ? keys[e] : 0u;
-    A.ntk = j;
+    A.tkj = j;
     A.rd_touch = &st->rd.touch[j];
     A.rd_top = &st->rd.top[j];
     A.rd_birth = &st->rd.birth[j];
@@ -2510,12 +2549,23 @@ struct RoundCtx {
     const uint32_t *keys;  // RoundHead::key
     uint32_t *dec;         // RoundHead::dec
     uint32_t mask;         // the members merged (round_valid)
+    const uint32_t *jn;    // the junction counts (DevState::rd_jn)
+    uint32_t n;            // members
 };
 __device__ inline void round_credit(const RoundCtx &rc, uint32_t key) {
     const uint32_t x = key & 0xFFFF, y = key >> 16;
     uint32_t m = rc.j;
     for (uint32_t i = 0; i < rc.j; i++) {
         if (!(rc.mask >> i & 1u)) continue;  // (a skipped member's deltas are not applied)
+        // member i's junction decrements (round_junction_adjust): (b_i, a_e) and (b_e, a_i), unless e merged first
+        bool jd = false;
+        for (uint32_t e = 0; e < rc.n; e++) {
+            if (e == i || ((rc.mask >> e & 1u) && e < i)) continue;
+            const uint32_t ke = rc.keys[e];
+            jd |= (rc.jn[i * RJ + e] && x == (rc.keys[i] >> 16) && y == (ke & 0xFFFF)) ||
+                  (rc.jn[RJ_R + e * RJ + i] && x == (ke >> 16) && y == (rc.keys[i] & 0xFFFF));
+        }
+        if (jd) { m = i; break; }
         const uint32_t *l = rc.base + (size_t)i * (2 * 65536 + 64);
         const uint32_t ki = rc.keys[i], ai = ki & 0xFFFF, bi = ki >> 16;
         if ((y == ai && l[x]) || (x == bi && l[65536 + y]) || (x == bi && y == ai && l[2 * 65536])) { m = i; break; }
@@ -2744,25 +2794,47 @@ __device__ inline bool dev_zig_at_max_load(uint64_t cap, uint64_t D);
 //     load for every live-pair count the merged members can leave (each kills its own pair and at most one pair
 //     per new pair: D in [D0 - k, D0 + births - k] after k merges);
 //   - else the round ends.
-enum RoundWhy : uint32_t { RW_ALL, RW_FLAGS, RW_WALK, RW_TOUCH, RW_REC, RW_END, RW_ARENA, RW_SLACK, RW_CAP, RW_N };
+enum RoundWhy : uint32_t { RW_ALL, RW_FLAGS, RW_WALK, RW_TOUCH, RW_REC, RW_END, RW_ARENA, RW_SLACK, RW_CAP, RW_JUNC, RW_N };
 struct RoundVerdict {
     uint32_t mask;   // members merged (bit j: member j; bit 0 always)
     uint32_t k;      // how many
     uint32_t why;    // what ended the round (RoundWhy), at member jend
     uint32_t jend;
-    uint32_t flags;  // (RW_FLAGS: the merged members' RoundHead::top bits)
+    uint32_t flags;  // (RW_FLAGS: 1 a new pair at the top count, 2 adjacent occurrences at it, 4 a junction's pair
+                     // with a non-member at it, 8 two merged members' junction pair at it)
 };
 // (dbase: the members' delta buffers, DELTA_WORDS apart. A member's adjacent occurrences (xx, its tail word) make
 // (X, X), one more new pair, with count xx: a flag only at the top count; the (b, a) they decrement is a tied
-// pair leaving the set, or a later member that shares their tokens and is skipped.)
-__device__ inline RoundVerdict round_valid(const RoundHead &R, const uint32_t *dbase, uint32_t T, uint32_t X0, uint32_t x_end,
-                                           uint32_t C, uint32_t arena_top, uint32_t rec_cap) {
+// pair leaving the set, or a later member that shares their tokens and is skipped. jn: the junction counts: a
+// merged member's junction side makes one more new pair -- (X_e, a_o) or (b_o, X_e), with its count in e's deltas
+// plus the junctions --, and two merged members' junctions one more, (X_L, X_R), counted alike by both walks.)
+__device__ inline RoundVerdict round_valid(const RoundHead &R, const uint32_t *dbase, const uint32_t *jn, uint32_t T, uint32_t X0,
+                                           uint32_t x_end, uint32_t C, uint32_t arena_top, uint32_t rec_cap) {
     constexpr uint32_t DW = 2 * 65536 + 64;
     RoundVerdict v{1u, 1u, RW_ALL, 0u, 0u};
-    const uint32_t xx0 = dbase[2 * 65536];
-    uint64_t births = R.birth[0] + (xx0 ? 1u : 0u);
-    uint32_t flags = (R.top[0] & 1u) | (xx0 >= T ? 2u : 0u);
     const uint32_t n = min(R.n, (uint32_t)ROUND_MAX);
+    uint32_t anyj = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < (uint32_t)ROUND_MAX; e++)
+        if (e < n) anyj |= R.top[e] & 16u;
+    uint64_t births = 0;
+    uint32_t flags = 0;
+    const auto bring = [&](uint32_t e) {  // what merging member e adds to the map
+        const uint32_t *de = dbase + (size_t)e * DW;
+        const uint32_t xxe = de[2 * 65536];
+        births += R.birth[e] + (xxe ? 1u : 0u);
+        flags |= (R.top[e] & 1u) | (xxe >= T ? 2u : 0u);
+        if (anyj) {
+#pragma unroll
+            for (uint32_t o = 0; o < (uint32_t)ROUND_MAX; o++) {
+                if (o >= n || o == e) continue;
+                const uint32_t ko = R.key[o], cl = jn[e * RJ + o], cr = jn[RJ_R + o * RJ + e];
+                if (cl) { births++; if (de[65536 + (ko & 0xFFFF)] + cl >= T) flags |= 4u; }  // (X_e, a_o)
+                if (cr) { births++; if (de[ko >> 16] + cr >= T) flags |= 4u; }              // (b_o, X_e)
+            }
+        }
+    };
+    bring(0);
 #pragma unroll
     for (uint32_t j = 1; j < (uint32_t)ROUND_MAX; j++) {
         if (j >= n) break;
@@ -2770,8 +2842,21 @@ __device__ inline RoundVerdict round_valid(const RoundHead &R, const uint32_t *d
         if (flags) { v.why = RW_FLAGS; v.flags = flags; break; }
         const uint32_t tch = R.touch[j];
         if (tch & v.mask * RT_SHARED) continue;  // decremented: no longer tied
+        uint64_t jb = 0;
+        uint32_t jf = 0;
+        bool jbad = false;
+        if (anyj) {
+#pragma unroll
+            for (uint32_t i = 0; i < (uint32_t)ROUND_MAX; i++) {
+                if (i >= j || !(v.mask >> i & 1u)) continue;
+                const uint32_t a1 = jn[i * RJ + j], a2 = jn[RJ_R + i * RJ + j], b1 = jn[j * RJ + i], b2 = jn[RJ_R + j * RJ + i];
+                jbad |= a1 != a2 || b1 != b2;
+                if (a1) { jb++; if (a1 >= T) jf |= 8u; }  // (X_i, X_j)
+                if (b1) { jb++; if (b1 >= T) jf |= 8u; }  // (X_j, X_i)
+            }
+        }
         v.why = !R.walk[j]                                                ? RW_WALK
-                : (tch & (v.mask * RT_NEIGHBOUR | RT_WINDOW | RT_SLOW))   ? RW_TOUCH
+                : jbad                                                    ? RW_JUNC
                 : R.rec[j] != T                                           ? RW_REC
                 : X0 + v.k >= x_end                                       ? RW_END
                 : (uint64_t)arena_top + (uint64_t)(j + 1) * T > rec_cap   ? RW_ARENA
@@ -2789,12 +2874,41 @@ __device__ inline RoundVerdict round_valid(const RoundHead &R, const uint32_t *d
         }
         v.mask |= 1u << j;
         v.k++;
-        const uint32_t xxj = dbase[(size_t)j * DW + 2 * 65536];
-        births += R.birth[j] + (xxj ? 1u : 0u);
-        flags |= (R.top[j] & 1u) | (xxj >= T ? 2u : 0u);
+        bring(j);
+        births += jb;
+        flags |= jf;
     }
     if (v.why == RW_ALL) v.jend = n;
     return v;
+}
+// Member j's junction sides in its update blocks' deltas (group g of the count update, its threads' t from beg):
+// with the partner merged, the first of the two decrements (b_L, a_R) and the second makes (X_L, X_R); a partner
+// not merged leaves member j's side a plain neighbour (decrement and new pair with the original token).
+__device__ inline void round_junction_adjust(uint32_t (&dv)[UPD_MAX_PER], uint32_t g, uint32_t beg, uint32_t per, uint32_t j,
+                                             uint32_t mask, uint32_t n, const uint32_t *keys, const uint32_t *jn, uint32_t X0) {
+    const auto add = [&](uint32_t t, uint32_t c) {
+#pragma unroll
+        for (uint32_t k = 0; k < UPD_MAX_PER; k++)
+            if (k < per && beg + k * UPD_THREADS + threadIdx.x == t) dv[k] += c;
+    };
+#pragma unroll
+    for (uint32_t e = 0; e < (uint32_t)ROUND_MAX; e++) {
+        if (e >= n || e == j) continue;
+        const uint32_t ke = keys[e], ae = ke & 0xFFFF, be = ke >> 16;
+        const bool me = mask >> e & 1u;
+        const uint32_t Xe = X0 + (uint32_t)__popc(mask & ((1u << e) - 1u));
+        const uint32_t cl = jn[j * RJ + e], cr = jn[RJ_R + e * RJ + j];  // j -> e (j's right side), e -> j (its left side)
+        if (cl) {
+            if (!me) { if (g == 2 || g == 3) add(ae, cl); }
+            else if (j < e) { if (g == 2) add(ae, cl); }  // decrement (b_j, a_e)
+            else if (g == 3) add(Xe, cl);                 // make (X_j, X_e)
+        }
+        if (cr) {
+            if (!me) { if (g == 0 || g == 1) add(be, cr); }
+            else if (j < e) { if (g == 0) add(be, cr); }  // decrement (b_e, a_j)
+            else if (g == 1) add(Xe, cr);                 // make (X_e, X_j)
+        }
+    }
 }
 // pair selects: merge X+1's candidate bound, by the replace's extra workgroup (defined with the home views below)
 __device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Summ *sup, uint32_t C, uint32_t nb,
@@ -2935,19 +3049,18 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     }
     if (H.halt) return;
     const uint32_t Tc = H.top_count;
-    const RoundVerdict v = round_valid(RH, left, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap);
+    const RoundVerdict v = round_valid(RH, left, st->rd_jn, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->rd_v = v.k;
         st->rd_mask = v.mask;
         if (RH.n > 1) {  // (rounds with named keys: what ended them, the ending touch's kinds, the members skipped)
             atomicAdd(&st->rd_why[v.why], 1u);
-            if (v.why == RW_TOUCH) {
-                const uint32_t tb = RH.touch[v.jend];
-                if (tb & RT_NEIGHBOUR * 0x1Fu) atomicAdd(&st->rd_why[RW_N], 1u);
-                if (tb & RT_WINDOW) atomicAdd(&st->rd_why[RW_N + 1], 1u);
-                if (tb & RT_SLOW) atomicAdd(&st->rd_why[RW_N + 2], 1u);
-            }
-            if (v.why == RW_FLAGS) atomicAdd(&st->rd_why[RW_N + 4 + (v.flags & 1u ? 0 : 1)], 1u);
+            uint32_t jm = 0;  // members merged with a junction to an earlier merged member
+#pragma unroll
+            for (uint32_t e = 1; e < (uint32_t)ROUND_MAX; e++)
+                if ((v.mask >> e & 1u) && (RH.touch[e] & (v.mask & ((1u << e) - 1u)) * RT_NEIGHBOUR)) jm++;
+            if (jm) atomicAdd(&st->rd_why[RW_N], jm);
+            if (v.why == RW_FLAGS) atomicAdd(&st->rd_why[RW_N + 4 + (v.flags & 13u ? 0 : 1)], 1u);
             const uint32_t skipped = ((1u << v.jend) - 1u) & ~v.mask;
             if (skipped) atomicAdd(&st->rd_why[RW_N + 3], (uint32_t)__popc(skipped));
         }
@@ -2976,7 +3089,13 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     const uint32_t ublk = lb - apply_blocks;
     const uint32_t *tj = lj + 2 * 65536;
     if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc) occ_check_failed(st, X, tj[1], Tc, key);
-    const RoundCtx rc{left, j, &st->rd.key[0], &st->rd.dec[0], v.mask};
+    const uint32_t nch = update_chunks(Xp, per);
+    if (ublk < 4 * nch && (RH.top[j] & 16u)) {  // (member j's walk counted junctions)
+        const uint32_t g = ublk / nch;
+        round_junction_adjust(dv, g, (ublk - g * nch) * UPD_THREADS * per, per, j, v.mask, min(RH.n, (uint32_t)ROUND_MAX),
+                              &RH.key[0], st->rd_jn, H.cur_x);
+    }
+    const RoundCtx rc{left, j, &st->rd.key[0], &st->rd.dec[0], v.mask, st->rd_jn, min(RH.n, (uint32_t)ROUND_MAX)};
     update_block(T, st, lj, lj + 65536, tj, a, b, X, key, ublk, per, dv, H.theta, 0, Tc, NO_ID, NO_ID, NO_ID, NO_ID, &rc, Xp);
 }
 
@@ -4715,6 +4834,14 @@ __device__ inline void round_roll(const Tables &T, DevState *st, const StateHead
 #pragma unroll
     for (int j = 0; j < ROUND_MAX; j++) {
         R.walk[j] = 0; R.touch[j] = 0; R.top[j] = 0; R.birth[j] = 0; R.rec[j] = 0; R.dec[j] = 0;
+    }
+    uint32_t anyj = 0;
+#pragma unroll
+    for (int j = 0; j < ROUND_MAX; j++) anyj |= RP.top[j] & 16u;
+    if (anyj) {
+        uint4 *jw = reinterpret_cast<uint4 *>(&st->rd_jn[0]);
+#pragma unroll
+        for (int w = 0; w < 16; w++) jw[w] = make_uint4(0, 0, 0, 0);
     }
     st->rd_v = 0;
     st->rd_merges += k - 1;

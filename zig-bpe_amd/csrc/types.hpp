@@ -151,6 +151,7 @@ struct DevState {
     alignas(128) RoundHead rd;
     uint32_t rd_merges;
     uint32_t rd_why[16];     // rounds that walked named keys, by what ended them (RoundWhy, kernels.hpp)
+    alignas(16) uint32_t rd_jn[64];  // the round's junction counts (kernels.hpp RJ, RJ_R), cleared by the roll
     // the named keys' scan plans (ScanArgs::pl), by a spare wave of the naming decision (zbpe_select_next, round
     // mode), valid for layout generation rp.gen: a member walk then starts without loading its lists' words
     alignas(16) RoundPlans rp;
