@@ -123,6 +123,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     std::string k(name);
     zbpe::Engine &e = ctx->eng;
     if (k == "debug_checks") e.debug_checks = value != 0;
+    else if (k == "batch_checks" && value >= 0 && value < 65536) e.batch_checks = value ? (uint32_t)value + 256 : 0u;
     else if (k == "exact_ties") e.force_exact_ties = value != 0;
     else if (k == "exact_ties_from" && value >= 0 && value < 65536) e.exact_lo = (uint32_t)value + 256;
     else if (k == "exact_ties_to" && value >= 0 && value < 65536) e.exact_hi = (uint32_t)value + 256;

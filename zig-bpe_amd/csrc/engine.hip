@@ -222,7 +222,10 @@ zbpe_status Engine::sync_state() {
                                            " occurrences of (" + std::to_string(h_st->err_key & 0xFFFF) + "," + std::to_string(h_st->err_key >> 16) +
                                            ") counted " + std::to_string(h_st->err_cnt) + ", " + (h_st->err_mode ? "list" : "stream") +
                                            " scan, rank " + std::to_string(rank) + "]").c_str()
-                                        : "");
+                                        : (h_st->error & 4u) ? (" [first 4: pair (" + std::to_string(h_st->err4_key & 0xFFFF) + "," +
+                                                                 std::to_string(h_st->err4_key >> 16) + ") at site " +
+                                                                 std::to_string(h_st->err4_site) + "]").c_str()
+                                                              : "");
     return ZBPE_OK;
 }
 
@@ -1080,6 +1083,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             const bool was_sharded = dist();
             const double t_b = now_s();
             CHECK(run_batch(X, &done, &halted));
+            if (batch_checks && X + done > batch_checks) CHECK(table_check(X, X + done, "batch"));
             (was_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_b;
             if (was_sharded) stats.sharded_merges += done;
             X += done;
@@ -1093,6 +1097,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             if (h_st->live <= 0) continue;
             const double t_m = now_s();
             CHECK(merge_sync(X));
+            if (batch_checks && X + 1 > batch_checks) CHECK(table_check(X, X + 1, "halted merge"));
             (was_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_m;
             if (was_sharded) stats.sharded_merges++;
             halt_log.insert(halt_log.end(), {X, reason, (uint32_t)std::min(4e9, (now_s() - t_h) * 1e6)});
@@ -1102,6 +1107,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         const bool was_sharded = dist();
         const double t_m = now_s();
         CHECK(merge_sync(X));
+        if (batch_checks && X + 1 > batch_checks) CHECK(table_check(X, X + 1, "merge"));
         (was_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_m;
         if (was_sharded) stats.sharded_merges++;
         X++;
@@ -1248,7 +1254,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // (and in tie streaks: a round of one costs more than a plain merge -- the members' walks, the full selects)
     const bool rounds = round_k >= 2 && !dist() && fused_select && pair_select && refresh_prefix && lists_on && list_streak &&
                         last_tied_pct >= round_ties && !replace_split && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS;
-    const uint32_t KM = rounds ? std::min<uint32_t>(K * (uint32_t)round_k, run.vocab - X0) : K;  // merges the batch may do
+    uint32_t KM = rounds ? std::min<uint32_t>(K * (uint32_t)round_k, run.vocab - X0) : K;  // merges the batch may do
+    if (X0 < exact_lo && exact_lo < exact_hi) KM = std::min<uint32_t>(KM, exact_lo - X0);      // (no round past the exact-tie window's start)
     // headroom for KM merges: ids, occurrence records (counts never grow), tie list; compaction
     CHECK(maybe_grow_tables(X0, KM));
     if (hot_stale) CHECK(rebuild_hot());  // a table rebuild renumbered the ids the tie kernels read
@@ -1355,9 +1362,13 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     batches++;
     // rounds: the merges the batch did follow from the state (the last select began cur_x); a round that reached the
     // vocabulary's end halted the launches after it (HALT_DONE at the end: not a halt of the merge loop)
-    if (rounds && h_st->halt == HALT_DONE && h_st->halt_at == run.vocab) {
+    // (and one that reached the batch's bound Xmax -- the vocabulary's end, the exact-tie window's start, or K
+    // launch triples' worth of merges: the merge there is not started; the next batch or the host path starts it)
+    bool at_bound = false;
+    if (rounds && h_st->halt == HALT_DONE && h_st->halt_at == Xmax) {
         h_st->halt = 0;
-        h_st->cur_x = run.vocab;
+        h_st->cur_x = Xmax;
+        at_bound = true;
         HIP_OK(hipMemsetAsync(&d_st->halt, 0, 4, stream));
     }
     const uint32_t m = h_st->halt ? h_st->halt_at - X0 : rounds ? h_st->cur_x - X0 : K;
@@ -1367,7 +1378,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         HIP_OK(hipEventElapsedTime(&ms, bev[BEV_PER_MERGE * MAX_BATCH], bev[BEV_PER_MERGE * MAX_BATCH + 1]));
         run.batch_s += ms * 1e-3;
     }
-    begun = fused_select && !h_st->halt;  // the last select started merge X0 + K
+    begun = fused_select && !h_st->halt && !at_bound;  // the last select started merge X0 + K
     if (h_st->halt) {
         *halted = true;
         batch_halts++;
@@ -1487,7 +1498,7 @@ zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_
     A.gen = layout_gen;
     A.batch = scan_batch;
     A.round = round_k;
-    A.x_end = run.vocab;
+    A.x_end = Xmax;  // (the rounds' delta layouts and update grids hold merges below Xmax)
     A.hv = HomeView{nullptr, d_summ, d_sup, (uint32_t)C, V.nb, V.nsb};
     A.cs = cs;
     const int g = list_streak && list_grid > 0 ? list_grid : scan_grid(n_slots);
@@ -1509,7 +1520,7 @@ zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_
                   nullptr, 1, nullptr, 1, (int)sel_prof, 0, d_summ, d_sup, (uint32_t)C, V.nb, V.nsb, cs, nullptr, nullptr, 0, layout_gen, 0};
     R.round = round_k;
     R.per_member = pm;
-    R.x_end = run.vocab;
+    R.x_end = Xmax;
     zbpe_replace_round<<<(uint32_t)round_k * pm, 256, 0, stream>>>(d_st, base, Xmax, ab, R, T);
     LAUNCH_OK();
     if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i + 4], stream));
@@ -1519,7 +1530,7 @@ zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_
     const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
     // the naming decision must name every member the rounds take: chains up to round_k - 1 further keys
     const int chain = std::min(3, std::max(pair_chain, round_k - 2));
-    NextArgs N{BeginArgs{Xmax, C, (uint32_t)arena_limit(), d_log, 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
+    NextArgs N{BeginArgs{Xmax, C, (uint32_t)arena_limit(), d_log, 0}, Xmax, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all, 1,
                (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen, scan_plan && lists_on ? 1 : 0, lp_lazy, pair_select,
                1, 1, chain};
@@ -1719,6 +1730,17 @@ zbpe_status Engine::tokens(uint16_t *out, size_t cap, size_t *n_tokens) {
 // Full recount of the current stream against the incremental table. Multi-GPU: each shard
 // recounts the pairs it owns; ids differ between ranks but the key sets are identical, so the
 // per-rank recounts line up in key order and one all-reduce sums them.
+// option batch_checks (diagnostics): the pair table against a full recount of the stream after merges [x0, x1)
+zbpe_status Engine::table_check(uint32_t x0, uint32_t x1, const char *what) {
+    uint64_t bad = 0;
+    uint32_t info[3] = {0, 0, 0};
+    CHECK(recount_check(&bad, info));
+    if (bad || h_st->error)
+        return fail(ZBPE_INTERNAL, "after the %s of merges [%u, %u): %llu pair counts differ from a full recount (first: key (%u,%u) "
+                                   "table %u, recount %u), error flags 0x%x",
+                    what, x0, x1, (unsigned long long)bad, info[0] & 0xFFFF, info[0] >> 16, info[1], info[2], h_st->error);
+    return ZBPE_OK;
+}
 zbpe_status Engine::recount_check(uint64_t *mismatches, uint32_t *first_bad_key) {
     HIP_OK(hipSetDevice(device));
     CHECK(sync_state());

@@ -233,6 +233,7 @@ struct Engine {
     uint64_t compact_den_lists = 8;  // the same once occurrence lists are on (a compaction also rebuilds them)
     int scan_blocks_per_cu = 4;  // set by set_scan_variant: occupancy, at most four (one dispatch round)
     bool debug_checks = false;    // extra syncs + consistency checks
+    uint32_t batch_checks = 0;    // option batch_checks m (> 0): the table against a recount after every batch / host merge past merge m
     bool force_exact_ties = false;  // resolve every tie by the exact emulation and cross-check the fast path
     // the same for the merges X in [exact_lo, exact_hi) only (options "exact_ties_from" / "exact_ties_to", merge
     // indices X - 256): those run on the synchronous path, the others in device-resident batches
@@ -289,6 +290,7 @@ struct Engine {
     zbpe_status rebuild_home(uint64_t cap);
     zbpe_status select_ready();
     void halo_from_boundaries();
+    zbpe_status table_check(uint32_t x0, uint32_t x1, const char *what);
     zbpe_status comm_sum(uint32_t *d, size_t n);
     zbpe_status recount_check(uint64_t *mismatches, uint32_t *first_bad_key);
     zbpe_status compact_to_spare(uint64_t *total);

@@ -165,10 +165,15 @@ __device__ inline void pair_new(const Tables &T, DevState *st, uint32_t key, uin
     if (count >= st->theta) hot_put(T, atomicAdd(&st->hot_len, 1u), id, key, count);
     else T.hpos[id] = NO_ID;
 }
+// error 4 (a pair missing from the table): the first one's key and site, for the message
+__device__ inline void key_missing(DevState *st, uint32_t key, uint32_t site) {
+    if (atomicCAS(&st->err4_site, 0u, site) == 0u) st->err4_key = key;
+    atomicOr(&st->error, 4u);
+}
 // (returns the count before the decrement, 0 for a missing key)
 __device__ inline uint32_t pair_dec(const Tables &T, DevState *st, uint32_t key, uint32_t d) {
     uint32_t id = ht_find(T, key);
-    if (id == NO_ID) { atomicOr(&st->error, 4u); return 0; }
+    if (id == NO_ID) { key_missing(st, key, 1); return 0; }
     hot_sub(T, id, d);
     uint32_t old = atomicSub(&T.id_cnt[id], d);
     if (old < d) atomicOr(&st->error, 2u);
@@ -2613,7 +2618,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
         if (tid == 2) {
             const uint32_t occ = tail[1];
             const uint32_t top_id = ht_find(T, top_key);
-            if (top_id == NO_ID) atomicOr(&st->error, 4u);
+            if (top_id == NO_ID) key_missing(st, top_key, 2);
             else {
                 hot_sub(T, top_id, occ);
                 const uint32_t old = atomicSub(&T.id_cnt[top_id], occ);
@@ -2694,7 +2699,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
         if (!create) {
             const uint32_t key = g == 0 ? pair_key(t, a) : pair_key(b, t);
             const uint32_t id = ht_find(T, key);
-            if (id == NO_ID) atomicOr(&st->error, 4u);
+            if (id == NO_ID) key_missing(st, key, 3);
             else {
                 hot_sub(T, id, c);
                 const uint32_t old = atomicSub(&T.id_cnt[id], c);
@@ -5525,7 +5530,7 @@ __global__ void __launch_bounds__(256) zbpe_first_occ(ScanArgs A, Tables T, uint
         const int64_t q = next_live_h(A, p);  // the pair leaving the shard is owned here
         if (q == NONE_POS) continue;
         const uint32_t id = ht_find(T, pair_key(x, tok_h(A, q)));
-        if (id == NO_ID) { atomicOr(&st->error, 4u); continue; }
+        if (id == NO_ID) { key_missing(st, pair_key(x, tok_h(A, q)), 4); continue; }
         atomicMin(&first[id], (uint32_t)p);
     }
 }

@@ -156,6 +156,7 @@ struct DevState {
     // mode), valid for layout generation rp.gen: a member walk then starts without loading its lists' words
     alignas(16) RoundPlans rp;
     uint32_t err_key, err_mode;  // (error 64: the pair, and its scan's form -- scan_mode)
+    uint32_t err4_key, err4_site;  // (error 4: the first missing pair and where: 1 pair_dec, 2 merged pair, 3 update, 4 first occurrences)
 };
 struct PairHead {  // what the light test reads (the kernel entry's round trip)
     uint32_t x, key, slack, ties, births, dt, hits, plan_gen;
