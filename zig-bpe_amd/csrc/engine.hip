@@ -26,10 +26,11 @@ namespace zbpe {
 // Device allocations. ZBPE_POISON=1 (diagnostics) fills every new buffer with 0xA5 bytes, so that a read of
 // memory no kernel wrote fails the same way on every run instead of depending on what the allocator hands back.
 static hipError_t dev_alloc_raw(void **p, size_t bytes) {
-    static const bool poison = getenv("ZBPE_POISON") && atoi(getenv("ZBPE_POISON")) != 0;
+    // (ZBPE_POISON=1: 0xA5 bytes, 2: 0xFF, 3: 0x01)
+    static const int poison = getenv("ZBPE_POISON") ? atoi(getenv("ZBPE_POISON")) : 0;
     hipError_t e = hipMalloc(p, bytes);
     if (e == hipSuccess && poison) {
-        e = hipMemset(*p, 0xA5, bytes);
+        e = hipMemset(*p, poison == 2 ? 0xFF : poison == 3 ? 0x01 : 0xA5, bytes);
         if (e == hipSuccess) e = hipDeviceSynchronize();
     }
     return e;
@@ -221,7 +222,7 @@ zbpe_status Engine::sync_state() {
                     (h_st->error & 64u) ? (" [first 64: merge " + std::to_string(h_st->err_x) + " found " + std::to_string(h_st->err_occ) +
                                            " occurrences of (" + std::to_string(h_st->err_key & 0xFFFF) + "," + std::to_string(h_st->err_key >> 16) +
                                            ") counted " + std::to_string(h_st->err_cnt) + ", " + (h_st->err_mode ? "list" : "stream") +
-                                           " scan, rank " + std::to_string(rank) + "]").c_str()
+                                           " scan" + (h_st->err_light ? ", a pair select" : "") + ", rank " + std::to_string(rank) + "]").c_str()
                                         : (h_st->error & 4u) ? (" [first 4: pair (" + std::to_string(h_st->err4_key & 0xFFFF) + "," +
                                                                  std::to_string(h_st->err4_key >> 16) + ") at site " +
                                                                  std::to_string(h_st->err4_site) + "]").c_str()

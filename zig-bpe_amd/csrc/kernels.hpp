@@ -2750,6 +2750,7 @@ __device__ inline void occ_check_failed(DevState *st, uint32_t X, uint32_t occ, 
         st->err_cnt = cnt;
         st->err_key = key;
         st->err_mode = st->scan_mode;
+        st->err_light = st->last_light == X ? 1u : 0u;
     }
     atomicOr(&st->error, 64u);
 }
@@ -4771,7 +4772,8 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
 //     already stored st->ref_noprefix = X (merge X + 1 needs no decision), then arrives once more on the
 //     top counter.
 //   - blocks [nref, nref + sel_blocks) run the hot-list argmax and keep the keys at their block's max;
-//     the last of them through st->ticket (block_ticket_last: write-through partials, no fences)
+//     the last of them through the launch parity's ticket (N.rtk counter 9; block_ticket_last: write-through
+//     partials, no fences)
 //     reduces, rolls merge X, evaluates the start of merge X + 1 and, on a tie, gathers the tied keys
 //     and takes the Zig-order decision in this launch (decide_body). Before deciding it spin-waits for
 //     the refresh arrivals (and, with precomputed carries, for the prefix's final arrival).
@@ -5208,7 +5210,11 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     if (N.prof && tid == 0) atomicMax(&st->sel_ta, (unsigned long long)wall_clock64());
-    if (!single && !block_ticket_last(&st->ticket, sel_blocks, &s_flag)) return;
+    // (the ticket is the launch parity's, zeroed by the launch before: a pair select's other argmax workgroups
+    // that start late see the state words block 0 has already rewritten for the next merge, take the full path
+    // and arrive on it, and no one waits -- a shared ticket then elected a later launch's last block early, which
+    // reduced stale partials)
+    if (!single && !block_ticket_last(N.rtk + (N.round ? N.par : X & 1) * RTK_SET + 9 * RTK_STRIDE, sel_blocks, &s_flag)) return;
     if (N.round) {  // roll_preload's LDS words (wave 0) landed (a single argmax block took no ticket)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -5216,7 +5222,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     // the refresh precomputes the carries (its predicate; a round's RoundHead words are in s_pre: roll_preload)
     const bool pfx = nref && N.cs && (N.round ? reinterpret_cast<const RoundHead *>(s_pre + RI_WORDS)->ties0 > 1 : N.B.log[X - 256].ties > 1);
     // the next launch's refresh count (the launch before this one used it and has ended)
-    if (tid < 9) st_wt(N.rtk + (N.round ? N.par ^ 1u : (X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
+    if (tid < 10) st_wt(N.rtk + (N.round ? N.par ^ 1u : (X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
     unsigned long long pt = 0;
     if (N.prof && tid == 0 && !light) {
         pt = st->sel_t0;
@@ -5302,6 +5308,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
             bool tie;
             const uint32_t h = merge_begin_eval_v(T, fo, NB, &tie);
             if (light && !h && tie) {  // a pair select: the decision's commit, with its winner
+                st->last_light = N.B.X;
                 st->cur_x = N.B.X;
                 st->tie_on = 0;
                 st->cur_key = s_key[0];

@@ -156,6 +156,7 @@ struct DevState {
     // mode), valid for layout generation rp.gen: a member walk then starts without loading its lists' words
     alignas(16) RoundPlans rp;
     uint32_t err_key, err_mode;  // (error 64: the pair, and its scan's form -- scan_mode)
+    uint32_t last_light, err_light;  // the last merge a pair select started; (error 64: was the merge one)
     uint32_t err4_key, err4_site;  // (error 4: the first missing pair and where: 1 pair_dec, 2 merged pair, 3 update, 4 first occurrences)
 };
 struct PairHead {  // what the light test reads (the kernel entry's round trip)
@@ -183,7 +184,7 @@ static_assert(offsetof(DevState, rec_count) == 32 && offsetof(DevState, plan_r1)
 // per-XCD counters (workgroup i counts in i % 8) and a top counter, each on its own 128-B line. The
 // select of X - 1 zeroes parity X & 1; the host zeroes both before a batch that does not continue one.
 constexpr int RTK_STRIDE = 32;                     // words between counters
-constexpr int RTK_SET = 9 * RTK_STRIDE;            // words per parity
+constexpr int RTK_SET = 10 * RTK_STRIDE;           // words per parity (counter 9: the argmax workgroups' ticket)
 constexpr int RTK_WORDS = 2 * RTK_SET;
 // why a device-resident batch stopped (the host finishes that merge on the synchronous path)
 enum HaltReason : uint32_t {
