@@ -1085,8 +1085,10 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             const double t_b = now_s();
             CHECK(run_batch(X, &done, &halted));
             if (batch_checks && X + done > batch_checks) CHECK(table_check(X, X + done, "batch"));
-            (was_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_b;
-            if (was_sharded) stats.sharded_merges += done;
+            // (a batch that replicated at its start ran its merges as a replica)
+            const bool batch_sharded = was_sharded && dist();
+            (batch_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_b;
+            if (batch_sharded) stats.sharded_merges += done;
             X += done;
             if (!halted) continue;
             // the device stopped at merge X: clear the flag, make the selection valid, finish X here
@@ -1099,8 +1101,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             const double t_m = now_s();
             CHECK(merge_sync(X));
             if (batch_checks && X + 1 > batch_checks) CHECK(table_check(X, X + 1, "halted merge"));
-            (was_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_m;
-            if (was_sharded) stats.sharded_merges++;
+            (batch_sharded ? stats.sharded_s : stats.replicated_s) += now_s() - t_m;
+            if (batch_sharded) stats.sharded_merges++;
             halt_log.insert(halt_log.end(), {X, reason, (uint32_t)std::min(4e9, (now_s() - t_h) * 1e6)});
             X++;
             continue;
@@ -1199,7 +1201,7 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
                     bucket[k], Q[10] * us / nr, Q[11] * us / nr, Q[12] * us / nr, Q[13] * us / nr, Q[14] * us / nr);
         }
     }
-    stats.sharded_s = std::max(0.0, stats.sharded_s - stats.replicate_s);
+    stats.replicated_s = std::max(0.0, stats.replicated_s - stats.replicate_s);  // (the replicating batch's wall held it)
     stats.total_s = now_s() - t_start;
     stats.other_s = std::max(0.0, stats.total_s - ev_count - ev_select - ev_replace);
     stats.distinct_pairs = (uint64_t)std::max(h_st->live, 0);
@@ -1237,7 +1239,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         HIP_OK(hipEventElapsedTime(&ms, ev[3], ev[4]));
         run.ev_replace += ms * 1e-3;
         CHECK(sync_state());
-        stats.replicate_s += now_s() - t_rep;  // (inside this batch's wall, taken out of sharded_s in train)
+        stats.replicate_s += now_s() - t_rep;  // (inside this batch's wall, taken out of replicated_s in train)
     }
     const uint64_t C = home_slots;
     const uint32_t nb = (uint32_t)((C + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
