@@ -168,7 +168,7 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * (0: always stream the token stream; 1: token occurrence lists once counts are small), "list_ratio"
  * (train: list scan when list length * ratio < stream slots), "encode_list_ratio" (the same for encode), "list_start" (build the lists at a compaction
  * once top count * list_start < live tokens; 0: at the first compaction), "compact_den_lists" (compact_den
- * once lists are on), "print_runtime" (0: no generateInitialTokens
+ * once lists are on), "compact_den_walks" (default 4: the same once the merges only walk lists, one GPU), "print_runtime" (0: no generateInitialTokens
  * runtime line on stderr), "pair_select" (0/1, default 1: a tied merge's decision qualifies the next
  * merge's winner, whose select then skips the argmax and the decision), "pair_chain"
  * (0-3, default 2: a pair select passes that on to up to this many further merges), "pair_refresh"

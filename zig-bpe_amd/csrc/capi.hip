@@ -128,6 +128,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "exact_ties_from" && value >= 0 && value < 65536) e.exact_lo = (uint32_t)value + 256;
     else if (k == "exact_ties_to" && value >= 0 && value < 65536) e.exact_hi = (uint32_t)value + 256;
     else if (k == "compact_den" && value > 0) e.compact_den = (uint64_t)value;
+    else if (k == "compact_den_walks" && value > 0) e.compact_den_walks = (uint64_t)value;
     else if (k == "scan_blocks_per_cu" && value > 0) e.scan_blocks_per_cu = (int)value;
     else if (k == "scan_variant") return e.set_scan_variant((int)value);
     else if (k == "scan_batch") {

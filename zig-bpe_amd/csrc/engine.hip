@@ -315,6 +315,10 @@ zbpe_status Engine::compact() {
 // (a rank-local trigger let one rank's arena_rep drift from the others').
 bool Engine::holes_over() const {
     const uint64_t den = lists_on ? compact_den_lists : compact_den;
+    // one GPU or replicas, once the merges only walk lists (the last batch did): holes cost the list walks little,
+    // a compaction rebuilds the lists (~11 ms at C4) -- compact later (sharded: the ranks' scan forms may differ,
+    // so the replicated rule above stays)
+    if (!dist() && lists_on && list_streak) return (uint64_t)(n_slots - n_live) * compact_den_walks > (uint64_t)n_slots;
     if (!dist()) return (uint64_t)(n_slots - n_live) * den > (uint64_t)n_slots;
     return (global_slots - global_live) * den > global_slots;
 }

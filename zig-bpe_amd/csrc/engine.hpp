@@ -231,6 +231,7 @@ struct Engine {
     // policy knobs
     uint64_t compact_den = 8;     // compact when holes > slots / compact_den
     uint64_t compact_den_lists = 8;  // the same once occurrence lists are on (a compaction also rebuilds them)
+    uint64_t compact_den_walks = 4;  // option "compact_den_walks": the same while the merges only walk lists (one GPU)
     int scan_blocks_per_cu = 4;  // set by set_scan_variant: occupancy, at most four (one dispatch round)
     bool debug_checks = false;    // extra syncs + consistency checks
     uint32_t batch_checks = 0;    // option batch_checks m (> 0): the table against a recount after every batch / host merge past merge m
