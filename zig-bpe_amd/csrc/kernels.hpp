@@ -4979,8 +4979,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         // written by the launch before); then the last workgroup to arrive is elected (returning
         // atomics, per-XCD counters, then the top one) and arrives once more when done. Else a
         // workgroup's arrival is one non-returning add to its XCD's counter.
-        // (rounds: the round's first merge was tied -- its scan stored the count -- ties come in streaks)
-        const bool pfx = N.cs && (N.round ? ld_wt(&st->rd.ties0) > 1 : N.B.log[X - 256].ties > 1);
+        // (rounds: always, see below)
+        // (rounds: always -- a round's merges are mostly tied, and the carries are what lets the next decision
+        // name a round's keys; a round of one with an untied merge skipping them ended the naming, measured)
+        const bool pfx = N.cs && (N.round ? true : N.B.log[X - 256].ties > 1);
         // merge X's neighbour deltas, cleared for merge X + 2 by these workgroups (off the argmax's
         // critical path: the argmax grid is sized by the hot list alone; nothing in this launch reads
         // [0, 2X) -- the roll reads the tail words past it)
@@ -5220,7 +5222,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         __syncthreads();
     }
     // the refresh precomputes the carries (its predicate; a round's RoundHead words are in s_pre: roll_preload)
-    const bool pfx = nref && N.cs && (N.round ? reinterpret_cast<const RoundHead *>(s_pre + RI_WORDS)->ties0 > 1 : N.B.log[X - 256].ties > 1);
+    const bool pfx = nref && N.cs && (N.round ? true : N.B.log[X - 256].ties > 1);
     // the next launch's refresh count (the launch before this one used it and has ended)
     if (tid < 10) st_wt(N.rtk + (N.round ? N.par ^ 1u : (X + 1) & 1) * RTK_SET + tid * RTK_STRIDE, 0u);
     unsigned long long pt = 0;
