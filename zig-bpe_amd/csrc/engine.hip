@@ -1618,7 +1618,7 @@ zbpe_status Engine::merge_sync(uint32_t X) {
         }
         zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, dist() ? d_x0 : nullptr, nullptr);
         LAUNCH_OK();
-        zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
+        zbpe_scan_self<<<std::min(ntiles, SELF_GRID), SELF_THREADS, 0, stream>>>(A, d_carry);
         LAUNCH_OK();
         }
     }
@@ -1975,7 +1975,7 @@ zbpe_status Engine::encode(const uint16_t *triples_in, size_t n_merges, const ui
             LAUNCH_OK();
             zbpe_self_carry<<<1, 1024, 0, stream>>>(d_tile_fn, ntiles, d_carry, nullptr, nullptr);
             LAUNCH_OK();
-            zbpe_scan_self<<<ntiles, SELF_THREADS, 0, stream>>>(A, d_carry);
+            zbpe_scan_self<<<std::min(ntiles, SELF_GRID), SELF_THREADS, 0, stream>>>(A, d_carry);
             LAUNCH_OK();
         }
         zbpe_encode_apply<<<512, 256, 0, stream>>>(d_tok[cur], n_slots, recbuf, reccap, use_lists ? 1 : 0, X, d_st, T, tail,
