@@ -178,7 +178,8 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * replace and select launch when the reference's loop would merge them next; 1: no rounds), "round_ties" (0-100,
  * default 50: rounds in batches after one with at least this many percent tied merges), "lp_lazy" (0/1,
  * default 1: the stream's last pair is looked up only for a tie whose Zig capacity depends on it),
- * "refresh_wgs" (home refresh workgroups of a select). */
+ * "refresh_wgs" (home refresh workgroups of a select), "self_batch" (0/1, default 1: a self pair (a, a) whose
+ * list the host path would walk runs inside a batch instead of halting it). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* printTimeStats (src/utils/time_statistics.zig:36-60): the reference's "Time statistics" text for

@@ -192,13 +192,16 @@ def test_encode_batched_vs_oracle(batch):
     e.close()
 
 
+@pytest.mark.parametrize("self_batch", [0, 1])
 @pytest.mark.parametrize("kind,seed,n,vocab", [("runs", 51, 60000, 500), ("words_utf8", 52, 300000, 900), ("uniform", 53, 8000, 700)])
-def test_self_pairs_from_lists_vs_oracle(kind, seed, n, vocab):
+def test_self_pairs_from_lists_vs_oracle(kind, seed, n, vocab, self_batch):
     """Self pairs (a, a) walked from a's occurrence list (lists built at the first compaction, used for
-    every self pair) give the reference's merges and counts, in training and in encode."""
+    every self pair) give the reference's merges and counts, in training and in encode -- on the host path
+    (self_batch 0: every self pair halts its batch) and inside the device's batches (self_batch 1)."""
     text = zbpe.synth_corpus(kind, seed, n)
     r = O.train(text, vocab)
     e = zbpe.Engine(0)
+    e.set_option("self_batch", self_batch)
     e.set_option("list_start", 0)
     e.set_option("compact_den", 2)
     e.set_option("compact_den_lists", 2)

@@ -19,6 +19,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DUMP = 0
 
 
 def run(out, opts):
@@ -131,6 +132,10 @@ def analyse(d, logp):
         t_lo = ks[min(i0 + 2, len(ks) - 1)][1]
         t_hi = first[m + 1]
         h = hwin.setdefault(names.get(reason, str(reason)), {"n": 0, "window_us": 0.0, "kernels": {}})
+        if DUMP and reason == 5 and m < DUMP:  # the window's kernels: start offset, duration (us)
+            seq = [(round((a0 - t_lo) / 1e3, 1), round((a1 - a0) / 1e3, 1), name.split("(")[0].replace("void ", "")[:28])
+                   for a0, a1, name in ks[i0 + 3:] if t_lo <= a0 < t_hi]
+            print(json.dumps({"halt_merge": m, "host_us": us, "window_us": round((t_hi - t_lo) / 1e3, 1), "kernels": seq}), file=sys.stderr)
         h["n"] += 1
         h["window_us"] += (t_hi - t_lo) / 1e3
         for a0, a1, name in ks[i0 + 3:]:
@@ -174,7 +179,9 @@ if __name__ == "__main__":
     p.add_argument("--run", default="")
     p.add_argument("--analyse", nargs=2, default=None)
     p.add_argument("--opt", action="append", default=[], help="engine option k=v")
+    p.add_argument("--dump-self", type=int, default=0, help="print the kernels of self-pair halts below this merge to stderr")
     a = p.parse_args()
+    DUMP = a.dump_self
     if a.run:
         run(a.run, a.opt)
     if a.analyse:

@@ -173,6 +173,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "print_runtime") e.print_runtime = value != 0;
     else if (k == "encode_batch" && value >= 1) e.enc_batch = (uint32_t)value;
     else if (k == "self_list_ratio" && value >= 0) e.self_list_ratio = (uint32_t)value;
+    else if (k == "self_batch" && (value == 0 || value == 1)) e.self_batch = (int)value;
     else return e.fail(ZBPE_INVALID_ARGUMENT, "unknown option %s", name);
     return ZBPE_OK;
 }

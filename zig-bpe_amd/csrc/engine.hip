@@ -1280,6 +1280,11 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     if (dist()) HIP_OK(hipMemcpyAsync(d_halo, &halo, sizeof(Halo), hipMemcpyHostToDevice, stream));
     // rounds: the kernels' bound on the merge index (delta clearing, update grids)
     const uint32_t Xmax = X0 + KM;
+    // self pairs the batch takes: those self_list_ok would walk (a's list shorter than self_lim), tested by the
+    // merge's begin on the device; the others halt to the host path
+    const bool sb = self_batch && lists_on && !dist() && self_list_ratio && h_st->lists_valid;
+    const uint32_t *self_len = sb ? T.lst_len : nullptr;
+    const uint32_t self_lim = sb ? (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, ((uint64_t)n_slots + self_list_ratio - 1) / self_list_ratio) : 0u;
     const uint32_t ab = (uint32_t)std::min<uint64_t>(2048, top0 / 256 + 1);
     const int64_t slots = n_slots;
     const double t0 = now_s();
@@ -1287,7 +1292,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     if (merge_timing) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * MAX_BATCH], stream));
     for (uint32_t i = 0; i < K; i++) {
         if (rounds) {
-            CHECK(launch_round(i, X0, Xmax, K, top0, V, cs));
+            CHECK(launch_round(i, X0, Xmax, K, top0, V, cs, self_len, self_lim));
             continue;
         }
         const uint32_t X = X0 + i;
@@ -1349,7 +1354,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
             const uint64_t hot_est = std::min<uint64_t>(T.hot_cap, (uint64_t)h_st->hot_len + (uint64_t)K * sel_growth + sel_margin);
             const uint64_t work = std::max<uint64_t>(hot_est / SEL_U, C ? 0ull : 2ull * X / 4);  // refresh blocks clear the deltas
             const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
-            NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
+            NextArgs N{BeginArgs{X + 1, C, (uint32_t)arena_limit(), d_log, dist() ? 1 : 0, self_len, self_lim}, run.vocab, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                        d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all,
                        dist() ? world : 1, (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen,
                        scan_plan && lists_on ? 1 : 0, lp_lazy, pair_select, pair_refresh ? 0 : 1, pair_m3w, pair_chain};
@@ -1402,7 +1407,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         run.out_triples[3 * run.merges + 2] = (uint16_t)X;
         if (run.out_counts) run.out_counts[run.merges] = L.count;
         run.merges++;
-        global_live -= L.count;  // batch merges are never self pairs: one token per occurrence
+        if (a == b) stats.self_pair_merges++;  // (its occurrences are fewer than its count: live tokens below)
+        else global_live -= L.count;           // one token per occurrence
         stats.sum_tokens += L.live;
         if (replicated) sum_tokens_rep += L.live;
         stats.scan_alg_bytes += 2ull * L.live;
@@ -1475,6 +1481,7 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     for (uint32_t i = 0; i < m; i++) ntied += h_log[X0 - 256 + i].ties > 1 ? 1u : 0u;
     last_tied_pct = m ? 100u * ntied / m : 0u;
     n_live = h_st->live_tokens;
+    if (sb) global_live = (uint64_t)n_live;  // (self pairs only run here on one GPU or replicas: the stream is whole)
     if (dist()) halo_from_boundaries();
     *done = m;
     return ZBPE_OK;
@@ -1483,7 +1490,8 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
 // Launch triple i of a batch of multi-merge rounds (run_batch): the round scan, the round replace and the
 // select, each reading the round's first merge from the state; X0: the batch's first merge (begun by the last
 // batch's select, else here), Xmax: the bound on every merge index of the batch (delta clearing, update grids).
-zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_t K, uint32_t top0, const HomeView &V, uint32_t *cs) {
+zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_t K, uint32_t top0, const HomeView &V, uint32_t *cs,
+                                 const uint32_t *self_len, uint32_t self_lim) {
     const uint64_t C = V.C;
     const bool timed = merge_timing && i % merge_timing == 0;
     if (timed) HIP_OK(hipEventRecord(bev[BEV_PER_MERGE * i], stream));
@@ -1537,7 +1545,7 @@ zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_
     const uint32_t sel = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(NEXT_MAX_SEL, (work + NEXT_THREADS - 1) / NEXT_THREADS));
     // the naming decision must name every member the rounds take: chains up to round_k - 1 further keys
     const int chain = std::min(3, std::max(pair_chain, round_k - 2));
-    NextArgs N{BeginArgs{Xmax, C, (uint32_t)arena_limit(), d_log, 0}, Xmax, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
+    NextArgs N{BeginArgs{Xmax, C, (uint32_t)arena_limit(), d_log, 0, self_len, self_lim}, Xmax, V, d_tie_list, (uint32_t)tie_list_cap, sel, d_cand,
                d_cand + (size_t)NEXT_MAX_SEL * NEXT_CAND, d_cand + (size_t)NEXT_MAX_SEL * (NEXT_CAND + 1), d_bnd_all, 1,
                (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen, scan_plan && lists_on ? 1 : 0, lp_lazy, pair_select,
                1, 1, chain};

@@ -166,6 +166,7 @@ struct Engine {
     uint32_t list_ratio = 96;   // training: list scan when list length * ratio < stream slots
     uint32_t enc_list_ratio = 48;   // the same for encode (option "encode_list_ratio")
     uint32_t self_list_ratio = 8;  // self pair from a's list when length * ratio < stream slots (0: never)
+    int self_batch = 1;            // batches take the self pairs self_list_ratio walks (0: they halt to the host path)
     uint64_t list_start = 64;   // build lists at a compaction once top count * list_start < live tokens (0: always)
     // per-merge trace (option "trace"), ZBPE_TRACE_COLS floats per merge
     bool trace_on = false;
@@ -270,7 +271,8 @@ struct Engine {
     zbpe_status maybe_grow_tables(uint32_t X, uint32_t k);
     zbpe_status merge_sync(uint32_t X);
     zbpe_status run_batch(uint32_t X0, uint32_t *done, bool *halted);
-    zbpe_status launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_t K, uint32_t top0, const HomeView &V, uint32_t *cs);
+    zbpe_status launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_t K, uint32_t top0, const HomeView &V, uint32_t *cs,
+                             const uint32_t *self_len, uint32_t self_lim);
     zbpe_status alloc_stream(size_t n);
     zbpe_status generate_initial_tokens(size_t n);
     zbpe_status build_presence();

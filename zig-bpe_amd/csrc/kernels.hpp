@@ -1117,12 +1117,91 @@ __device__ __attribute__((always_inline)) inline bool scan_list_dispatch(const S
     }
     return false;
 }
+// Self pair (a, a) from the occurrence list of a (one GPU, or the replicas of the late phase: no
+// shard edges). A thread takes an entry that still holds a and starts a live run of a's, walks the
+// run and takes every other pair of it from the start (left-greedy, basic_tokenizer.zig:217-226),
+// with the count deltas of zbpe_scan_self: the token before the run is the first occurrence's left
+// neighbour, adjacent occurrences give (X, X), and the last one's right neighbour is the lone
+// trailing a of an odd run or the token after the run. Two walks: count, then (after one atomic per
+// wave for the records) emit. O(list length) instead of three passes over the stream.
+// (vb, vg: this workgroup among the vg that walk the list -- zbpe_scan_self_list on the host path, or a batch
+// merge's scan, scan_dispatch)
+__device__ __attribute__((always_inline)) inline void self_list_walk(const ScanArgs &A, ScanLds &S, uint32_t vb, uint32_t vg) {
+    const uint32_t a = A.a, len = A.lst_len[a];
+    if (len == NO_LIST || (vb > 0 && (uint64_t)vb * SCAN_THREADS >= len)) return;
+    const uint32_t *L = A.lists + A.lst_off[a];
+    scan_lds_clear(S);
+    if (threadIdx.x == 0) S.any = 0;
+    __syncthreads();
+    NeighbourHist H{S.left, S.right, A.left, A.right, S.hleft, S.hright};
+    const uint16_t *tok = A.tok;
+    const int lane = threadIdx.x & 63;
+    uint32_t xx = 0, any = 0;
+    const uint32_t stride = vg * SCAN_THREADS, len64 = (len + 63) & ~63u;
+    for (uint32_t i = vb * SCAN_THREADS + threadIdx.x; i - lane < len64; i += stride) {
+        int64_t p = -1, l = -1;
+        uint32_t run = 0;
+        if (i < len) {
+            p = L[i];
+            if (tok[p] == a) {
+                l = prev_live(tok, p);
+                if (l < 0 || tok[l] != a)  // the run starts here: walk it
+                    for (int64_t q = p; q >= 0 && tok[q] == a; q = next_live(tok, A.n, q)) run++;
+            }
+        }
+        const uint32_t cnt = run / 2;
+        const uint32_t incl = wave_incl_scan(cnt), total = (uint32_t)__shfl((int)incl, 63);
+        if (!total) continue;
+        any = 1;
+        uint32_t base = 0;
+        if (lane == 0) {
+            base = atomicAdd(A.rec_ctr, total);
+            atomicAdd(A.occ_out, total);
+        }
+        base = (uint32_t)__shfl((int)base, 0) + incl - cnt;
+        if (!cnt) continue;
+        if (A.count_deltas && l >= 0) H.left((uint16_t)tok[l]);
+        int64_t q = p;
+        for (uint32_t k = 0; k < cnt; k++) {
+            if (base + k < A.rec_cap) A.rec[base + k] = (uint32_t)q;
+            else atomicOr(&A.st->error, 8u);
+            q = next_live(tok, A.n, q);       // the second a of occurrence k
+            q = q >= 0 ? next_live(tok, A.n, q) : -1;  // the next live token after it
+        }
+        if (A.count_deltas) {
+            xx += cnt - 1;
+            if (run & 1) H.right((uint16_t)a);  // the lone trailing a
+            else if (q >= 0) H.right((uint16_t)tok[q]);
+        }
+    }
+    xx = wave_sum(xx);
+    if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
+    if (lane == 0 && any) S.any = 1;
+    __syncthreads();
+    if (S.any) scan_lds_flush(S, A.left, A.right);
+}
 // one pair scan with resolved arguments: the list form when the shorter token list is short
 // enough, else the stream form
 // (vb, vg: this workgroup among the vg that walk a list)
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool PROF = false, bool BATCH = false>
 __device__ __attribute__((always_inline)) inline void scan_dispatch(const ScanArgs &A, ScanLds &S, const StateHead &H,
                                                                     uint32_t vb, uint32_t vg) {
+    if (A.a == A.b) {  // a self pair the batch took (merge_begin_eval_v: a's list is short, the lists are valid)
+        if (!A.lists || !H.lists_valid) {
+            if (threadIdx.x == 0) atomicOr(&A.st->error, 2048u);
+            return;
+        }
+        if (vb == 0 && threadIdx.x == 0) {
+            A.st->scan_mode = 1;
+            if (A.log) {
+                A.log[A.X - 256].mode = 1;
+                A.log[A.X - 256].list_len = A.lst_len[A.a];
+                A.log[A.X - 256].key_live = A.tokcnt ? (uint32_t)A.tokcnt[A.a] : 0u;
+            }
+        }
+        self_list_walk(A, S, vb, vg);
+        return;
+    }
     if (scan_list_dispatch<PROF>(A, S, H, vb, vg)) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.st->scan_mode = 0;
     scan_pairs_body<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH>(A, S);
@@ -2705,9 +2784,10 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 const uint32_t old = atomicSub(&T.id_cnt[id], c);
                 if (old < c) atomicOr(&st->error, 2u);
                 if (old == c) { live_delta--; home_add(T, st, key, false); }
-                // (a pair's first decrement sees its count before the merge: each tied pair counts once)
-                if (rc && old == top_count) round_credit(*rc, key);
-                if (pr_key != NO_ID && old == top_count)
+                // (a pair's first decrement sees its count before the merge: each tied pair counts once; a self
+                // pair's lone trailing a decrements the merged pair itself, which is no other tied pair)
+                if (rc && old == top_count && key != top_key) round_credit(*rc, key);
+                if (pr_key != NO_ID && old == top_count && key != top_key)
                     atomicAdd(&st->pr_dt, key == pr_key    ? 0x10001u
                                           : key == pr_key2 ? 0x80001u
                                           : key == pr_key3 ? 0x100001u
@@ -3015,7 +3095,9 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
         return;
     }
     const uint32_t ublk = blockIdx.x - apply_blocks;
-    if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count) occ_check_failed(st, R.X, R.tail[1], H.top_count, R.top_key);
+    // (a self pair: runs of a hold fewer occurrences than (a, a) pairs)
+    if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count && R.a != R.b)
+        occ_check_failed(st, R.X, R.tail[1], H.top_count, R.top_key);
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof, H.top_count,
                  R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2, pr_key3, pr_key4);
     if (R.prof) {
@@ -3094,7 +3176,7 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     }
     const uint32_t ublk = lb - apply_blocks;
     const uint32_t *tj = lj + 2 * 65536;
-    if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc) occ_check_failed(st, X, tj[1], Tc, key);
+    if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc && a != b) occ_check_failed(st, X, tj[1], Tc, key);
     const uint32_t nch = update_chunks(Xp, per);
     if (ublk < 4 * nch && (RH.top[j] & 16u)) {  // (member j's walk counted junctions)
         const uint32_t g = ublk / nch;
@@ -3395,68 +3477,11 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
     }
 }
 
-// Self pair (a, a) from the occurrence list of a (one GPU, or the replicas of the late phase: no
-// shard edges). A thread takes an entry that still holds a and starts a live run of a's, walks the
-// run and takes every other pair of it from the start (left-greedy, basic_tokenizer.zig:217-226),
-// with the count deltas of zbpe_scan_self: the token before the run is the first occurrence's left
-// neighbour, adjacent occurrences give (X, X), and the last one's right neighbour is the lone
-// trailing a of an odd run or the token after the run. Two walks: count, then (after one atomic per
-// wave for the records) emit. O(list length) instead of three passes over the stream.
+// Self pair (a, a) from the occurrence list of a on the host path (self_list_walk)
 __global__ void __launch_bounds__(SCAN_THREADS) zbpe_scan_self_list(ScanArgs A0) {
     const ScanArgs A = scan_args_resolve(A0, load_head(A0.st), A0.X);
-    const uint32_t a = A.a, len = A.lst_len[a];
-    if (len == NO_LIST || (blockIdx.x > 0 && (uint64_t)blockIdx.x * SCAN_THREADS >= len)) return;
-    const uint32_t *L = A.lists + A.lst_off[a];
     __shared__ ScanLds S;
-    scan_lds_clear(S);
-    if (threadIdx.x == 0) S.any = 0;
-    __syncthreads();
-    NeighbourHist H{S.left, S.right, A.left, A.right, S.hleft, S.hright};
-    const uint16_t *tok = A.tok;
-    const int lane = threadIdx.x & 63;
-    uint32_t xx = 0, any = 0;
-    const uint32_t stride = gridDim.x * SCAN_THREADS, len64 = (len + 63) & ~63u;
-    for (uint32_t i = blockIdx.x * SCAN_THREADS + threadIdx.x; i - lane < len64; i += stride) {
-        int64_t p = -1, l = -1;
-        uint32_t run = 0;
-        if (i < len) {
-            p = L[i];
-            if (tok[p] == a) {
-                l = prev_live(tok, p);
-                if (l < 0 || tok[l] != a)  // the run starts here: walk it
-                    for (int64_t q = p; q >= 0 && tok[q] == a; q = next_live(tok, A.n, q)) run++;
-            }
-        }
-        const uint32_t cnt = run / 2;
-        const uint32_t incl = wave_incl_scan(cnt), total = (uint32_t)__shfl((int)incl, 63);
-        if (!total) continue;
-        any = 1;
-        uint32_t base = 0;
-        if (lane == 0) {
-            base = atomicAdd(A.rec_ctr, total);
-            atomicAdd(A.occ_out, total);
-        }
-        base = (uint32_t)__shfl((int)base, 0) + incl - cnt;
-        if (!cnt) continue;
-        if (A.count_deltas && l >= 0) H.left((uint16_t)tok[l]);
-        int64_t q = p;
-        for (uint32_t k = 0; k < cnt; k++) {
-            if (base + k < A.rec_cap) A.rec[base + k] = (uint32_t)q;
-            else atomicOr(&A.st->error, 8u);
-            q = next_live(tok, A.n, q);       // the second a of occurrence k
-            q = q >= 0 ? next_live(tok, A.n, q) : -1;  // the next live token after it
-        }
-        if (A.count_deltas) {
-            xx += cnt - 1;
-            if (run & 1) H.right((uint16_t)a);  // the lone trailing a
-            else if (q >= 0) H.right((uint16_t)tok[q]);
-        }
-    }
-    xx = wave_sum(xx);
-    if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
-    if (lane == 0 && any) S.any = 1;
-    __syncthreads();
-    if (S.any) scan_lds_flush(S, A.left, A.right);
+    self_list_walk(A, S, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3810,7 +3835,14 @@ struct BeginArgs {
     uint32_t rec_cap;   // arena entries the halt test allows (records go at st->arena_top)
     MergeLog *log;
     int rep;            // sharded: test the replicated bound st->arena_rep (every rank halts alike)
+    // a self pair (a, a) runs in the batch when a's list is shorter than self_lim (the host path's self_list_ok:
+    // one GPU or replicas, valid lists); self_len: the list lengths, nullptr: every self pair halts
+    const uint32_t *self_len;
+    uint32_t self_lim;
 };
+__device__ inline uint32_t self_verdict(const BeginArgs &B, uint32_t key) {
+    return B.self_len && B.self_len[key & 0xFFFF] < B.self_lim ? HALT_NONE : HALT_SELF;
+}
 __device__ inline uint32_t merge_begin_eval_v(const Tables &T, const FinishOut &f, const BeginArgs &B, bool *tie) {
     *tie = false;
     const int32_t live = f.live;
@@ -3825,7 +3857,7 @@ __device__ inline uint32_t merge_begin_eval_v(const Tables &T, const FinishOut &
         *tie = true;
         return HALT_NONE;
     }
-    return (key & 0xFFFF) == (key >> 16) ? HALT_SELF : HALT_NONE;
+    return (key & 0xFFFF) == (key >> 16) ? self_verdict(B, key) : HALT_NONE;
 }
 // the state words read, loaded together
 __device__ inline FinishOut finish_state(const DevState *st) {
@@ -4612,7 +4644,8 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                                    MergeLog *log, int dyn, unsigned long long *prof_t = nullptr,
                                    const uint32_t *cs = nullptr, bool plan_on = false, const PlanCtx &plan = PlanCtx{},
                                    uint32_t plan_gen = 0, uint32_t pair_x = 0, bool m3_w4 = false,
-                                   bool chain = false, bool chain2 = false, bool chain3 = false, bool rplan = false) {
+                                   bool chain = false, bool chain2 = false, bool chain3 = false, bool rplan = false,
+                                   const BeginArgs *self_b = nullptr) {
     static_assert(NT >= 192 && NT % 64 == 0, "three waves");
     // plan (NT >= 256): wave 3 finds the smallest home's key itself and loads its scan plan during the
     // carries; the commit below stores it with cur_key
@@ -4721,7 +4754,7 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
         if (verdict) {
             st->halt = HALT_TIE;
             st->halt_at = st->cur_x;
-        } else if ((key & 0xFFFF) == (key >> 16)) {
+        } else if ((key & 0xFFFF) == (key >> 16) && (!self_b || self_verdict(*self_b, key) != HALT_NONE)) {
             st->halt = HALT_SELF;
             st->halt_at = st->cur_x;
         } else {
@@ -5525,7 +5558,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     }
     decide_body<NEXT_THREADS>(st, tie_list, total, total, N.V, N.B.log, 1, N.prof ? &pt : nullptr, pfx ? N.cs : nullptr,
                               plan_on, plan, N.gen, N.pair && NB.X + 1 < N.x_end ? NB.X + 1 : 0u, N.m3_w4 != 0,
-                              N.skip_refresh != 0 && N.chain != 0, N.chain >= 2, N.chain >= 3, N.round != 0);
+                              N.skip_refresh != 0 && N.chain != 0, N.chain >= 2, N.chain >= 3, N.round != 0, &NB);
     if (N.prof && tid == 0) { sel_tick(st, 4, &pt); atomicAdd(&st->sel_prof[8], 1ull); st->pp_t[7] = wall_clock64(); }
     put_key();
 }
