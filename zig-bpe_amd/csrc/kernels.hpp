@@ -3267,7 +3267,7 @@ __global__ void __launch_bounds__(256) zbpe_reset_merge(DevState *st, uint32_t *
 constexpr int SELF_THREADS = 256;
 constexpr int SELF_PER_THREAD = 32;
 constexpr int SELF_TILE = SELF_THREADS * SELF_PER_THREAD;  // 8192
-constexpr int64_t SELF_GRID = 1024;                         // persistent zbpe_scan_self workgroups (4 per CU)
+constexpr int64_t SELF_GRID = 768;                          // persistent zbpe_scan_self workgroups (3 per CU)
 static_assert(SELF_TILE == PRES_BLK, "a self-pair tile is one presence block");
 // run-parity function of a segment: bit0 = no live non-a (x -> x ^ p), bit1 = p
 __device__ inline uint8_t self_apply(uint8_t f, uint8_t x) { return (f & 1) ? (uint8_t)(x ^ ((f >> 1) & 1)) : (uint8_t)((f >> 1) & 1); }
@@ -3393,20 +3393,35 @@ __global__ void zbpe_self_x0(const uint32_t *__restrict__ fns, int rank, uint8_t
     *x0 = x;
 }
 // (persistent: a workgroup takes tiles blockIdx.x, blockIdx.x + gridDim.x, ...; its LDS neighbour bins are
-// cleared once and flushed once -- one workgroup per 8192-token tile spent most of its time on them)
+// cleared once and flushed once, and its records are staged over several tiles: a flush (one global atomic on the
+// shared record counter) only once another tile might not fit. One workgroup per tile with a flush each made
+// ~2.6e5 same-address atomics per launch at C4 -- ~12 ns each at the counter, most of the launch's 1-2 ms.)
+constexpr uint32_t SELF_REC = 2 * (SELF_TILE / 2);  // staged records: two tiles' worth (a tile holds <= SELF_TILE / 2)
 __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, const uint8_t *__restrict__ carry_in) {
     const ScanArgs A = scan_args_resolve(A0, load_head(A0.st), A0.X);
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
-    __shared__ uint32_t s_rec[SELF_TILE / 2];
+    __shared__ uint32_t s_rec[SELF_REC];
     __shared__ uint8_t s_wave[SELF_THREADS / 64];
-    __shared__ uint32_t s_nrec, s_base, s_any;
+    __shared__ uint32_t s_nrec, s_base;
     for (int i = threadIdx.x; i < LDS_BINS; i += SELF_THREADS) { s_left[i] = 0; s_right[i] = 0; }
-    if (threadIdx.x == 0) { s_nrec = 0; s_any = 0; }
+    if (threadIdx.x == 0) s_nrec = 0;
     NeighbourHist H{s_left, s_right, A.left, A.right};
     const uint16_t *tok = A.tok;
-    const uint32_t a = A.a;
+    const uint32_t a = A.a, lane = threadIdx.x & 63;
     const int64_t ntiles = (A.n + SELF_TILE - 1) / SELF_TILE;
-    uint32_t xx = 0;
+    uint32_t xx = 0, staged = 0, occ = 0;  // (staged, occ: workgroup-uniform)
+    const auto flush = [&]() {  // every thread; after a barrier that published s_nrec == staged
+        if (threadIdx.x == 0) s_base = atomicAdd(A.rec_ctr, staged);
+        __syncthreads();
+        const uint32_t base = s_base;
+        for (uint32_t i = threadIdx.x; i < staged; i += SELF_THREADS)
+            if (base + i < A.rec_cap) A.rec[base + i] = s_rec[i];
+        if (threadIdx.x == 0 && base + staged > A.rec_cap) atomicOr(&A.st->error, 8u);
+        occ += staged;
+        staged = 0;
+        __syncthreads();  // (every thread has read s_base and s_rec)
+        if (threadIdx.x == 0) s_nrec = 0;
+    };
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t beg = tile * (int64_t)SELF_TILE;
         const int64_t end = min(A.n, beg + SELF_TILE);
@@ -3414,61 +3429,61 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
         uint32_t w[16];
         self_load(tok, t0, end, w);
         // parity of the live a-run entering my slots: the tile's carry through the threads before mine
-        // (self_block_scan's barrier also orders the last tile's record flush before s_nrec is reused)
+        // (self_block_scan's barrier also orders a flush's s_nrec reset before this tile's records)
         const uint8_t pre = self_block_scan(self_walk(w, a, -1, nullptr), s_wave, nullptr);
         uint32_t cand;
         (void)self_walk(w, a, self_apply(pre, carry_in[tile] & 1), &cand);
-        while (cand) {  // a's at even offsets of their runs: occurrences when the next live token is an a
-            const int i = __builtin_ctz(cand);
-            cand &= cand - 1;
-            const int64_t p = t0 + i;
-            const int64_t q = next_live_h(A, p);
-            if (q == NONE_POS || tok_h(A, q) != a) continue;
-            // occurrence (p, q)
-            if (A.count_deltas) {
-                // first a of its run: the left neighbour is not the end of a previous occurrence
-                const int64_t l = prev_live_h(A, p);
-                if (l != NONE_POS) {
-                    const uint32_t tl = tok_h(A, l);
-                    if (tl != a) H.left((uint16_t)tl);
-                }
-                const int64_t r = next_live_h(A, q);
-                if (r != NONE_POS) {
-                    const uint32_t tr = tok_h(A, r);
-                    bool r_occ = false;
-                    if (tr == a) {
-                        const int64_t r2 = next_live_h(A, r);
-                        r_occ = r2 != NONE_POS && tok_h(A, r2) == a;
+        // a's at even offsets of their runs: occurrences when the next live token is an a (wave-uniform steps:
+        // one LDS atomic per wave and step reserves the records)
+        while (__ballot(cand != 0)) {
+            bool hit = false;
+            int64_t p = 0;
+            if (cand) {
+                const int i = __builtin_ctz(cand);
+                cand &= cand - 1;
+                p = t0 + i;
+                const int64_t q = next_live_h(A, p);
+                hit = q != NONE_POS && tok_h(A, q) == a;
+                if (hit && A.count_deltas) {  // occurrence (p, q)
+                    // the left neighbour, unless it is the end of a previous occurrence
+                    const int64_t l = prev_live_h(A, p);
+                    if (l != NONE_POS) {
+                        const uint32_t tl = tok_h(A, l);
+                        if (tl != a) H.left((uint16_t)tl);
                     }
-                    if (r_occ) xx++;
-                    else H.right((uint16_t)tr);
+                    const int64_t r = next_live_h(A, q);
+                    if (r != NONE_POS) {
+                        const uint32_t tr = tok_h(A, r);
+                        bool r_occ = false;
+                        if (tr == a) {
+                            const int64_t r2 = next_live_h(A, r);
+                            r_occ = r2 != NONE_POS && tok_h(A, r2) == a;
+                        }
+                        if (r_occ) xx++;
+                        else H.right((uint16_t)tr);
+                    }
                 }
             }
-            const uint32_t slot = atomicAdd(&s_nrec, 1u);
-            s_rec[slot] = (uint32_t)p;
+            const uint64_t hm = __ballot(hit);
+            if (hm) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&s_nrec, (uint32_t)__popcll(hm));
+                base = (uint32_t)__shfl((int)base, 0);
+                if (hit) s_rec[base + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint32_t)p;
+            }
         }
         __syncthreads();
         const uint32_t nrec = s_nrec;
-        if (nrec) {
-            if (threadIdx.x == 0) {
-                s_base = atomicAdd(A.rec_ctr, nrec);
-                atomicAdd(A.occ_out, nrec);
-                s_any = 1;
-                if (A.pres) pres_set(A, beg);  // SELF_TILE == PRES_BLK: the tile is one presence block
-            }
-            __syncthreads();
-            const uint32_t base = s_base;
-            for (uint32_t i = threadIdx.x; i < nrec; i += SELF_THREADS)
-                if (base + i < A.rec_cap) A.rec[base + i] = s_rec[i];
-            if (threadIdx.x == 0 && base + nrec > A.rec_cap) atomicOr(&A.st->error, 8u);
-            __syncthreads();  // (every thread has read s_base and s_rec)
-            if (threadIdx.x == 0) s_nrec = 0;
-        }
+        if (nrec != staged && threadIdx.x == 0 && A.pres) pres_set(A, beg);  // (SELF_TILE == PRES_BLK: one block)
+        staged = nrec;
+        if (staged > SELF_REC - SELF_TILE / 2) flush();  // the next tile might not fit
     }
+    if (staged) flush();
+    if (threadIdx.x == 0 && occ) atomicAdd(A.occ_out, occ);
     xx = wave_sum(xx);
     if ((threadIdx.x & 63) == 0 && xx) atomicAdd(A.xx_out, xx);
     __syncthreads();
-    if (s_any) {
+    if (occ) {
         for (int i = threadIdx.x; i < LDS_BINS; i += SELF_THREADS) {
             uint32_t l = s_left[i], r = s_right[i];
             if (l) atomicAdd(&A.left[i], l);
