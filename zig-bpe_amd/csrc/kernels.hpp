@@ -3351,14 +3351,32 @@ __global__ void __launch_bounds__(1024) zbpe_self_carry(const uint8_t *__restric
                                                         uint8_t *__restrict__ carry_in, const uint8_t *x0,
                                                         uint32_t *shard_fn) {
     // function of a tile: x -> all_a ? x ^ p : p   (x, p parities)
+    // (a thread's segment is a whole number of 16-tile words, read and written as 16-B vectors: one byte at a time,
+    // each a dependent miss, the launch took 0.1-0.25 ms at C4)
     __shared__ uint8_t s_all[1024], s_par[1024];
-    const int64_t per = (ntiles + 1023) / 1024;
+    const int64_t per = ((ntiles + 1023) / 1024 + 15) & ~(int64_t)15;
     const int64_t b0 = threadIdx.x * per, b1 = min(ntiles, b0 + per);
+    const auto word = [&](int64_t t, uint8_t (&f)[16]) {  // tile functions [t, t + 16) (past ntiles: identity)
+        if (t + 16 <= ntiles) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(tile_fn + t);
+            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 16; k++) f[k] = (uint8_t)(u[k >> 2] >> (8 * (k & 3)));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) f[k] = t + k < ntiles ? tile_fn[t + k] : (uint8_t)1;
+        }
+    };
     uint8_t all = 1, par = 0;  // identity
-    for (int64_t t = b0; t < b1; t++) {
-        uint8_t f = tile_fn[t], fa = f & 1, fp = (f >> 1) & 1;
-        if (fa) par ^= fp;   // compose: g(x) = f(cur(x))
-        else { all = 0; par = fp; }
+    for (int64_t t = b0; t < b1; t += 16) {
+        uint8_t f[16];
+        word(t, f);
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint8_t fa = f[k] & 1, fp = (f[k] >> 1) & 1;
+            if (fa) par ^= fp;  // compose: g(x) = f(cur(x))
+            else { all = 0; par = fp; }
+        }
     }
     s_all[threadIdx.x] = all;
     s_par[threadIdx.x] = par;
@@ -3376,10 +3394,23 @@ __global__ void __launch_bounds__(1024) zbpe_self_carry(const uint8_t *__restric
     }
     __syncthreads();
     uint8_t x = s_par[threadIdx.x];
-    for (int64_t t = b0; t < b1; t++) {
-        carry_in[t] = x;
-        uint8_t f = tile_fn[t], fa = f & 1, fp = (f >> 1) & 1;
-        x = fa ? (x ^ fp) : fp;
+    for (int64_t t = b0; t < b1; t += 16) {
+        uint8_t f[16], c[16];
+        word(t, f);
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            c[k] = x;
+            const uint8_t fa = f[k] & 1, fp = (f[k] >> 1) & 1;
+            x = fa ? (x ^ fp) : fp;
+        }
+        if (t + 16 <= ntiles) {
+            uint32_t u[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 16; k++) u[k >> 2] |= (uint32_t)c[k] << (8 * (k & 3));
+            *reinterpret_cast<uint4 *>(carry_in + t) = make_uint4(u[0], u[1], u[2], u[3]);
+        } else {
+            for (int k = 0; k < 16 && t + k < ntiles; k++) carry_in[t + k] = c[k];
+        }
     }
 }
 // parity of the a-run entering shard `rank` from the gathered whole-shard functions of ranks < rank
