@@ -88,8 +88,9 @@ typedef struct zbpe_stats {
  * consumer compares zbpe_stats_size() with the size of the zbpe_stats of the header it was built against
  * before passing a zbpe_stats: the library writes zbpe_stats_size() bytes.
  *   1: up to tie_fallbacks ... list_builds;  2: + replications, phase split, sharded_merges;
- *   3: + tie_crosschecks, generate_tokens_s;  4: + pair_selects, round_merges. */
-#define ZBPE_STATS_VERSION 4
+ *   3: + tie_crosschecks, generate_tokens_s;  4: + pair_selects, pair_scans;
+ *   5: pair_scans -> round_merges (same size and offset: merges applied by rounds beyond their first members). */
+#define ZBPE_STATS_VERSION 5
 size_t zbpe_stats_size(void);
 
 /* Create a single-GPU context on HIP device `device`. */

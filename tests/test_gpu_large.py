@@ -164,6 +164,9 @@ def test_c4_full_sequence_vs_oracle_golden(c4):
     assert c4.stats.tie_iterations == sum(t > 1 for t in g["ties"])
     assert c4.log[:, 3].astype(int).tolist() == g["ties"]  # every merge's tied-pair count (rounds derive them)
     assert c4.log[:, 1].astype(int).tolist() == g["counts"]
+    # the multi-merge rounds ran (a gate change that switched them off would otherwise leave this green):
+    # round 5 measured ~15,000 merges applied beyond the rounds' first members
+    assert c4.stats.round_merges > 10000, c4.stats.round_merges
     k, ln, fnv = g["fnv64_after"][-1]
     assert k == 31744 and c4.final_len == ln and c4.final_fnv == int(fnv, 16)
     cps = {k: (ln, h) for k, ln, h in g["fnv64_after"]}
@@ -237,6 +240,7 @@ def test_c3_full_sequence_vs_oracle_golden(c3):
     assert c3.log[:, 3].astype(int).tolist() == g["ties"]
     k, ln, fnv = g["fnv64_after"][-1]
     assert k == 3840 and c3.final_len == ln and c3.final_fnv == int(fnv, 16)
+    assert c3.stats.round_merges > 0, "multi-merge rounds did not run on C3"
 
 
 def test_c3_every_tie_exact(c3):
@@ -320,3 +324,35 @@ def test_c4_pair_chain_depths_same_run(c4, depth):
     assert st.tie_iterations == c4.stats.tie_iterations
     assert fnv == c4.final_fnv and mism == 0
     assert (st.pair_selects > c4.stats.pair_selects) == (depth > 2)
+
+
+# --- multi-merge rounds: the same run whatever the round size -------------------
+ROUND_OPTS = [
+    {"round_k": 1},
+    {"round_k": 2, "round_ties": 0},
+    {"round_k": 5, "round_ties": 0},
+    {"round_k": 5, "round_ties": 0, "pair_chain": 0},
+]
+
+
+@pytest.mark.parametrize("opts", ROUND_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_c3_round_sizes_same_run(c3, opts):
+    """C3 with rounds off (round_k 1), rounds of two, and rounds of five in every list streak (round_ties 0, with
+    and without pair chains): every merge, count and per-merge tie count of the golden, the final stream (FNV-64)
+    and a full recount; the rounds ran exactly when enabled"""
+    g = large_golden(C3_GOLDEN)
+    e = zbpe.Engine(0)
+    e.upload(c3.text)
+    try:
+        for k, v in opts.items():
+            e.set_option(k, v)
+        m, c, st = e.train_resident(c3.vocab)
+        log = e.merge_log()
+        fnv = O.fnv64(e.tokens())
+        mism = e.verify_counts()
+    finally:
+        e.close()
+    assert m.astype(int).tolist() == g["merges"] and c.astype(int).tolist() == g["counts"]
+    assert log[:, 3].astype(int).tolist() == g["ties"]
+    assert fnv == c3.final_fnv and mism == 0
+    assert (st.round_merges > 0) == (opts["round_k"] > 1), st.round_merges

@@ -1026,6 +1026,9 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
     hot_stale = true;
     halo = halo0;
     HIP_OK(hipMemsetAsync(d_delta, 0, 2 * DELTA_WORDS * 4, stream));
+    // the rounds' member buffers: each round's select clears them, but a train that failed between a round's
+    // replace and its select (e.g. a hot-list rebuild's error) left them dirty for the next train on this engine
+    HIP_OK(hipMemsetAsync(d_rdelta, 0, (size_t)ROUND_MAX * DELTA_WORDS * 4, stream));
     HIP_OK(hipMemsetAsync(d_hist, 0, 65536 * 4, stream));
     HIP_OK(hipEventRecord(ev[0], stream));
     if (n + (next_byte >= 0 ? 1 : 0) >= 2) {

@@ -4903,14 +4903,9 @@ __device__ inline void round_roll(const Tables &T, DevState *st, const StateHead
             T.lst_off[X0 + x] = arena_top + m * Tc;
             T.lst_len[X0 + x] = rec[m];
         }
-        if (x) {
+        if (x) {  // (the whole row: d_log is not cleared between trains)
             ties = ties - 1u - dec[prev];
-            MergeLog &L = log[X0 + x - 256];
-            L.key = key[m];
-            L.count = Tc;
-            L.live = (uint32_t)(live_tokens - (long long)x * Tc);
-            L.ties = ties;
-            L.mode = 1;
+            log[X0 + x - 256] = MergeLog{key[m], Tc, (uint32_t)(live_tokens - (long long)x * Tc), ties, 1u, rec[m], 0u, 0u};
         }
         sum += rec[m];
         prev = last = m;
@@ -5161,7 +5156,8 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         if (st->pp_t[5]) {  // the replace launch: its work span, its start -> this select's start, its phases
             unsigned long long *P = st->pipe_prof[pp_bucket(X)];
             const unsigned long long t5 = st->pp_t[5];
-            P[5] += st->pp_t[6] - t5;
+            // (pp_t[6]: the replace's latest block end, 0 when no probed replace block stamped it since pp_t[5])
+            if (st->pp_t[6] >= t5) P[5] += st->pp_t[6] - t5;
             P[6] += now - t5;
             P[7]++;
             for (int k = 8; k <= 12; k++) {
