@@ -177,7 +177,9 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * "pair_m3w" (0/1: the decision's further tied homes by a wave of their own), "round_k" (1-5, default 5:
  * members of a multi-merge round -- a tied merge and the tied keys its decision named, applied in one scan,
  * replace and select launch when the reference's loop would merge them next; 1: no rounds), "round_ties" (0-100,
- * default 50: rounds in batches after one with at least this many percent tied merges), "lp_lazy" (0/1,
+ * default 50: rounds in batches after one with at least this many percent tied merges), "round_untied" (0/1, default 1:
+ * untied rounds -- an untied merge and the pairs of the next distinct counts, each held by one pair, merged in one
+ * launch triple while no pair the merged members made reaches the next member's count; rounds in every list streak), "lp_lazy" (0/1,
  * default 1: the stream's last pair is looked up only for a tie whose Zig capacity depends on it),
  * "refresh_wgs" (home refresh workgroups of a select), "self_batch" (0/1, default 1: a self pair (a, a) whose
  * list the host path would walk runs inside a batch instead of halting it). */

@@ -332,6 +332,8 @@ ROUND_OPTS = [
     {"round_k": 2, "round_ties": 0},
     {"round_k": 5, "round_ties": 0},
     {"round_k": 5, "round_ties": 0, "pair_chain": 0},
+    {"round_k": 5, "round_untied": 0},  # tied rounds only (the round-5 form)
+    {"round_k": 3, "round_ties": 100},  # untied rounds, tied ones only in all-tied batches
 ]
 
 
@@ -356,3 +358,23 @@ def test_c3_round_sizes_same_run(c3, opts):
     assert log[:, 3].astype(int).tolist() == g["ties"]
     assert fnv == c3.final_fnv and mism == 0
     assert (st.round_merges > 0) == (opts["round_k"] > 1), st.round_merges
+
+
+@pytest.mark.parametrize("untied", [0, 1])
+def test_c4_untied_rounds_same_run(c4, untied):
+    """C4 with untied rounds off and on: all 31,744 merges, counts and per-merge tie counts, the final stream and the
+    recount are the fixture's; with them on, untied rounds merged members (the mid phase's merges are mostly untied)"""
+    e = zbpe.Engine(0)
+    e.upload(c4.text)
+    try:
+        e.set_option("round_untied", untied)
+        m, c, st = e.train_resident(c4.vocab)
+        log = e.merge_log()
+        fnv = O.fnv64(e.tokens())
+        mism = e.verify_counts()
+    finally:
+        e.close()
+    assert np.array_equal(m, c4.merges) and np.array_equal(c, c4.counts)
+    assert np.array_equal(log[:, 3], c4.log[:, 3])
+    assert fnv == c4.final_fnv and mism == 0
+    assert st.round_merges > 0

@@ -1191,6 +1191,11 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
         fprintf(stderr, "sel_prof: merged members with a junction to an earlier one %u; members skipped (decremented by a merged member) %u; "
                         "ending flags: a new pair (or junction pair) at the top count %u, only adjacent occurrences %u\n",
                 W[10], W[13], W[14], W[15]);
+        const uint32_t *U = W + 16;  // (kernels.hpp RW_U)
+        fprintf(stderr, "sel_prof: untied rounds with named keys %u, members merged beyond the first %u; ended by: all walked %u, "
+                        "a merged member's pair at the member's count %u, not walked %u, decremented %u, records %u, vocabulary end %u, "
+                        "arena %u, junction counts differ %u\n",
+                U[10], U[11], U[0], U[1], U[2], U[3], U[4], U[5], U[6], U[9]);
         const unsigned long long nw = (P[23] & 0xFFFFFFFFull) + (P[23] >> 32);
         fprintf(stderr, "sel_prof: round member walks %llu (%llu with the decision's plan), average %.2f us from the workgroup's state words in (round_scan) to the walk's start\n",
                 nw, P[23] & 0xFFFFFFFFull, P[22] * us / std::max(1.0, (double)nw));
@@ -1262,8 +1267,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // merges, which the device decides (round_valid), so the kernels take the merge index from the state and
     // the batch's merges are counted after it
     // (and in tie streaks: a round of one costs more than a plain merge -- the members' walks, the full selects)
+    // (untied rounds, option round_untied: in every list streak -- the mid phase's merges are mostly untied)
     const bool rounds = round_k >= 2 && !dist() && fused_select && pair_select && refresh_prefix && lists_on && list_streak &&
-                        last_tied_pct >= round_ties && !replace_split && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS;
+                        (round_untied || last_tied_pct >= round_ties) && !replace_split && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS;
     uint32_t KM = rounds ? std::min<uint32_t>(K * (uint32_t)round_k, run.vocab - X0) : K;  // merges the batch may do
     if (X0 < exact_lo && exact_lo < exact_hi) KM = std::min<uint32_t>(KM, exact_lo - X0);      // (no round past the exact-tie window's start)
     // headroom for KM merges: ids, occurrence records (counts never grow), tie list; compaction
@@ -1553,6 +1559,7 @@ zbpe_status Engine::launch_round(uint32_t i, uint32_t X0, uint32_t Xmax, uint32_
                (int)sel_prof, cs, d_rtk, A.dir_row, A.dir, A.dir_w, layout_gen, scan_plan && lists_on ? 1 : 0, lp_lazy, pair_select,
                1, 1, chain};
     N.round = round_k;
+    N.untied = round_untied;
     N.par = rpar;
     N.seq = launch_seq++;
     N.rlog_i = i;

@@ -56,6 +56,7 @@ struct Engine {
     bool last_rounds = false;
     int round_k = 5;            // option "round_k": members of a multi-merge round (1: no rounds; at most ROUND_MAX)
     uint32_t round_ties = 50;   // option "round_ties": rounds once this many percent of the last batch's merges were tied
+    int round_untied = 1;       // option "round_untied": untied rounds (the next distinct counts' pairs), in every list streak
     uint32_t last_tied_pct = 0; // (the last batch's)
 
     // multi-GPU: this rank's shard and its neighbours' boundary tokens

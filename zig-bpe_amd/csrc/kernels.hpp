@@ -385,13 +385,12 @@ struct NeighbourHist {
     uint32_t *g_left, *g_right;
     uint32_t *h_left = nullptr, *h_right = nullptr;  // nullptr: no hash (large tokens go to HBM)
     // multi-merge rounds: every add to the global deltas returns the old value, so that the workgroup counts the
-    // new pairs (a delta word leaving 0: one per distinct neighbour token, whichever workgroup adds first) and
-    // sees a new pair reaching the top count (the add that completes it); rd = its LDS words {new pairs, top,
-    // queued adds}. The walk's adds past the LDS bins and hash are queued in LDS (rd_queue, the round scan's
-    // dynamic LDS) and made by the flush, all in flight together: a returning add here held its thread for a
-    // memory round trip per occurrence.
+    // new pairs (a delta word leaving 0: one per distinct neighbour token, whichever workgroup adds first) and the
+    // largest count a new pair reaches (the add that completes a word sees its final value); rd = its LDS words
+    // {new pairs, largest new count, queued adds}. The walk's adds past the LDS bins and hash are queued in LDS
+    // (rd_queue, the round scan's dynamic LDS) and made by the flush, all in flight together: a returning add here
+    // held its thread for a memory round trip per occurrence.
     uint32_t *rd = nullptr;
-    uint32_t top = 0;
     __device__ inline void gadd(uint32_t *g, uint32_t t, uint32_t v) const;
     __device__ inline void add(uint32_t *lds, uint32_t *h, uint32_t *g, uint16_t t) const {
         if (t < LDS_BINS) {
@@ -441,7 +440,7 @@ __device__ inline void NeighbourHist::gadd(uint32_t *g, uint32_t t, uint32_t v) 
     }
     const uint32_t old = atomicAdd(&g[t], v);  // (queue full: added here)
     if (old == 0) atomicAdd(&rd[0], 1u);
-    if (old + v >= top) rd[1] = 1u;
+    atomicMax(&rd[1], old + v);
 }
 // option sel_prof: merge-index bucket of the pipeline probes (DevState::pipe_prof)
 __device__ inline int pp_bucket(uint32_t X) { return X < 8192 ? 0 : X < 20000 ? 1 : 2; }
@@ -502,7 +501,7 @@ struct ScanArgs {
     // words and the round's junction counts (DevState::rd_jn)
     uint32_t tk[ROUND_MAX];
     uint32_t ntk, tkj;
-    uint32_t *rd_touch, *rd_top, *rd_birth, *rd_jn;
+    uint32_t *rd_touch, *rd_top, *rd_birth, *rd_jn, *rd_nmax;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
 // batching pays below about one occurrence per 400 slots and costs above it (tools/scan_bands.py:
@@ -598,7 +597,7 @@ __device__ __attribute__((always_inline)) inline void round_touch_commit(const S
     if (t) atomicOr(A.rd_touch, t);
     if (jl >= 0) atomicAdd(&A.rd_jn[RJ_R + (uint32_t)jl * RJ + A.tkj], 1u);
     if (jr >= 0) atomicAdd(&A.rd_jn[A.tkj * RJ + (uint32_t)jr], 1u);
-    if (jl >= 0 || jr >= 0) atomicOr(A.rd_top, 16u);  // (the roll clears rd_jn)
+    if (jl >= 0 || jr >= 0) atomicOr(A.rd_top, RT_JUNCTION);  // (the roll clears rd_jn)
 }
 // General occurrence handler (any holes, any position, shard boundaries through the halo).
 // Returns 1 if (p, next live) == (a, b).
@@ -915,7 +914,7 @@ struct ScanLds {
     unsigned long long scanned;
     uint32_t lrec[LREC_CAP];
     uint32_t lrec_n, lrec_base;
-    uint32_t rd[3];  // multi-merge rounds: {new pairs, a new pair reached the top count, queued adds} (NeighbourHist::rd)
+    uint32_t rd[3];  // multi-merge rounds: {new pairs, the largest new-pair count, queued adds} (NeighbourHist::rd)
 };
 // A list walk's wave with hit lanes: stage their record starts `pr` in the workgroup's LDS buffer; lanes
 // past its capacity reserve in the arena directly (one atomic per wave). Every lane of the wave calls it.
@@ -1004,28 +1003,29 @@ __device__ inline void scan_lds_flush_rd(const ScanArgs &A, ScanLds &S, const Ne
         const uint32_t vk = (e[k] >> 17) & 1u ? 0x8000u : 1u;
         oq[k] = e[k] != ~0u ? atomicAdd(((e[k] >> 16) & 1u ? A.right : A.left) + (e[k] & 0xFFFFu), vk) : 1u;
     }
-    uint32_t births = 0, top = 0;
+    uint32_t births = 0, top = 0;  // (top: the largest value an add of this thread left in a delta word)
 #pragma unroll
     for (int k = 0; k < NB; k++) {
         births += v[k] && old[k] == 0 ? 1u : 0u;
-        top |= v[k] && old[k] + v[k] >= H.top ? 1u : 0u;
+        top = v[k] ? max(top, old[k] + v[k]) : top;
     }
 #pragma unroll
     for (int k = 0; k < NQ; k++) {
         const uint32_t vk = (e[k] >> 17) & 1u ? 0x8000u : 1u;
         births += e[k] != ~0u && oq[k] == 0 ? 1u : 0u;
-        top |= e[k] != ~0u && oq[k] + vk >= H.top ? 1u : 0u;
+        top = e[k] != ~0u ? max(top, oq[k] + vk) : top;
     }
     births = wave_sum(births);
-    top = __ballot(top) ? 1u : 0u;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) top = max(top, (uint32_t)__shfl_xor((int)top, off));
     if ((threadIdx.x & 63) == 0) {
         if (births) atomicAdd(&S.rd[0], births);
-        if (top) S.rd[1] = 1u;
+        if (top) atomicMax(&S.rd[1], top);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         if (S.rd[0]) atomicAdd(A.rd_birth, S.rd[0]);
-        if (S.rd[1]) atomicOr(A.rd_top, 1u);
+        if (S.rd[1]) atomicMax(A.rd_nmax, S.rd[1]);
     }
 }
 // add the workgroup's neighbour histograms to the global deltas (every thread calls it)
@@ -1255,22 +1255,28 @@ __device__ inline void round_free(const ScanArgs &A0, uint32_t K, const PairTail
     }
     if (lane == 0) st->rd.freeb[w] = (int32_t)min(f, (int64_t)0x7FFFFFFF);
 }
-// (P, PT, pr_full: the naming decision's words, loaded by the kernel's entry with the state head)
+// (P, PT, pr_full: the naming decision's words, U: the untied names, loaded by the kernel's entry with the state head)
 // (PROF: the pipeline probes, st->pp_t: the member walks' phases as a list scan's, the bound workgroups' end in pp_t[13])
 template <int UNROLL, bool NT, bool FILTER, bool PIPE, bool COMPACT, bool BATCH, bool PROF = false>
 __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs &A0, const StateHead &H, ScanLds &S, const PairHead &P,
-                                                                 const PairTail &PT, const RoundPlans &RPL, uint32_t pr_full) {
+                                                                 const PairTail &PT, const RoundPlans &RPL, uint32_t pr_full,
+                                                                 const UntiedHead &U) {
     DevState *st = A0.st;
     const unsigned long long t_in = PROF ? wall_clock64() : 0ull;
     const uint32_t X0 = H.cur_x, T = H.top_count, G = gridDim.x - RD_FREE_WGS;
     ScanArgs A = scan_args_resolve(A0, H, X0);
-    // the members: merge X0 and the keys its decision named (pr_x == X0 + 1), while every one is a list walk
+    // the members: merge X0 and the keys its decision named (pr_x == X0 + 1: a tied round), or the keys of the next
+    // distinct counts the select that began X0 named (ur.x == X0: an untied round), while every one is a list walk
     // with room in the arena and below the vocabulary's end
-    const uint32_t keys[ROUND_MAX] = {pair_key(A.a, A.b), P.key, PT.key2, PT.key3, PT.key4};
+    const bool tied = P.x == X0 + 1 && pr_full == X0 + 1, untied = !tied && U.x == X0 && U.n > 0;
+    const uint32_t keys[ROUND_MAX] = {pair_key(A.a, A.b), tied ? P.key : U.key[0], tied ? PT.key2 : U.n > 1 ? U.key[1] : NO_ID,
+                                      tied ? PT.key3 : U.n > 2 ? U.key[2] : NO_ID, tied ? PT.key4 : U.n > 3 ? U.key[3] : NO_ID};
+    const uint32_t cnts[ROUND_MAX] = {T, tied ? T : U.cnt[0], tied ? T : U.cnt[1], tied ? T : U.cnt[2], tied ? T : U.cnt[3]};
     uint32_t K = 1;
-    if (A0.round >= 2 && P.x == X0 + 1 && pr_full == X0 + 1 && plan_is_list(A, H) && T) {
+    if (A0.round >= 2 && (tied || untied) && plan_is_list(A, H) && T) {
         const uint32_t kmax = min(min((uint32_t)A0.round, (uint32_t)ROUND_MAX), A0.x_end > X0 ? A0.x_end - X0 : 1u);
         // (a self pair's occurrences overlap in runs: the touch tests assume none do, so one ends the members)
+        // (records: member j's at arena_top + j T, at most T each -- an untied member's count is below T)
         while (K < kmax && keys[K] != NO_ID && (keys[K] & 0xFFFF) != (keys[K] >> 16) && (uint64_t)(K + 1) * T <= (uint64_t)A.rec_cap) K++;
     }
     // Workgroups [0, RD_FREE_WGS) bound the free slots (one wave per range) and store the round's words; the
@@ -1288,13 +1294,16 @@ __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs 
     if (blockIdx.x < RD_FREE_WGS) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->rd.n = K;
-            st->rd.ties = P.ties;
+            st->rd.ties = tied ? P.ties : 0u;
             st->rd.live0 = st->live;
-            st->rd.ties0 = st->tie_count;  // (merge X0's tied pairs, as its begin logged them)
+            st->rd.ties0 = st->tie_count;  // (merge X0's tied pairs, as its begin logged them: 1 in an untied round)
 #pragma unroll
-            for (int e = 0; e < ROUND_MAX; e++) st->rd.key[e] = (uint32_t)e < K ? keys[e] : NO_ID;
+            for (int e = 0; e < ROUND_MAX; e++) {
+                st->rd.key[e] = (uint32_t)e < K ? keys[e] : NO_ID;
+                st->rd.cnt[e] = (uint32_t)e < K ? cnts[e] : 0u;
+            }
         }
-        round_free(A0, K, PT, blockIdx.x * (SCAN_THREADS / 64) + (threadIdx.x >> 6));
+        if (tied) round_free(A0, K, PT, blockIdx.x * (SCAN_THREADS / 64) + (threadIdx.x >> 6));
         if (PROF) {
             __syncthreads();
             if (threadIdx.x == 0) atomicMax(&st->pp_t[13], (unsigned long long)wall_clock64());
@@ -1304,6 +1313,7 @@ __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs 
     A.rd_top = &st->rd.top[0];
     A.rd_birth = &st->rd.birth[0];
     A.rd_touch = &st->rd.touch[0];
+    A.rd_nmax = &st->rd.nmax[0];
     A.rd_jn = &st->rd_jn[0];
 #pragma unroll
     for (int e = 0; e < ROUND_MAX; e++) A.tk[e] = (uint32_t)e < K ? keys[e] : 0u;
@@ -1327,6 +1337,10 @@ __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs 
     A.rec_cap = T;
     A.rec_ctr = &st->rd.rec[j];
     A.pres = nullptr;
+    // (the walk sizes its entries per thread from the pair's count)
+#pragma unroll
+    for (int e = 1; e < ROUND_MAX; e++)
+        if ((uint32_t)e == j) A.top_count = cnts[e];
     // the plan the naming decision loaded (RoundPlans, entry words), else two dependent round trips
     uint32_t kj = 0;
 #pragma unroll
@@ -1358,7 +1372,8 @@ __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs 
     A.rd_touch = &st->rd.touch[j];
     A.rd_top = &st->rd.top[j];
     A.rd_birth = &st->rd.birth[j];
-    if (scan_list_dispatch<PROF, true>(A, S, H, vb, vg) && vb == 0 && threadIdx.x == 0) st->rd.walk[j] = 1;
+    A.rd_nmax = &st->rd.nmax[j];
+    if (scan_list_dispatch<PROF, true>(A, S, H, vb, vg) && vb == 0 && threadIdx.x == 0) atomicOr(&st->rd.top[j], RT_WALKED);
 }
 // PROF (option sel_prof): the pipeline probes; a separate instantiation, so the production kernel's
 // code and register allocation are untouched by them
@@ -1382,15 +1397,19 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
     PairHead P{};
     PairTail PT{};
     RoundPlans RPL{};
+    UntiedHead U{};
     uint32_t pr_full = 0;
     if (ROUND) {
         P = *reinterpret_cast<const PairHead *>(&stp->pr_x);
         PT = *reinterpret_cast<const PairTail *>(&stp->pr_plan[0]);
         RPL = stp->rp;
+        U = stp->ur;
         pr_full = stp->pr_full;
         asm volatile("" ::"s"(P.x), "s"(P.key), "s"(P.ties), "s"(PT.key2), "s"(PT.key3), "s"(PT.key4), "s"(PT.h2), "s"(PT.h3),
                      "s"(PT.h4), "s"(PT.h5), "s"(PT.h6), "s"(PT.hmax), "s"(pr_full), "s"(RPL.gen), "s"(RPL.key[0]),
                      "s"(RPL.key[1]), "s"(RPL.key[2]), "s"(RPL.key[3]));
+        asm volatile("" ::"s"(U.x), "s"(U.n), "s"(U.key[0]), "s"(U.key[1]), "s"(U.key[2]), "s"(U.key[3]), "s"(U.cnt[0]),
+                     "s"(U.cnt[1]), "s"(U.cnt[2]), "s"(U.cnt[3]));
         // the round's argument words (a kernarg word first used deep in the walk's setup cost a cache-miss round trip)
         asm volatile("" ::"s"(A0.round), "s"(A0.x_end), "s"(A0.lst_len), "s"(A0.lst_off), "s"(A0.dir), "s"(A0.dir_w),
                      "s"(A0.log), "s"(A0.list_ratio), "s"(A0.nb), "s"(A0.tokcnt), "s"(A0.cs), "s"(A0.hv.summ), "s"(A0.hv.sup),
@@ -1404,7 +1423,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
     if (A0.dyn && H.halt) return;
     __shared__ ScanLds S;
     if (ROUND) {
-        round_scan<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH, PROF>(A0, H, S, P, PT, RPL, pr_full);
+        round_scan<UNROLL, NT, FILTER, PIPE, COMPACT, BATCH, PROF>(A0, H, S, P, PT, RPL, pr_full, U);
         return;
     }
     const ScanArgs A = scan_args_resolve(A0, H, A0.X);
@@ -1540,7 +1559,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{S.left, S.right, A.left, A.right, S.hleft, S.hright};
-    if (RD) { H.rd = S.rd; H.top = A.top_count; }
+    if (RD) H.rd = S.rd;
     const uint4 *tv = reinterpret_cast<const uint4 *>(A.tok);
     const int64_t nvec = (A.n + 7) / 8;
     const int lane = threadIdx.x & 63;
@@ -1656,7 +1675,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
     }
     xx = wave_sum(xx);
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
-    if (RD && lane == 0 && xx) atomicOr(A.rd_top, 2u);  // adjacent occurrences: (X, X) is new, (b, a) falls
+    if (RD && lane == 0 && xx) atomicOr(A.rd_top, RT_XX);
     if (lane == 0 && any) S.any = 1;
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
@@ -1686,7 +1705,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[1], (unsigned long long)wall_clock64());
     NeighbourHist H{s_left, s_right, A.left, A.right, S.hleft, S.hright};
-    if (RD) { H.rd = S.rd; H.top = A.top_count; }
+    if (RD) H.rd = S.rd;
     const uint16_t *tok = A.tok;
     const uint32_t key = by_b ? A.b : A.a;
     uint32_t xx = 0, any = 0;
@@ -1778,7 +1797,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
     }
     xx = wave_sum(xx);
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
-    if (RD && lane == 0 && xx) atomicOr(A.rd_top, 2u);
+    if (RD && lane == 0 && xx) atomicOr(A.rd_top, RT_XX);
     if (lane == 0 && any) s_any = 1;
     __syncthreads();
     if (PROF && threadIdx.x == 0) atomicMax(&A.st->pp_t[2], (unsigned long long)wall_clock64());
@@ -2865,8 +2884,8 @@ struct ReplaceArgs {
 __device__ inline uint64_t dev_zig_cap_for(uint64_t D);
 __device__ inline bool dev_zig_at_max_load(uint64_t cap, uint64_t D);
 // Which members of a multi-merge round the reference's loop merges next, one after the other (every workgroup
-// of the round's replace evaluates it on the same words: the scan's RoundHead, final at this launch). The named
-// keys are the decision's tied pairs in home order; member j >= 1 is
+// of the round's replace evaluates it on the same words: the scan's RoundHead, final at this launch).
+// Tied rounds: the named keys are the decision's tied pairs in home order; member j >= 1 is
 //   - skipped when an occurrence of it shares a token with one of a merged member's (RT_SHARED): merging that
 //     member decrements its pair, which leaves the tied set, so the loop never takes it (tied pairs only fall);
 //   - else merged next (merge X0 + the members merged before it) when it was walked (a list form) with exactly
@@ -2880,7 +2899,15 @@ __device__ inline bool dev_zig_at_max_load(uint64_t cap, uint64_t D);
 //     load for every live-pair count the merged members can leave (each kills its own pair and at most one pair
 //     per new pair: D in [D0 - k, D0 + births - k] after k merges);
 //   - else the round ends.
+// Untied rounds (ties0 == 1): member j holds the j-th distinct count T_j below T (the only pair with it; every
+// pair outside the round is below the last member's count). It is merged next when no merged member shares a
+// token with it (else its count fell: the round ends), it was walked with exactly T_j occurrences, its
+// junctions agree, and no pair a merged member made -- its neighbours' new pairs, (X, X), junction pairs --
+// reaches T_j: then T_j is the unique top count, whatever the Zig map's order; else the round ends.
 enum RoundWhy : uint32_t { RW_ALL, RW_FLAGS, RW_WALK, RW_TOUCH, RW_REC, RW_END, RW_ARENA, RW_SLACK, RW_CAP, RW_JUNC, RW_N };
+// DevState::rd_why: [0, RW_N) tied rounds' ends, [RW_N, RW_N + 6) tied-round details (sel_prof), untied rounds' ends
+// from RW_U, then untied rounds named (RW_U + RW_N) and their merged members (RW_U + RW_N + 1)
+constexpr uint32_t RW_U = 16;
 struct RoundVerdict {
     uint32_t mask;   // members merged (bit j: member j; bit 0 always)
     uint32_t k;      // how many
@@ -2890,33 +2917,36 @@ struct RoundVerdict {
                      // with a non-member at it, 8 two merged members' junction pair at it)
 };
 // (dbase: the members' delta buffers, DELTA_WORDS apart. A member's adjacent occurrences (xx, its tail word) make
-// (X, X), one more new pair, with count xx: a flag only at the top count; the (b, a) they decrement is a tied
-// pair leaving the set, or a later member that shares their tokens and is skipped. jn: the junction counts: a
-// merged member's junction side makes one more new pair -- (X_e, a_o) or (b_o, X_e), with its count in e's deltas
-// plus the junctions --, and two merged members' junctions one more, (X_L, X_R), counted alike by both walks.)
+// (X, X), one more new pair, with count xx; the (b, a) they decrement is a tied pair leaving the set, or a later
+// member that shares their tokens (skipped, or the untied round's end). jn: the junction counts: a merged member's
+// junction side makes one more new pair -- (X_e, a_o) or (b_o, X_e), with its count in e's deltas plus the
+// junctions --, and two merged members' junctions one more, (X_L, X_R), counted alike by both walks.)
 __device__ inline RoundVerdict round_valid(const RoundHead &R, const uint32_t *dbase, const uint32_t *jn, uint32_t T, uint32_t X0,
                                            uint32_t x_end, uint32_t C, uint32_t arena_top, uint32_t rec_cap) {
     constexpr uint32_t DW = 2 * 65536 + 64;
     RoundVerdict v{1u, 1u, RW_ALL, 0u, 0u};
     const uint32_t n = min(R.n, (uint32_t)ROUND_MAX);
+    const bool untied = R.ties0 == 1;
     uint32_t anyj = 0;
 #pragma unroll
     for (uint32_t e = 0; e < (uint32_t)ROUND_MAX; e++)
-        if (e < n) anyj |= R.top[e] & 16u;
+        if (e < n) anyj |= R.top[e] & RT_JUNCTION;
     uint64_t births = 0;
     uint32_t flags = 0;
+    uint32_t M = 0;  // the largest count of a pair the merged members made
     const auto bring = [&](uint32_t e) {  // what merging member e adds to the map
         const uint32_t *de = dbase + (size_t)e * DW;
         const uint32_t xxe = de[2 * 65536];
         births += R.birth[e] + (xxe ? 1u : 0u);
-        flags |= (R.top[e] & 1u) | (xxe >= T ? 2u : 0u);
+        M = max(M, max(R.nmax[e], xxe));
+        flags |= (R.nmax[e] >= T ? 1u : 0u) | (xxe >= T ? 2u : 0u);
         if (anyj) {
 #pragma unroll
             for (uint32_t o = 0; o < (uint32_t)ROUND_MAX; o++) {
                 if (o >= n || o == e) continue;
                 const uint32_t ko = R.key[o], cl = jn[e * RJ + o], cr = jn[RJ_R + o * RJ + e];
-                if (cl) { births++; if (de[65536 + (ko & 0xFFFF)] + cl >= T) flags |= 4u; }  // (X_e, a_o)
-                if (cr) { births++; if (de[ko >> 16] + cr >= T) flags |= 4u; }              // (b_o, X_e)
+                if (cl) { births++; const uint32_t c = de[65536 + (ko & 0xFFFF)] + cl; M = max(M, c); if (c >= T) flags |= 4u; }  // (X_e, a_o)
+                if (cr) { births++; const uint32_t c = de[ko >> 16] + cr; M = max(M, c); if (c >= T) flags |= 4u; }            // (b_o, X_e)
             }
         }
     };
@@ -2925,11 +2955,15 @@ __device__ inline RoundVerdict round_valid(const RoundHead &R, const uint32_t *d
     for (uint32_t j = 1; j < (uint32_t)ROUND_MAX; j++) {
         if (j >= n) break;
         v.jend = j;
-        if (flags) { v.why = RW_FLAGS; v.flags = flags; break; }
+        const uint32_t Tj = untied ? R.cnt[j] : T;
+        if (untied ? M >= Tj : flags != 0) { v.why = RW_FLAGS; v.flags = flags; break; }
         const uint32_t tch = R.touch[j];
-        if (tch & v.mask * RT_SHARED) continue;  // decremented: no longer tied
+        if (tch & v.mask * RT_SHARED) {  // decremented: no longer tied (skipped), or no longer T_j (the end)
+            if (untied) { v.why = RW_TOUCH; break; }
+            continue;
+        }
         uint64_t jb = 0;
-        uint32_t jf = 0;
+        uint32_t jf = 0, jm = 0;
         bool jbad = false;
         if (anyj) {
 #pragma unroll
@@ -2937,32 +2971,35 @@ __device__ inline RoundVerdict round_valid(const RoundHead &R, const uint32_t *d
                 if (i >= j || !(v.mask >> i & 1u)) continue;
                 const uint32_t a1 = jn[i * RJ + j], a2 = jn[RJ_R + i * RJ + j], b1 = jn[j * RJ + i], b2 = jn[RJ_R + j * RJ + i];
                 jbad |= a1 != a2 || b1 != b2;
-                if (a1) { jb++; if (a1 >= T) jf |= 8u; }  // (X_i, X_j)
-                if (b1) { jb++; if (b1 >= T) jf |= 8u; }  // (X_j, X_i)
+                if (a1) { jb++; jm = max(jm, a1); if (a1 >= T) jf |= 8u; }  // (X_i, X_j)
+                if (b1) { jb++; jm = max(jm, b1); if (b1 >= T) jf |= 8u; }  // (X_j, X_i)
             }
         }
-        v.why = !R.walk[j]                                                ? RW_WALK
+        v.why = !(R.top[j] & RT_WALKED)                                   ? RW_WALK
                 : jbad                                                    ? RW_JUNC
-                : R.rec[j] != T                                           ? RW_REC
+                : R.rec[j] != Tj                                          ? RW_REC
                 : X0 + v.k >= x_end                                       ? RW_END
                 : (uint64_t)arena_top + (uint64_t)(j + 1) * T > rec_cap   ? RW_ARENA
                                                                           : RW_ALL;
         if (v.why != RW_ALL) break;
-        const uint64_t slack = R.ties == j + 1 ? ~0ull
-                               : (R.freeb[j] < 0 || R.freeb[0] < 0) ? 0ull
-                                                                    : (uint64_t)min(R.freeb[j], R.freeb[0]);
-        if (births >= slack) { v.why = RW_SLACK; break; }
-        const int64_t lo = (int64_t)R.live0 - (int64_t)v.k, hi = (int64_t)R.live0 + (int64_t)births - (int64_t)v.k;
-        if (lo < 1 || dev_zig_cap_for((uint64_t)lo) != C || dev_zig_cap_for((uint64_t)hi) != C ||
-            dev_zig_at_max_load(C, (uint64_t)hi)) {
-            v.why = RW_CAP;
-            break;
+        if (!untied) {  // the Zig order among the tied keys
+            const uint64_t slack = R.ties == j + 1 ? ~0ull
+                                   : (R.freeb[j] < 0 || R.freeb[0] < 0) ? 0ull
+                                                                        : (uint64_t)min(R.freeb[j], R.freeb[0]);
+            if (births >= slack) { v.why = RW_SLACK; break; }
+            const int64_t lo = (int64_t)R.live0 - (int64_t)v.k, hi = (int64_t)R.live0 + (int64_t)births - (int64_t)v.k;
+            if (lo < 1 || dev_zig_cap_for((uint64_t)lo) != C || dev_zig_cap_for((uint64_t)hi) != C ||
+                dev_zig_at_max_load(C, (uint64_t)hi)) {
+                v.why = RW_CAP;
+                break;
+            }
         }
         v.mask |= 1u << j;
         v.k++;
         bring(j);
         births += jb;
         flags |= jf;
+        M = max(M, jm);
     }
     if (v.why == RW_ALL) v.jend = n;
     return v;
@@ -3138,10 +3175,15 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     if (H.halt) return;
     const uint32_t Tc = H.top_count;
     const RoundVerdict v = round_valid(RH, left, st->rd_jn, Tc, H.cur_x, R.x_end, R.C, H.arena_top, R.rec_cap);
+    const bool untied = RH.ties0 == 1;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->rd_v = v.k;
         st->rd_mask = v.mask;
-        if (RH.n > 1) {  // (rounds with named keys: what ended them, the ending touch's kinds, the members skipped)
+        if (RH.n > 1 && untied) {  // (untied rounds: what ended them, how many, their members merged)
+            atomicAdd(&st->rd_why[RW_U + v.why], 1u);
+            atomicAdd(&st->rd_why[RW_U + RW_N], 1u);
+            atomicAdd(&st->rd_why[RW_U + RW_N + 1], v.k - 1);
+        } else if (RH.n > 1) {  // (rounds with named keys: what ended them, the ending touch's kinds, the members skipped)
             atomicAdd(&st->rd_why[v.why], 1u);
             uint32_t jm = 0;  // members merged with a junction to an earlier merged member
 #pragma unroll
@@ -3156,10 +3198,11 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     if (!(v.mask >> j & 1u)) return;
     // member j is merge X0 + (the members merged before it)
     const uint32_t X = H.cur_x + (uint32_t)__popc(v.mask & ((1u << j) - 1u)), key = RH.key[j], a = key & 0xFFFF, b = key >> 16;
+    const uint32_t Tj = j ? RH.cnt[j] : Tc;  // member j's count (below Tc in an untied round)
     if (lb < apply_blocks) {
         // X at each occurrence start, a hole at its b (one GPU: the b is always in the stream)
         const uint32_t *rec = R.rec + H.arena_top + (size_t)j * Tc;
-        const uint32_t cnt = min(j ? RH.rec[j] : H.rec_count, Tc);
+        const uint32_t cnt = min(j ? RH.rec[j] : H.rec_count, Tj);
         uint32_t made = 0;
         for (uint32_t i = lb * 256 + threadIdx.x; i < cnt; i += apply_blocks * 256) {
             const int64_t p = rec[i];
@@ -3176,15 +3219,17 @@ __global__ void __launch_bounds__(256) zbpe_replace_round(DevState *st, const ui
     }
     const uint32_t ublk = lb - apply_blocks;
     const uint32_t *tj = lj + 2 * 65536;
-    if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tc && a != b) occ_check_failed(st, X, tj[1], Tc, key);
+    if (ublk == 0 && threadIdx.x == 0 && tj[1] != Tj && a != b) occ_check_failed(st, X, tj[1], Tj, key);
     const uint32_t nch = update_chunks(Xp, per);
-    if (ublk < 4 * nch && (RH.top[j] & 16u)) {  // (member j's walk counted junctions)
+    if (ublk < 4 * nch && (RH.top[j] & RT_JUNCTION)) {  // (member j's walk counted junctions)
         const uint32_t g = ublk / nch;
         round_junction_adjust(dv, g, (ublk - g * nch) * UPD_THREADS * per, per, j, v.mask, min(RH.n, (uint32_t)ROUND_MAX),
                               &RH.key[0], st->rd_jn, H.cur_x);
     }
     const RoundCtx rc{left, j, &st->rd.key[0], &st->rd.dec[0], v.mask, st->rd_jn, min(RH.n, (uint32_t)ROUND_MAX)};
-    update_block(T, st, lj, lj + 65536, tj, a, b, X, key, ublk, per, dv, H.theta, 0, Tc, NO_ID, NO_ID, NO_ID, NO_ID, &rc, Xp);
+    // (the tie counts' credit: pairs tied at the round's start, the top count -- none besides member 0 in an untied round)
+    update_block(T, st, lj, lj + 65536, tj, a, b, X, key, ublk, per, dv, H.theta, 0, untied ? 0xFFFFFFFFu : Tc, NO_ID, NO_ID, NO_ID,
+                 NO_ID, &rc, Xp);
 }
 
 // this shard's boundary record: first 3 / last 2 live tokens (holes skipped) and its live count
@@ -4496,6 +4541,8 @@ struct PlanCtx {
     const uint32_t *lst_off, *lst_len, *dir_row, *dir;
     uint32_t dir_w, lists_x, xn, xoff, xlen, xnum = 1;
     uint32_t xmask = 0;  // (a round that skipped members: token xn + i is member m_i, the i-th set bit; list at xoff + m_i * xlen)
+    // (a round: member m >= 1's list is xcnt[m] long -- RoundHead::cnt, in LDS -- its count, below xlen in an untied round)
+    const uint32_t *xcnt = nullptr;
 };
 // the member of a round's i-th merge (the i-th set bit of the mask; the identity without one)
 __device__ inline uint32_t round_member(uint32_t mask, uint32_t i) {
@@ -4520,8 +4567,16 @@ __device__ inline void plan_compute(const PlanCtx &P, uint32_t key, uint32_t *ou
         r0 = P.dir[rb];
         r1 = P.dir[rb + 1];
     }
-    if (a - P.xn < P.xnum) { la = P.xlen; oa = P.xoff + round_member(P.xmask, a - P.xn) * P.xlen; }
-    if (b - P.xn < P.xnum) { lb = P.xlen; ob = P.xoff + round_member(P.xmask, b - P.xn) * P.xlen; }
+    if (a - P.xn < P.xnum) {
+        const uint32_t m = round_member(P.xmask, a - P.xn);
+        la = P.xcnt && m ? P.xcnt[m] : P.xlen;
+        oa = P.xoff + m * P.xlen;
+    }
+    if (b - P.xn < P.xnum) {
+        const uint32_t m = round_member(P.xmask, b - P.xn);
+        lb = P.xcnt && m ? P.xcnt[m] : P.xlen;
+        ob = P.xoff + m * P.xlen;
+    }
     out[0] = la; out[1] = lb; out[2] = oa; out[3] = ob; out[4] = r0; out[5] = r1;
 }
 // the plan of merge x1 = key (after the state's cur_key for it is stored; the next kernel boundary orders both)
@@ -4874,28 +4929,32 @@ __global__ void __launch_bounds__(DECIDE_THREADS) zbpe_tie_decide(DevState *st, 
 // fits one dispatch round.
 // ------------------------------------------------------------------------------------------
 // The roll of a multi-merge round (the last argmax workgroup's thread 0, after select_finish without its roll):
-// every member's records become its new token's list (member j's at arena_top + j T, T of them), the stream and
-// arena counters advance by all of them, the members' merge-log rows get their pairs, counts, live tokens and
-// tie counts (member j's tied set is member j-1's less member j-1 and the tied pairs member j-1 decremented
-// first, RoundHead::dec), and the round's words are cleared for the next round's scan.
+// every member's records become its new token's list (member j's at arena_top + j T, cnt[j] of them), the stream
+// and arena counters advance by all of them, the members' merge-log rows get their pairs, counts, live tokens
+// and tie counts (tied: member j's tied set is member j-1's less member j-1 and the tied pairs member j-1
+// decremented first, RoundHead::dec; untied: 1), and the round's words are cleared for the next round's scan.
 __device__ inline void round_roll(const Tables &T, DevState *st, const StateHead &H0, MergeLog *log, const uint32_t *pre,
                                   FinishOut *fo, uint32_t *rlog) {
     const uint32_t k = H0.rd_v, X0 = H0.cur_x, Tc = H0.top_count, mask = H0.rd_mask;
     RoundHead &R = st->rd;
     // the RoundHead words, preloaded into LDS at the kernel's entry (roll_preload rd)
     const RoundHead &RP = *reinterpret_cast<const RoundHead *>(pre + RI_WORDS);
-    uint32_t rec[ROUND_MAX], key[ROUND_MAX], dec[ROUND_MAX];
+    uint32_t rec[ROUND_MAX], key[ROUND_MAX], dec[ROUND_MAX], cnt[ROUND_MAX];
 #pragma unroll
     for (int j = 0; j < ROUND_MAX; j++) {
         rec[j] = RP.rec[j];
         key[j] = RP.key[j];
         dec[j] = RP.dec[j];
+        cnt[j] = RP.cnt[j];
     }
     rec[0] = pre[RI_REC];
+    cnt[0] = Tc;
+    const bool untied = RP.ties0 == 1;
     const uint32_t holes = pre[RI_HOLES], arena_top = pre[RI_ARENA_TOP], arena_rep = pre[RI_ARENA_REP], total_occ = pre[RI_TOTAL_OCC];
     const long long live_tokens = (long long)(((uint64_t)pre[RI_LIVE_TOK_HI] << 32) | pre[RI_LIVE_TOK_LO]);
     // merge X0 + x is member m (the x-th set bit of mask); member m's records are at arena_top + m Tc
     uint32_t ties = RP.ties0, sum = 0, x = 0, prev = 0, last = 0;
+    long long gone = 0;  // tokens the merged members before this one removed (one per occurrence)
 #pragma unroll
     for (uint32_t m = 0; m < (uint32_t)ROUND_MAX; m++) {
         if (!(mask >> m & 1u)) continue;
@@ -4904,9 +4963,10 @@ __device__ inline void round_roll(const Tables &T, DevState *st, const StateHead
             T.lst_len[X0 + x] = rec[m];
         }
         if (x) {  // (the whole row: d_log is not cleared between trains)
-            ties = ties - 1u - dec[prev];
-            log[X0 + x - 256] = MergeLog{key[m], Tc, (uint32_t)(live_tokens - (long long)x * Tc), ties, 1u, rec[m], 0u, 0u};
+            ties = untied ? 1u : ties - 1u - dec[prev];
+            log[X0 + x - 256] = MergeLog{key[m], cnt[m], (uint32_t)(live_tokens - gone), ties, 1u, rec[m], 0u, 0u};
         }
+        gone += cnt[m];
         sum += rec[m];
         prev = last = m;
         x++;
@@ -4925,11 +4985,11 @@ __device__ inline void round_roll(const Tables &T, DevState *st, const StateHead
     st->rec_count = 0;
 #pragma unroll
     for (int j = 0; j < ROUND_MAX; j++) {
-        R.walk[j] = 0; R.touch[j] = 0; R.top[j] = 0; R.birth[j] = 0; R.rec[j] = 0; R.dec[j] = 0;
+        R.touch[j] = 0; R.top[j] = 0; R.birth[j] = 0; R.rec[j] = 0; R.dec[j] = 0; R.nmax[j] = 0;
     }
     uint32_t anyj = 0;
 #pragma unroll
-    for (int j = 0; j < ROUND_MAX; j++) anyj |= RP.top[j] & 16u;
+    for (int j = 0; j < ROUND_MAX; j++) anyj |= RP.top[j] & RT_JUNCTION;
     if (anyj) {
         uint4 *jw = reinterpret_cast<uint4 *>(&st->rd_jn[0]);
 #pragma unroll
@@ -4986,6 +5046,7 @@ struct NextArgs {
     int round;
     uint32_t par, seq, rlog_i;
     uint32_t *rlog;
+    int untied;           // option round_untied: a round's select that begins an untied merge names the next distinct counts' pairs
 };
 // every thread of the block calls it after its last global store of the phase; true in the last block.
 // Every byte the last block reads from another workgroup was stored write-through (sc1: agent-scope
@@ -5368,7 +5429,8 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     __shared__ uint32_t s_plan[6];
     // (X's list: the roll's lst_off / lst_len, from the same words; a round's members: T records each)
     const PlanCtx plan = N.round && H0.rd_v ? PlanCtx{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, H0.cur_x, H0.arena_top,
-                                                      H0.top_count, H0.rd_v, H0.rd_mask}
+                                                      H0.top_count, H0.rd_v, H0.rd_mask,
+                                                      s_pre + RI_WORDS + offsetof(RoundHead, cnt) / 4}
                                             : PlanCtx{T.lst_off, T.lst_len, N.dir_row, N.dir, N.dir_w, H0.lists_x, X, H0.arena_top,
                                                       H0.rec_count, 1u};
     const bool plan_on = N.plan && T.lst_off && H0.lists_valid;
@@ -5384,6 +5446,52 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     if (N.prof && tid == 0 && !light) sel_tick(st, 1, &pt);
+    // ---- untied rounds (N.untied): merge X+1 has the unique top count T_0. Waves 2..7, beside thread 0's roll and
+    // begin, find the next ROUND_MAX - 1 distinct counts below it among the hot entries (every pair with a count
+    // >= theta is listed), each with how many entries hold it and one of their keys: per wave, then (below) merged
+    // by wave 2. A distinct count held by one pair names it as the next round member (UntiedHead).
+    constexpr uint32_t UR_U = 16;  // hot entries per thread (the pass covers hot lists of up to 384 * UR_U ids)
+    constexpr uint32_t UR_L = ROUND_MAX - 1;
+    __shared__ uint32_t s_uw[6 * UR_L * 3];
+    const bool ur_on = N.round && N.untied && !light && Q.ties == 1 && Q.cnt && NB.X + 1 < N.x_end &&
+                       min(H0.hot_len, T.hot_cap) <= 384u * UR_U;
+    if (ur_on && tid >= 128) {
+        const uint32_t w = (tid >> 6) - 2, t = tid - 128, lane = tid & 63;
+        const uint32_t nh = min(H0.hot_len, T.hot_cap), theta = H0.theta;
+        const uint32_t *hk = reinterpret_cast<const uint32_t *>(hot);  // (a hot entry's upper word: its key)
+        uint32_t c[UR_U], k[UR_U];
+#pragma unroll
+        for (uint32_t u = 0; u < UR_U; u++) {
+            const uint32_t i = t + u * 384u;
+            c[u] = i < nh ? hcnt[i] : 0u;
+            k[u] = i < nh ? hk[2 * i + 1] : NO_ID;
+        }
+        uint32_t Lp = Q.cnt;
+#pragma unroll
+        for (uint32_t l = 0; l < UR_L; l++) {
+            uint32_t L = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < UR_U; u++) L = c[u] < Lp && c[u] >= theta && c[u] > L ? c[u] : L;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) L = max(L, (uint32_t)__shfl_xor((int)L, off));
+            uint32_t m = 0, kk = NO_ID;
+#pragma unroll
+            for (uint32_t u = 0; u < UR_U; u++) {
+                const bool eq = L && c[u] == L;
+                m += eq ? 1u : 0u;
+                kk = eq ? k[u] : kk;
+            }
+            const uint64_t has = __ballot(m != 0);
+            kk = has ? (uint32_t)__shfl((int)kk, __ffsll((unsigned long long)has) - 1) : NO_ID;
+            m = wave_sum(m);
+            if (lane == 0) {
+                s_uw[(w * UR_L + l) * 3 + 0] = L;
+                s_uw[(w * UR_L + l) * 3 + 1] = m;
+                s_uw[(w * UR_L + l) * 3 + 2] = kk;
+            }
+            Lp = L;
+        }
+    }
     if (tid == 0) {
         FinishOut fo;
         const bool rnd = N.round && H0.rd_v;
@@ -5454,6 +5562,37 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     };
     if (s_h || !s_tie) {
         if (plan_on && tid == 64 && !s_h && (light || (Q.ties == 1 && Q.cnt))) plan_store(st, NB.X, s_key[0], N.gen, s_plan);
+        if (ur_on && !s_h && tid >= 128 && tid < 192) {  // wave 2: the waves' counts merged, the round's names stored
+            const uint32_t lane = tid - 128;
+            const bool rec = lane < 6 * UR_L;
+            const uint32_t L = rec ? s_uw[lane * 3] : 0u, M = rec ? s_uw[lane * 3 + 1] : 0u, K = rec ? s_uw[lane * 3 + 2] : NO_ID;
+            uint32_t Lp = Q.cnt, nu = 0, uk[UR_L], uc[UR_L];
+            bool go = true;
+#pragma unroll
+            for (uint32_t l = 0; l < UR_L; l++) {
+                uk[l] = NO_ID;
+                uc[l] = 0;
+                if (!go) continue;
+                uint32_t Lk = L < Lp ? L : 0u;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) Lk = max(Lk, (uint32_t)__shfl_xor((int)Lk, off));
+                const uint32_t msum = wave_sum(Lk && L == Lk ? M : 0u);
+                const uint64_t has = __ballot(Lk && L == Lk);
+                const uint32_t key = has ? (uint32_t)__shfl((int)K, __ffsll((unsigned long long)has) - 1) : NO_ID;
+                // (a count held by several pairs is a tie: the Zig order decides it, so the names end; so does a self pair)
+                go = Lk && msum == 1 && key != NO_ID && (key & 0xFFFF) != (key >> 16);
+                if (go) { uk[l] = key; uc[l] = Lk; nu++; }
+                Lp = Lk;
+            }
+            if (lane == 0) {
+                UntiedHead u;
+                u.x = NB.X;
+                u.n = nu;
+#pragma unroll
+                for (uint32_t l = 0; l < UR_L; l++) { u.key[l] = uk[l]; u.cnt[l] = uc[l]; }
+                st->ur = u;
+            }
+        }
         if (N.prof && tid == 0) {
             const unsigned long long now = wall_clock64();
             st->pp_t[7] = now;

@@ -22,30 +22,47 @@ constexpr int PRES_GROUP = 32;       // presence blocks per bitmap word
 
 __host__ __device__ constexpr inline uint32_t pair_key(uint32_t first, uint32_t second) { return first | (second << 16); }
 
-// Multi-merge rounds (option round_k). A tied merge's decision names the tied keys by
-// home slot order (DevState::pr_key .. pr_key4); a round applies the merge and up to ROUND_MAX - 1 of those
-// keys in one scan, one replace and one select launch. The round's scan walks every member's occurrences
-// (member j -> merge cur_x + j, new token cur_x + j) into its own delta buffer and records; the replace
-// applies the longest prefix of members that the reference's loop would merge next, one after the other
-// (each member j >= 1: still tied and first in Zig slot order, no occurrence touching an earlier member's);
-// the select rolls them all and starts the merge after the round.
+// Multi-merge rounds (option round_k). A round applies a merge and up to ROUND_MAX - 1
+// named keys in one scan, one replace and one select launch. The keys are named two ways:
+//   - tied rounds: a tied merge's decision names the next tied keys by home slot order (DevState::pr_key ..
+//     pr_key4); member j >= 1 merges when it is still tied and first in Zig slot order;
+//   - untied rounds (option round_untied): the select that begins an untied merge (its count T_0 unique) names
+//     the pairs of the next distinct counts T_1 > T_2 > .. below it, each held by one pair (DevState::ur);
+//     member j merges when no merged member decremented it and no pair a merged member made reaches T_j (then
+//     it holds the unique top count, as the reference's loop would see it).
+// The round's scan walks every member's occurrences (member j -> merge cur_x + j, new token cur_x + j) into
+// its own delta buffer and records; the replace applies the longest valid prefix of members, one after the
+// other, with no occurrence touching an earlier member's; the select rolls them all and starts the merge after
+// the round.
 constexpr int ROUND_MAX = 5;
+// RoundHead::top bits (member j's walk)
+constexpr uint32_t RT_XX = 2u;        // adjacent occurrences: (X, X) is new, (b, a) falls
+constexpr uint32_t RT_JUNCTION = 16u; // the walk counted junction sides (DevState::rd_jn)
+constexpr uint32_t RT_WALKED = 32u;   // member j >= 1 walked by a list form (a stream scan is never a member)
 struct RoundHead {
     uint32_t n;                  // members the scan took (1 .. ROUND_MAX; written by its block 0)
-    uint32_t ties;               // tied keys at the decision that named them (pr_ties)
+    uint32_t ties;               // tied keys at the decision that named them (pr_ties; 0: an untied round)
     int32_t live0;               // live pairs at the round's start (DevState::live as the scan saw it)
-    uint32_t ties0;              // merge cur_x's tied pairs (DevState::tie_count as the scan saw it)
+    uint32_t ties0;              // merge cur_x's tied pairs (DevState::tie_count as the scan saw it; 1: untied round)
     uint32_t key[ROUND_MAX];     // member keys (key[0] = cur_key)
-    uint32_t walk[ROUND_MAX];    // member j >= 1 walked by a list form (a stream scan is never a member)
     uint32_t touch[ROUND_MAX];   // an occurrence of member j touches one of an earlier member's
-    uint32_t top[ROUND_MAX];     // bit 0: a new pair of member j has the top count; bit 1: adjacent occurrences
+    uint32_t top[ROUND_MAX];     // RT_XX | RT_JUNCTION | RT_WALKED
     uint32_t birth[ROUND_MAX];   // new pairs of member j: its distinct neighbour tokens
     uint32_t rec[ROUND_MAX];     // records of member j >= 1 (member 0's: DevState::rec_count)
-    int32_t freeb[ROUND_MAX];    // free Zig-map slots: [0] after the largest tied home's block, [j] after member j's
-                                 // home block and before the next tied home (j >= 1); -1: no bound
+    int32_t freeb[ROUND_MAX];    // tied rounds: free Zig-map slots: [0] after the largest tied home's block, [j] after
+                                 // member j's home block and before the next tied home (j >= 1); -1: no bound
     uint32_t dec[ROUND_MAX];     // tied pairs member j decremented first (the replace), for the tie counts
+    uint32_t nmax[ROUND_MAX];    // the largest count a new pair of member j's neighbour deltas reaches
+    uint32_t cnt[ROUND_MAX];     // member j's count: the top count (tied), the j-th distinct count (untied)
 };
-static_assert(sizeof(RoundHead) == 4 * (4 + 8 * ROUND_MAX), "round head: packed words");
+static_assert(sizeof(RoundHead) == 4 * (4 + 9 * ROUND_MAX), "round head: packed words");
+// Untied rounds: the select that began untied merge x named the pairs of the next n distinct counts (each the
+// only pair with its count, at least the hot list's threshold, not a self pair), in count order
+struct UntiedHead {
+    uint32_t x, n;
+    uint32_t key[ROUND_MAX - 1], cnt[ROUND_MAX - 1];
+};
+static_assert(sizeof(UntiedHead) == 4 * (2 + 2 * (ROUND_MAX - 1)), "untied head: packed words");
 struct RoundPlans {
     uint32_t key[ROUND_MAX - 1];
     uint32_t gen;
@@ -150,11 +167,12 @@ struct DevState {
     // rounds applied beyond their first members
     alignas(128) RoundHead rd;
     uint32_t rd_merges;
-    uint32_t rd_why[16];     // rounds that walked named keys, by what ended them (RoundWhy, kernels.hpp)
+    uint32_t rd_why[32];     // rounds that walked named keys, by what ended them (RoundWhy, kernels.hpp; untied from RW_U)
     alignas(16) uint32_t rd_jn[64];  // the round's junction counts (kernels.hpp RJ, RJ_R), cleared by the roll
     // the named keys' scan plans (ScanArgs::pl), by a spare wave of the naming decision (zbpe_select_next, round
     // mode), valid for layout generation rp.gen: a member walk then starts without loading its lists' words
     alignas(16) RoundPlans rp;
+    alignas(64) UntiedHead ur;  // untied rounds' named keys (zbpe_select_next, read by the next round's scan)
     uint32_t err_key, err_mode;  // (error 64: the pair, and its scan's form -- scan_mode)
     uint32_t last_light, err_light;  // the last merge a pair select started; (error 64: was the merge one)
     uint32_t err4_key, err4_site;  // (error 4: the first missing pair and where: 1 pair_dec, 2 merged pair, 3 update, 4 first occurrences)
