@@ -1216,7 +1216,7 @@ __device__ inline bool plan_is_list(const ScanArgs &A, const StateHead &H) {
 }
 // ------------------------------------------------------------------------------------------
 // Multi-merge rounds (option round_k; RoundHead, types.hpp). The scan of a round: the merge (member 0,
-// cur_key) and the tied keys its decision named in home-slot order (pr_key .. pr_key4: members 1..4 for
+// cur_key) and the tied keys its decision named in home-slot order (DevState::ph key, pr_key2 .. pr_key4: members 1..4 for
 // merges cur_x + 1 ..), each walked by its own share of the grid into its own delta buffer (fixed
 // layout: left at +0, right at +65536, tail at +131072) and records (arena_top + j * T: every member has
 // the top count T of occurrences). Member walks also test every occurrence against the earlier members'
@@ -1265,7 +1265,7 @@ __device__ __attribute__((always_inline)) inline void round_scan(const ScanArgs 
     const unsigned long long t_in = PROF ? wall_clock64() : 0ull;
     const uint32_t X0 = H.cur_x, T = H.top_count, G = gridDim.x - RD_FREE_WGS;
     ScanArgs A = scan_args_resolve(A0, H, X0);
-    // the members: merge X0 and the keys its decision named (pr_x == X0 + 1: a tied round), or the keys of the next
+    // the members: merge X0 and the keys its decision named (its candidate slot names X0 + 1: a tied round), or the keys of the next
     // distinct counts the select that began X0 named (ur.x == X0: an untied round), while every one is a list walk
     // with room in the arena and below the vocabulary's end
     const bool tied = P.x == X0 + 1 && pr_full == X0 + 1, untied = !tied && U.x == X0 && U.n > 0;
@@ -1400,12 +1400,15 @@ __global__ void __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_
     UntiedHead U{};
     uint32_t pr_full = 0;
     if (ROUND) {
-        P = *reinterpret_cast<const PairHead *>(&stp->pr_x);
+        // (both candidate slots, in the head's round trip: the round's merge picks its successor's, DevState::ph)
+        const PairHead Pa = stp->ph[0], Pb = stp->ph[1];
+        asm volatile("" ::"s"(Pa.x), "s"(Pa.key), "s"(Pa.ties), "s"(Pb.x), "s"(Pb.key), "s"(Pb.ties));
+        P = (H.cur_x + 1) & 1 ? Pb : Pa;
         PT = *reinterpret_cast<const PairTail *>(&stp->pr_plan[0]);
         RPL = stp->rp;
         U = stp->ur;
         pr_full = stp->pr_full;
-        asm volatile("" ::"s"(P.x), "s"(P.key), "s"(P.ties), "s"(PT.key2), "s"(PT.key3), "s"(PT.key4), "s"(PT.h2), "s"(PT.h3),
+        asm volatile("" ::"s"(PT.key2), "s"(PT.key3), "s"(PT.key4), "s"(PT.h2), "s"(PT.h3),
                      "s"(PT.h4), "s"(PT.h5), "s"(PT.h6), "s"(PT.hmax), "s"(pr_full), "s"(RPL.gen), "s"(RPL.key[0]),
                      "s"(RPL.key[1]), "s"(RPL.key[2]), "s"(RPL.key[3]));
         asm volatile("" ::"s"(U.x), "s"(U.n), "s"(U.key[0]), "s"(U.key[1]), "s"(U.key[2]), "s"(U.key[3]), "s"(U.cnt[0]),
@@ -2688,11 +2691,11 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                                     const uint32_t (&dv)[UPD_MAX_PER], uint32_t theta, int prof = 0,
                                     uint32_t top_count = 0, uint32_t pr_key = NO_ID, uint32_t pr_key2 = NO_ID,
                                     uint32_t pr_key3 = NO_ID, uint32_t pr_key4 = NO_ID, const RoundCtx *rc = nullptr,
-                                    uint32_t Xc = 0) {
+                                    uint32_t Xc = 0, PairHead *ph = nullptr) {
     // Xc: the bound the blocks' groups and ranges were laid out for (update_preload's X; 0: X itself -- a round's
     // replace lays them out for the batch's bound on every member's X)
-    // pr_key != NO_ID: merge X+1 has a pair-select candidate (DevState::pr_key): count the new pairs, the
-    // tied pairs decremented (old count == top_count) and flag what rules the candidate out
+    // pr_key != NO_ID: merge X+1 has a pair-select candidate (ph: its slot DevState::ph[(X + 1) & 1]): count the new
+    // pairs, the tied pairs decremented (old count == top_count) and flag what rules the candidate out
     // option sel_prof: the latest stamp of each phase over the update blocks (st->pp_t[8..11])
     const auto stamp = [&](int k) {
         if (prof && threadIdx.x == 0) atomicMax(&st->pp_t[k], (unsigned long long)wall_clock64());
@@ -2711,7 +2714,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
             const uint32_t old = pair_dec(T, st, pair_key(b, a), xx);
             if (rc && old == top_count) round_credit(*rc, pair_key(b, a));
         }
-        if (tid == 0 && xx && pr_key != NO_ID) atomicOr(&st->pr_dt, 1u << 18);
+        if (tid == 0 && xx && pr_key != NO_ID) atomicOr(&ph->dt, 1u << 18);
         if (tid == 1 && xx) pair_new(T, st, pair_key(X, X), xx);
         if (tid == 2) {
             const uint32_t occ = tail[1];
@@ -2779,7 +2782,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
             if (nh) hb = atomicAdd(&st->hot_len, nh);
             s_base = atomicAdd(&st->num_ids, n);
             atomicAdd(&st->live, (int)n);
-            if (pr_key != NO_ID) atomicAdd(&st->pr_births, n);
+            if (pr_key != NO_ID) atomicAdd(&ph->births, n);
             s_hbase = hb;
         }
         __syncthreads();
@@ -2807,7 +2810,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
                 // pair's lone trailing a decrements the merged pair itself, which is no other tied pair)
                 if (rc && old == top_count && key != top_key) round_credit(*rc, key);
                 if (pr_key != NO_ID && old == top_count && key != top_key)
-                    atomicAdd(&st->pr_dt, key == pr_key    ? 0x10001u
+                    atomicAdd(&ph->dt, key == pr_key    ? 0x10001u
                                           : key == pr_key2 ? 0x80001u
                                           : key == pr_key3 ? 0x100001u
                                           : key == pr_key4 ? 0x200001u
@@ -2816,7 +2819,7 @@ __device__ inline void update_block(const Tables &T, DevState *st, const uint32_
         } else {
             const uint32_t id = s_base + i;
             const uint32_t key = g == 1 ? pair_key(t, X) : pair_key(X, t);
-            if (pr_key != NO_ID && c >= top_count) atomicOr(&st->pr_dt, 1u << 17);
+            if (pr_key != NO_ID && c >= top_count) atomicOr(&ph->dt, 1u << 17);
             if (id >= T.id_cap) atomicOr(&st->error, 1u);
             else {
                 T.id_key[id] = key;
@@ -3060,7 +3063,8 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     const uint32_t per = update_per(Xp);
     if (blockIdx.x >= apply_blocks) update_preload(left, left + Xp, Xp, blockIdx.x - apply_blocks, per, dv);
     const StateHead H = load_head(st);  // (with the deltas: one round trip)
-    const uint32_t pr_x = st->pr_x, pr_key0 = st->pr_key, pr_key2 = st->pr_key2, pr_key3 = st->pr_key3, pr_key4 = st->pr_key4;
+    PairHead *ph = &st->ph[(R.X + 1) & 1];  // (merge X+1's candidate slot)
+    const uint32_t pr_x = ph->x, pr_key0 = ph->key, pr_key2 = st->pr_key2, pr_key3 = st->pr_key3, pr_key4 = st->pr_key4;
     const uint32_t theta = H.theta;
     if (R.prof && blockIdx.x == 0 && threadIdx.x == 0) {  // fold the list scan's stamps
         const unsigned long long now = wall_clock64();
@@ -3136,7 +3140,7 @@ __global__ void __launch_bounds__(256) zbpe_replace(DevState *st, const uint32_t
     if (R.dyn && ublk == 0 && threadIdx.x == 0 && R.tail[1] != H.top_count && R.a != R.b)
         occ_check_failed(st, R.X, R.tail[1], H.top_count, R.top_key);
     update_block(T, st, R.left, R.right, R.tail, R.a, R.b, R.X, R.top_key, ublk, per, dv, theta, R.prof, H.top_count,
-                 R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2, pr_key3, pr_key4);
+                 R.dyn && pr_x == R.X + 1 ? pr_key0 : NO_ID, pr_key2, pr_key3, pr_key4, nullptr, 0, ph);
     if (R.prof) {
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(&st->pp_t[6], (unsigned long long)wall_clock64());
@@ -4705,7 +4709,8 @@ __device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Su
                                         uint32_t dir_w, uint32_t lists_x, bool plan_on, uint32_t gen) {
     const HomeView V{nullptr, summ, sup, C, nb, nsb};
     __shared__ int64_t s_r[4];
-    const uint32_t px = st->pr_x, slack = st->pr_slack, h2 = st->pr_h2, h3 = st->pr_h3, hmax = st->pr_hmax, key = st->pr_key;
+    PairHead &ph = st->ph[(X + 1) & 1];  // merge X+1's candidate
+    const uint32_t px = ph.x, slack = ph.slack, h2 = st->pr_h2, h3 = st->pr_h3, hmax = st->pr_hmax, key = ph.key;
     if (px != X + 1) return;
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // the candidate's scan plan (its tokens existed before merge X: their lists are the ones the scan of
@@ -4715,7 +4720,7 @@ __device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Su
         uint32_t pl[6];
         plan_compute(plan, key, pl);
         for (int k = 0; k < 6; k++) st->pr_plan[k] = pl[k];
-        st->pr_plan_gen = gen;
+        ph.plan_gen = gen;
     }
     if (slack != 0 || !cs || V.C < (uint32_t)(SUMM_SLOTS * SUPER_BLOCKS)) return;
     const uint32_t x23 = (h2 / SUMM_SLOTS + 1) * SUMM_SLOTS, xe = (hmax / SUMM_SLOTS + 1) * SUMM_SLOTS;
@@ -4730,7 +4735,7 @@ __device__ inline void pair_slack_block(DevState *st, const Summ *summ, const Su
     const int64_t f23 = x23 < h3 ? (int64_t)h3 - x23 - s_r[1] - s_r[0] : 0;
     const int64_t fe = xe < V.C ? (int64_t)V.C - xe - s_r[3] - s_r[2] : 0;
     const int64_t f = min(f23, fe);
-    st->pr_slack = f <= 0 ? 0u : (uint32_t)min(f, (int64_t)0xFFFFFFFEll);
+    ph.slack = f <= 0 ? 0u : (uint32_t)min(f, (int64_t)0xFFFFFFFEll);
 }
 __device__ inline void min2_combine(uint64_t &m1, uint64_t &m2, uint64_t b1, uint64_t b2) {
     const uint64_t a1 = m1, a2 = m2;
@@ -4868,7 +4873,8 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                 (len == 2 || V.C >= (uint32_t)(SUMM_SLOTS * SUPER_BLOCKS))) {
                 // two tied pairs: the candidate is the only one left (no bound needed); else 0 until merge
                 // X's replace has bounded the free slots (pair_slack_block)
-                st->pr_slack = len == 2 ? 0xFFFFFFFFu : 0u;
+                PairHead &ph = st->ph[pair_x & 1];  // (merge pair_x's slot: not the one this launch's light test read)
+                ph.slack = len == 2 ? 0xFFFFFFFFu : 0u;
                 st->pr_h2 = (uint32_t)(m2 >> 32);
                 st->pr_h3 = len >= 3 ? (uint32_t)(s_m3 >> 32) : 0u;
                 st->pr_h4 = len >= 4 && s_m4 != ~0ull ? (uint32_t)(s_m4 >> 32) : 0u;
@@ -4888,12 +4894,12 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                 const uint32_t k5 = (uint32_t)s_m5;
                 st->pr_key4 = c3 && chain3 && len >= 5 && s_m5 != ~0ull && (k5 & 0xFFFF) != (k5 >> 16) && (len == 5 || s_m6 != ~0ull)
                                   ? k5 : NO_ID;
-                st->pr_plan_gen = 0xFFFFFFFFu;  // (the replace's extra workgroup loads the plan)
-                st->pr_births = 0;
-                st->pr_dt = 0;
-                st->pr_key = k2;
-                st->pr_ties = total;
-                st->pr_x = pair_x;
+                ph.plan_gen = 0xFFFFFFFFu;  // (the replace's extra workgroup loads the plan)
+                ph.births = 0;
+                ph.dt = 0;
+                ph.key = k2;
+                ph.ties = total;
+                ph.x = pair_x;
                 st->pr_full = pair_x;
             }
         }
@@ -5057,7 +5063,11 @@ struct NextArgs {
 // workgroup whose add came last loads after its add has returned, its other waves after a barrier)
 // pair selects: does this launch start merge X+1 with the candidate (the conditions at the light path in
 // zbpe_select_next)? Both roles evaluate it on the same words: the refresh workgroups then leave the dirty
-// home blocks to the next launch, whose decision reads them
+// home blocks to the next launch, whose decision reads them.
+// Invariant (single-sourced verdict): every workgroup of the launch evaluates it on merge X+1's PairHead slot
+// (DevState::ph[x1 & 1]) and DevState::live, and no kernel writes either while the launch runs -- the committing
+// block writes the chain and a decision's candidate into merge X+2's slot, and the select writes no pair count --
+// so a workgroup that starts after the committing block has moved on to merge X+2 still gets the launch's verdict.
 // (scalar arguments: a reference to the kernel's NextArgs made the compiler copy all of it to scratch at entry)
 __device__ inline bool pair_light(int pair, uint32_t x1, uint32_t x_end, uint32_t C, const PairHead &P0, int32_t live0) {
     if (!pair || P0.x != x1 || x1 >= x_end) return false;
@@ -5142,7 +5152,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
             for (uint32_t t = blockIdx.x * NEXT_THREADS + tid; t < 2 * X; t += nref * NEXT_THREADS) delta[t] = 0;
         }
         if (N.pair && N.skip_refresh && !N.round) {  // a pair select: no decision in this launch reads the summaries
-            const PairHead P0 = *reinterpret_cast<const PairHead *>(&st->pr_x);
+            const PairHead P0 = st->ph[N.B.X & 1];  // (merge X+1's slot: no workgroup of this launch writes it)
             if (pair_light(N.pair, N.B.X, N.x_end, N.V.C, P0, st->live)) return;
         }
         // nref may be below the super-block count (option refresh_wgs): a smaller grid ends sooner -- a kernel
@@ -5201,7 +5211,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     PairHead P0{};
     int32_t live0 = 0;
     if (N.pair) {
-        P0 = *reinterpret_cast<const PairHead *>(&st->pr_x);
+        P0 = st->ph[N.B.X & 1];  // (merge X+1's slot: no workgroup of this launch writes it, DevState::ph)
         live0 = st->live;
     }
     if (H0.halt) return;
@@ -5241,9 +5251,9 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
     // the candidate's words wait in LDS (kept in registers across the argmax and decision code, they pushed
     // the kernel's scalar registers into spills)
     __shared__ uint32_t s_p0[5];
-    enum { P0_KEY, P0_TIES, P0_DT, P0_HITS, P0_PGEN };
+    enum { P0_KEY, P0_TIES, P0_DT, P0_BIRTHS, P0_PGEN };
     if (light && tid == 0) {
-        s_p0[P0_KEY] = P0.key; s_p0[P0_TIES] = P0.ties; s_p0[P0_DT] = P0.dt; s_p0[P0_HITS] = P0.hits; s_p0[P0_PGEN] = P0.plan_gen;
+        s_p0[P0_KEY] = P0.key; s_p0[P0_TIES] = P0.ties; s_p0[P0_DT] = P0.dt; s_p0[P0_BIRTHS] = P0.births; s_p0[P0_PGEN] = P0.plan_gen;
     }
     // one argmax workgroup (a short hot list): it is the last one by construction -- no ticket, no
     // partials through global memory
@@ -5359,10 +5369,11 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
         }
     }
     if (N.prof && tid == 0) atomicMax(&st->sel_ta, (unsigned long long)wall_clock64());
-    // (the ticket is the launch parity's, zeroed by the launch before: a pair select's other argmax workgroups
-    // that start late see the state words block 0 has already rewritten for the next merge, take the full path
-    // and arrive on it, and no one waits -- a shared ticket then elected a later launch's last block early, which
-    // reduced stale partials)
+    // (the ticket is the launch parity's, zeroed by the launch before. Round 5 found argmax workgroups of a pair
+    // select that started late, saw the candidate words block 0 had already rewritten for the next merge, took the
+    // full path and arrived on a shared ticket, which then elected a later launch's last block early; the verdict's
+    // words now live in a slot this launch never writes (pair_light), and the per-launch ticket stays as a second
+    // guard: arrivals of a launch never count for another)
     if (!single && !block_ticket_last(N.rtk + (N.round ? N.par : X & 1) * RTK_SET + 9 * RTK_STRIDE, sel_blocks, &s_flag)) return;
     if (N.round) {  // roll_preload's LDS words (wave 0) landed (a single argmax block took no ticket)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -5520,25 +5531,28 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 // still the decision's (this launch refreshed none)
                 const PairTail &PT = *reinterpret_cast<const PairTail *>(&st->pr_plan[0]);
                 const uint32_t key2 = PT.key2, key3 = PT.key3, key4 = PT.key4, h3 = PT.h3, h4 = PT.h4, h5 = PT.h5, h6 = PT.h6;
+                // (merge X+2's slot: the other one than this launch's workgroups read at entry, DevState::ph)
+                PairHead &pn = st->ph[(N.B.X + 1) & 1];
                 if (!h && N.skip_refresh && key2 != NO_ID && N.B.X + 1 < N.x_end) {
-                    st->pr_key = key2;  // the chain moves up one: key2 -> key, key3 -> key2, their flags with them
+                    pn.key = key2;  // the chain moves up one: key2 -> key, key3 -> key2, their flags with them
                     st->pr_key2 = key3;
                     st->pr_key3 = key4;
                     st->pr_key4 = NO_ID;
                     const uint32_t ties0 = s_p0[P0_TIES], dt0 = s_p0[P0_DT];
-                    st->pr_ties = ties0 - 1u;
-                    st->pr_dt = (dt0 & 0xFFFFu) | (((dt0 >> 19) & 1u) << 16) | (((dt0 >> 20) & 1u) << 19) | (((dt0 >> 21) & 1u) << 20);
+                    pn.ties = ties0 - 1u;
+                    pn.dt = (dt0 & 0xFFFFu) | (((dt0 >> 19) & 1u) << 16) | (((dt0 >> 20) & 1u) << 19) | (((dt0 >> 21) & 1u) << 20);
+                    pn.births = s_p0[P0_BIRTHS];  // (the next bound is against the new pairs of both merges)
                     st->pr_h2 = h3;
                     st->pr_h3 = h4;
                     st->pr_h4 = h5;
                     st->pr_h5 = h6;
-                    st->pr_slack = ties0 == 3u ? 0xFFFFFFFFu : 0u;  // (the third was the last tied key)
-                    st->pr_plan_gen = 0xFFFFFFFFu;
-                    st->pr_x = N.B.X + 1;
+                    pn.slack = ties0 == 3u ? 0xFFFFFFFFu : 0u;  // (the third was the last tied key)
+                    pn.plan_gen = 0xFFFFFFFFu;
+                    pn.x = N.B.X + 1;
                 } else {
-                    st->pr_x = 0;
+                    pn.x = 0;
                 }
-                st->pr_hits = s_p0[P0_HITS] + 1;
+                atomicAdd(&st->pr_hits, 1u);
             }
             s_h = h;
             s_tie = tie ? 1u : 0u;

@@ -24,7 +24,7 @@ __host__ __device__ constexpr inline uint32_t pair_key(uint32_t first, uint32_t 
 
 // Multi-merge rounds (option round_k). A round applies a merge and up to ROUND_MAX - 1
 // named keys in one scan, one replace and one select launch. The keys are named two ways:
-//   - tied rounds: a tied merge's decision names the next tied keys by home slot order (DevState::pr_key ..
+//   - tied rounds: a tied merge's decision names the next tied keys by home slot order (DevState::ph, pr_key2 ..
 //     pr_key4); member j >= 1 merges when it is still tied and first in Zig slot order;
 //   - untied rounds (option round_untied): the select that begins an untied merge (its count T_0 unique) names
 //     the pairs of the next distinct counts T_1 > T_2 > .. below it, each held by one pair (DevState::ur);
@@ -41,7 +41,7 @@ constexpr uint32_t RT_JUNCTION = 16u; // the walk counted junction sides (DevSta
 constexpr uint32_t RT_WALKED = 32u;   // member j >= 1 walked by a list form (a stream scan is never a member)
 struct RoundHead {
     uint32_t n;                  // members the scan took (1 .. ROUND_MAX; written by its block 0)
-    uint32_t ties;               // tied keys at the decision that named them (pr_ties; 0: an untied round)
+    uint32_t ties;               // tied keys at the decision that named them (PairHead ties; 0: an untied round)
     int32_t live0;               // live pairs at the round's start (DevState::live as the scan saw it)
     uint32_t ties0;              // merge cur_x's tied pairs (DevState::tie_count as the scan saw it; 1: untied round)
     uint32_t key[ROUND_MAX];     // member keys (key[0] = cur_key)
@@ -70,6 +70,10 @@ struct RoundPlans {
     uint32_t plan[ROUND_MAX - 1][6];
 };
 static_assert(sizeof(RoundPlans) == 4 * (8 + 6 * (ROUND_MAX - 1)), "round plans: packed words");
+// A pair select's candidate for merge x (DevState::ph): what the light test reads (the kernel entry's round trip)
+struct PairHead {
+    uint32_t x, key, slack, ties, births, dt, pad, plan_gen;
+};
 // Device-resident state. Host reads a copy after each merge (one small D2H per merge).
 struct DevState {
     // ---- hot header (the first 96 B): the words the merge kernels read first, loaded together in one
@@ -143,26 +147,31 @@ struct DevState {
     // last refresh workgroup skips the decision's carries (zeroed with the state at each train)
     uint32_t ref_noprefix;
     // Pair selects (option pair_select, zbpe_select_next): the tie decision of merge X names the tied key of
-    // the second-smallest home as merge X+1's candidate (pr_key, pr_x = X+1); merge X's replace computes a
-    // lower bound on the free Zig-map slots that keep it first (pr_slack), counts its new pairs (pr_births) and, in
-    // pr_dt, the tied pairs it decremented (low 16 bits) with flags above them (bit 16 the candidate was
+    // the second-smallest home as merge X+1's candidate (PairHead key, x = X+1); merge X's replace computes a
+    // lower bound on the free Zig-map slots that keep it first (slack), counts its new pairs (births) and, in
+    // dt, the tied pairs it decremented (low 16 bits) with flags above them (bit 16 the candidate was
     // decremented, bit 17 a new pair reached the top count, bit 18 adjacent occurrences); the select of merge
     // X then starts merge X+1 with the candidate and no argmax or decision when every condition holds
     // (pr_hits counts those). Loaded as PairHead (the test, at kernel entry) and PairTail,
-    // and the candidate's scan plan (valid for layout generation pr_plan_gen; by the replace's extra workgroup)
-    alignas(128) uint32_t pr_x;
-    uint32_t pr_key, pr_slack, pr_ties, pr_births, pr_dt, pr_hits, pr_plan_gen;
+    // and the candidate's scan plan (pr_plan, valid for layout generation plan_gen; by the replace's extra workgroup)
+    // Two PairHead slots, by the candidate merge's parity: ph[x & 1] holds merge x's candidate. The select that starts
+    // merge x1 evaluates the light test on ph[x1 & 1] in every workgroup at entry, and a workgroup may start after the
+    // launch's committing block has moved on to merge x1 + 1: so no kernel writes ph[x1 & 1] in that launch (the
+    // chain and a decision name merge x1 + 1's candidate in ph[(x1 + 1) & 1]), and every workgroup sees the words the
+    // launch started with.
+    alignas(128) PairHead ph[2];
     uint32_t pr_plan[6];
     // chains (option pair_refresh 0): the third-smallest home's key, candidate of merge X+2 once merge X+1 was a
-    // pair select (bit 19 of pr_dt: decremented); the tied homes the replace bounds the free slots with: the
+    // pair select (bit 19 of dt: decremented); the tied homes the replace bounds the free slots with: the
     // candidate's and the next one's (pr_h2, pr_h3), the one after (pr_h4) and the largest (pr_hmax)
-    uint32_t pr_key2, pr_key3;        // (pr_key3: merge X+3's, option pair_chain 2; bit 20 of pr_dt: decremented)
+    uint32_t pr_key2, pr_key3;        // (pr_key3: merge X+3's, option pair_chain 2; bit 20 of dt: decremented)
     uint32_t pr_h2, pr_h3, pr_h4, pr_hmax, pr_h5;
     uint32_t pr_key4, pr_h6;          // (merge X+4's, option pair_chain 3; bit 21)
-    // pr_x as a tie decision set it (a pair select's chain shift leaves it): a multi-merge round takes the named
+    // the candidate's merge as a tie decision set it (a pair select's chain shift leaves it): a multi-merge round takes the named
     // keys only from the decision itself (the chain state past a pair select counts what that merge did)
     uint32_t pr_full;
-    uint32_t pr_pad2[8];
+    uint32_t pr_hits;        // pair selects taken (the committing block's counter)
+    uint32_t pr_pad2[7];
     // multi-merge rounds (option round_k, one GPU or replicas): see RoundHead; rd_merges counts the merges
     // rounds applied beyond their first members
     alignas(128) RoundHead rd;
@@ -176,9 +185,6 @@ struct DevState {
     uint32_t err_key, err_mode;  // (error 64: the pair, and its scan's form -- scan_mode)
     uint32_t last_light, err_light;  // the last merge a pair select started; (error 64: was the merge one)
     uint32_t err4_key, err4_site;  // (error 4: the first missing pair and where: 1 pair_dec, 2 merged pair, 3 update, 4 first occurrences)
-};
-struct PairHead {  // what the light test reads (the kernel entry's round trip)
-    uint32_t x, key, slack, ties, births, dt, hits, plan_gen;
 };
 struct PairTail {  // what a pair select then reads (plan, chain)
     uint32_t plan[6], key2, key3;
