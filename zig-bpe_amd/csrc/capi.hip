@@ -166,6 +166,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "round_k" && value >= 1 && value <= zbpe::ROUND_MAX) e.round_k = (int)value;
     else if (k == "round_ties" && value >= 0 && value <= 100) e.round_ties = (uint32_t)value;
     else if (k == "round_untied" && (value == 0 || value == 1)) e.round_untied = (int)value;
+    else if (k == "round_streak" && (value == 0 || value == 1)) e.round_streak = (int)value;
     else if (k == "encode_list_ratio" && value >= 1) e.enc_list_ratio = (uint32_t)value;
     else if (k == "list_start" && value >= 0) e.list_start = (uint64_t)value;
     else if (k == "hot_target" && value > 0) e.hot_target = (uint64_t)value;

@@ -1268,7 +1268,10 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // the batch's merges are counted after it
     // (and in tie streaks: a round of one costs more than a plain merge -- the members' walks, the full selects)
     // (untied rounds, option round_untied: in every list streak -- the mid phase's merges are mostly untied)
-    const bool rounds = round_k >= 2 && !dist() && fused_select && pair_select && refresh_prefix && lists_on && list_streak &&
+    // (round_streak 0: also in batches that follow stream scans, while the batch's bound on its records -- round_k merges
+    // per launch triple, each at most the top count -- is a sixteenth of the arena: else every batch would compact)
+    const bool streak_ok = list_streak || (!round_streak && (uint64_t)K * round_k * h_st->top_count * 16 < arena_limit());
+    const bool rounds = round_k >= 2 && !dist() && fused_select && pair_select && refresh_prefix && lists_on && streak_ok &&
                         (round_untied || last_tied_pct >= round_ties) && !replace_split && cs && C >= (uint64_t)SUMM_SLOTS * SUPER_BLOCKS;
     uint32_t KM = rounds ? std::min<uint32_t>(K * (uint32_t)round_k, run.vocab - X0) : K;  // merges the batch may do
     if (X0 < exact_lo && exact_lo < exact_hi) KM = std::min<uint32_t>(KM, exact_lo - X0);      // (no round past the exact-tie window's start)

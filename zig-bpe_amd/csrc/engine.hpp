@@ -57,6 +57,8 @@ struct Engine {
     int round_k = 5;            // option "round_k": members of a multi-merge round (1: no rounds; at most ROUND_MAX)
     uint32_t round_ties = 50;   // option "round_ties": rounds once this many percent of the last batch's merges were tied
     int round_untied = 1;       // option "round_untied": untied rounds (the next distinct counts' pairs), in every list streak
+    int round_streak = 1;       // option "round_streak": 1 rounds only in list streaks; 0 in any batch once the lists are on
+                                // and the batch's records fit the arena with room to spare (a stream scan is a round of one)
     uint32_t last_tied_pct = 0; // (the last batch's)
 
     // multi-GPU: this rank's shard and its neighbours' boundary tokens
