@@ -166,11 +166,12 @@ def test_sharded_corpus_over_4GiB(tmp_path):
     assert (r1.pair, r1.count) == ((m[1][0], m[1][1]), c[1])
 
 
-def handover_merge(g: dict, n_bytes: int, world: int, list_start: int = 64) -> int:
-    """the first merge k at which the sharded ranks may replicate (Engine::run_batch): the top count times
-    list_start times world is below the live tokens before merge k (the golden's counts and stream lengths)"""
+def handover_merge(g: dict, n_bytes: int, world: int, list_start: int = 64, power: int = 2) -> int:
+    """the first merge k at which the sharded ranks may replicate (Engine::run_batch, option handover = power): the top
+    count times list_start times world^power is below the live tokens before merge k (the golden's counts and stream
+    lengths)"""
     live = [n_bytes] + g["len_after"]
-    return next(k for k in range(len(g["counts"])) if g["counts"][k] * list_start * world < live[k])
+    return next(k for k in range(len(g["counts"])) if g["counts"][k] * list_start * world ** power < live[k])
 
 
 def check_sharded_vs_golden(g: dict, case: dict, world: int, timeout: int):

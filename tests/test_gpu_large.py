@@ -381,3 +381,4 @@ def test_c4_untied_rounds_same_run(c4, untied):
     assert np.array_equal(log[:, 3], c4.log[:, 3])
     assert fnv == c4.final_fnv and mism == 0
     assert st.round_merges > 0
+

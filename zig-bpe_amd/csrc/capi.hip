@@ -152,6 +152,7 @@ zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value) {
     else if (k == "fused_select") e.fused_select = value != 0;
     else if (k == "refresh_prefix") e.refresh_prefix = value != 0;
     else if (k == "replicate_late") e.replicate_late = value != 0;
+    else if (k == "handover" && value >= 1 && value <= 3) e.handover = (int)value;
     else if (k == "list_mode" && value >= 0 && value <= 1) e.list_mode = (int)value;
     else if (k == "compact_den_lists" && value >= 1) e.compact_den_lists = (uint64_t)value;
     else if (k == "list_grid" && value >= 0) e.list_grid = (int)value;

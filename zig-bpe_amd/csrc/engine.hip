@@ -457,9 +457,9 @@ zbpe_status Engine::build_lists(uint32_t lists_x, uint32_t ratio, bool ranges) {
     if (list_nb) {
         CHECK(ensure(&d_nb, nb_cap, (size_t)n + 64, "list neighbours"));
     }
+    const uint32_t tail_succ = dist() && halo.nright > 0 ? halo_right(halo, 0) : (uint32_t)HOLE;
     zbpe_list_scatter<<<nchunks, LIST_THREADS, pres_vp * 4, stream>>>(d_tok[cur], n, pres_vp, d_list_cnt, T.lst_off,
-                                                                       T.lst_len, d_lists, list_nb ? d_nb : nullptr,
-                                                                       dist() && halo.nright > 0 ? halo_right(halo, 0) : (uint32_t)HOLE);
+                                                                       T.lst_len, d_lists, list_nb ? d_nb : nullptr, tail_succ);
     LAUNCH_OK();
     // successor ranges: training on one stream (a shard's edge entries have no successor in it)
     dirs_built = false;
@@ -1237,8 +1237,10 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
     // multi-GPU: once pair counts are small against the stream (the single-GPU criterion for
     // occurrence lists, on replicated quantities so every rank decides alike), gather the stream
     // and continue as replicas
+    uint64_t wfac = 1;
+    for (int i = 0; i < handover; i++) wfac *= (uint64_t)world;
     if (dist() && replicate_late && list_mode && pres_vp <= PRES_MAX_VP &&
-        (uint64_t)h_st->top_count * list_start * (uint64_t)world < global_live &&
+        (uint64_t)h_st->top_count * list_start * wfac < global_live &&
         global_live + 64ull * world + (64u << 20) < 0xF0000000ull) {  // the gathered stream must fit u32 positions
         const double t_rep = now_s();
         HIP_OK(hipEventRecord(ev[3], stream));

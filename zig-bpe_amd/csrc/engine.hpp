@@ -69,6 +69,10 @@ struct Engine {
     // every rank gathers the whole stream and runs the remaining merges as a replica, with no
     // per-merge collective (option "replicate_late")
     bool replicate_late = true, replicated = false;
+    // option "handover": the ranks replicate once top count * list_start * world^handover < live tokens (1: the round-5
+    // rule; 2, default: later for more ranks -- a sharded merge's stream scan and replace shrink with the world while
+    // its two collectives and the select do not, so the sharded form stays cheaper for longer)
+    int handover = 2;
     uint64_t sum_tokens_rep = 0;     // stats.sum_tokens accumulated while replicated (counted once)
     uint64_t n_total = 0;            // corpus bytes over all ranks
     uint64_t global_live = 0;        // live tokens over all ranks (host-tracked from the merged counts)
