@@ -36,12 +36,14 @@ def main():
     except RuntimeError as e:
         print(json.dumps({"world": a.world, "case": a.case, "options": case["options"], "error": str(e).splitlines()[-1]}))
         return 0  # (reported; a non-zero exit is left to crashes and time limits)
-    res = {"world": a.world, "case": a.case, "options": case["options"]}
+    res = {"world": a.world, "case": a.case, "options": case["options"], "oracle_pair_tokens": int(ref.stats.pair_tokens),
+           "sum_tokens": int(out[0][3]["sum_tokens"]), "final_tokens": int(out[0][3]["final_tokens"]), "oracle_final": len(ref.tokens)}
     for r in range(a.world):
         _, m, c, st = out[r][:4]
         diff = next((i for i in range(max(len(m), len(rm))) if i >= len(m) or i >= len(rm) or m[i] != rm[i] or c[i] != rc[i]), None)
         res[f"rank{r}"] = {"first_diff": diff, "merges": len(m), "sharded_merges": st["sharded_merges"],
-                           "replications": st["replications"], "compactions": st["compactions"]}
+                           "replications": st["replications"], "compactions": st["compactions"],
+                           "round_merges": st.get("round_merges"), "self_pair_merges": st.get("self_pair_merges")}
     print(json.dumps(res))
     return 0
 

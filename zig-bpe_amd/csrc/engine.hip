@@ -1247,6 +1247,13 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         CHECK(compact());  // this shard's live tokens, contiguous
         CHECK(replicate());
         CHECK(build_lists(X0, list_ratio, true));
+        // merge X0 was begun by the last sharded select (begun): its log row holds the shard's live tokens; it runs as a
+        // replica, on the whole stream (sum_tokens and the scan bytes count the row's live tokens, rank 0 once replicated)
+        if (begun) {
+            const uint32_t lt = (uint32_t)n_live;
+            HIP_OK(hipMemcpyAsync(&d_log[X0 - 256].live, &lt, 4, hipMemcpyHostToDevice, stream));
+            HIP_OK(hipStreamSynchronize(stream));
+        }
         HIP_OK(hipEventRecord(ev[4], stream));
         HIP_OK(hipEventSynchronize(ev[4]));
         float ms;
