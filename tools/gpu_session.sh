@@ -1,8 +1,7 @@
-# round-6 GPU session: the sharded words case (world 4, hand-over at merge 190) against the oracle's sum of stream
-# lengths, then the full -m gpu suite and the bench line
+#!/bin/bash
+# One gpurun call's steps (edited per call): see tools/measure.sh for the steps.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
-O=${O:-gpurun_out/r06j}; mkdir -p $O
-timeout -k 10 120 python3 tools/dist_case.py --world 4 --case 0 2>> $O/dc.err | grep -v Gloo > $O/one.json || exit 1
-cut -c1-300 $O/one.json
-O=$O STEPS="test bench" bash tools/measure.sh || exit 2
+O=gpurun_out/r06m; mkdir -p $O
+timeout -k 10 400 python3 tools/ab_run.py --reps 2 --cfg "" --cfg sel_growth=8 --cfg sel_growth=4 --cfg sel_growth=0 --cfg sel_growth=0,hot_target=1024 > $O/ab_sel.jsonl 2> $O/ab_sel.err || { tail $O/ab_sel.err; exit 1; }
+cat $O/ab_sel.jsonl

@@ -1205,7 +1205,8 @@ zbpe_status Engine::train(uint16_t vocab_size, int verbose, uint16_t *out_triple
             const double nl = std::max(1.0, (double)Q[4]), nr = std::max(1.0, (double)Q[7]), ns = std::max(1.0, (double)Q[9]);
             fprintf(stderr, "pipe_prof %s: list scans %llu: avg us from the launch's block-0 start: LDS clear done %.2f, walk "
                             "done %.2f, flush done %.2f, replace starts %.2f; replace (%llu): work done %.2f, select starts %.2f; "
-                            "select end -> scan start (%llu) %.2f; round scans' bound workgroups done %.2f\n",
+                            "select's commit -> next scan's block-0 start, in-batch (%llu) %.2f; round scans' bound "
+                            "workgroups done %.2f\n",
                     bucket[k], Q[4], Q[0] * us / nl, Q[1] * us / nl, Q[2] * us / nl, Q[3] * us / nl, Q[7], Q[5] * us / nr,
                     Q[6] * us / nr, Q[9], Q[8] * us / ns, Q[15] * us / nl);
             fprintf(stderr, "pipe_prof %s: replace phases, avg us from its block-0 start (latest block): deltas in %.2f, "
@@ -1262,6 +1263,9 @@ zbpe_status Engine::run_batch(uint32_t X0, uint32_t *done, bool *halted) {
         CHECK(sync_state());
         stats.replicate_s += now_s() - t_rep;  // (inside this batch's wall, taken out of replicated_s in train)
     }
+    // option sel_prof: the select -> scan gap probe counts in-batch transitions only (a batch's first scan follows a
+    // host window: a halt's rebuild, a compaction or the host's own turn, not a launch gap)
+    if (sel_prof) HIP_OK(hipMemsetAsync(&d_st->pp_t[7], 0, 8, stream));
     const uint64_t C = home_slots;
     const uint32_t nb = (uint32_t)((C + SUMM_SLOTS - 1) / SUMM_SLOTS), nsb = (nb + SUPER_BLOCKS - 1) / SUPER_BLOCKS;
     const HomeView V{T.home_cnt, d_summ, d_sup, (uint32_t)C, nb, nsb};

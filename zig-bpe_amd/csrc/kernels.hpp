@@ -3482,17 +3482,10 @@ __global__ void zbpe_self_x0(const uint32_t *__restrict__ fns, int rank, uint8_t
 // shared record counter) only once another tile might not fit. One workgroup per tile with a flush each made
 // ~2.6e5 same-address atomics per launch at C4 -- ~12 ns each at the counter, most of the launch's 1-2 ms.)
 constexpr uint32_t SELF_REC = 2 * (SELF_TILE / 2);  // staged records: two tiles' worth (a tile holds <= SELF_TILE / 2)
-// Each candidate's neighbours come from the tile's live-slot masks in LDS (one 32-bit word per thread's slots): the
-// next / previous live slot of any slot is a bit scan, usually of one word, so the occurrence's second a, its left
-// neighbour, the slot after it and the one after that are found with LDS reads only and their tokens loaded together
-// (one global round trip, cache hits). The round-5 form walked next_live / prev_live slot by slot, a chain of dependent
-// global loads per candidate through every hole (PMC: 56 % of the wave cycles waiting on memory, 0.8-1.7 TB/s).
-// Slots outside the tile (its edges, the shard's halo) take the general next_live_h / prev_live_h.
 __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, const uint8_t *__restrict__ carry_in) {
     const ScanArgs A = scan_args_resolve(A0, load_head(A0.st), A0.X);
     __shared__ uint32_t s_left[LDS_BINS], s_right[LDS_BINS];
     __shared__ uint32_t s_rec[SELF_REC];
-    __shared__ uint32_t s_live[SELF_THREADS];  // bit i of word t: tile slot 32 t + i is live
     __shared__ uint8_t s_wave[SELF_THREADS / 64];
     __shared__ uint32_t s_nrec, s_base;
     for (int i = threadIdx.x; i < LDS_BINS; i += SELF_THREADS) { s_left[i] = 0; s_right[i] = 0; }
@@ -3520,39 +3513,11 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
         const int64_t t0 = beg + threadIdx.x * SELF_PER_THREAD;
         uint32_t w[16];
         self_load(tok, t0, end, w);
-        uint32_t live = 0;
-#pragma unroll
-        for (int i = 0; i < SELF_PER_THREAD; i++) live |= (((w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) != HOLE ? 1u : 0u) << i;
-        s_live[threadIdx.x] = live;  // (published by self_block_scan's barrier)
         // parity of the live a-run entering my slots: the tile's carry through the threads before mine
         // (self_block_scan's barrier also orders a flush's s_nrec reset before this tile's records)
         const uint8_t pre = self_block_scan(self_walk(w, a, -1, nullptr), s_wave, nullptr);
         uint32_t cand;
         (void)self_walk(w, a, self_apply(pre, carry_in[tile] & 1), &cand);
-        // the next / previous live slot around a position (absolute; NONE_POS: none), by the masks inside the tile
-        const auto next_of = [&](int64_t p) -> int64_t {
-            if (p == NONE_POS) return NONE_POS;
-            if (p >= beg && p + 1 < end) {
-                const uint32_t x = (uint32_t)(p + 1 - beg);
-                uint32_t tx = x >> 5, m = s_live[tx] & (~0u << (x & 31));
-                while (!m && ++tx < (uint32_t)SELF_THREADS) m = s_live[tx];
-                if (m) return beg + (int64_t)(tx << 5) + __builtin_ctz(m);
-                return next_live_h(A, end - 1);
-            }
-            return next_live_h(A, p);
-        };
-        const auto prev_of = [&](int64_t p) -> int64_t {
-            if (p > beg && p < end) {
-                const uint32_t x = (uint32_t)(p - 1 - beg);
-                int32_t tx = (int32_t)(x >> 5);
-                uint32_t m = s_live[tx] & (0xFFFFFFFFu >> (31 - (x & 31)));
-                while (!m && --tx >= 0) m = s_live[tx];
-                if (m) return beg + (int64_t)tx * 32 + (31 - __builtin_clz(m));
-                return prev_live_h(A, beg);
-            }
-            return prev_live_h(A, p);
-        };
-        const auto tok_of = [&](int64_t p) -> uint32_t { return p == NONE_POS ? (uint32_t)HOLE : tok_h(A, p); };
         // a's at even offsets of their runs: occurrences when the next live token is an a (wave-uniform steps:
         // one LDS atomic per wave and step reserves the records)
         while (__ballot(cand != 0)) {
@@ -3562,18 +3527,23 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
                 const int i = __builtin_ctz(cand);
                 cand &= cand - 1;
                 p = t0 + i;
-                // every position first (LDS masks), then their tokens together
-                const int64_t q = next_of(p);
-                const int64_t l = A.count_deltas ? prev_of(p) : NONE_POS;
-                const int64_t r = A.count_deltas ? next_of(q) : NONE_POS;
-                const int64_t r2 = A.count_deltas ? next_of(r) : NONE_POS;
-                const uint32_t tq = tok_of(q), tl = tok_of(l), tr = tok_of(r), tr2 = tok_of(r2);
-                hit = q != NONE_POS && tq == a;
+                const int64_t q = next_live_h(A, p);
+                hit = q != NONE_POS && tok_h(A, q) == a;
                 if (hit && A.count_deltas) {  // occurrence (p, q)
                     // the left neighbour, unless it is the end of a previous occurrence
-                    if (l != NONE_POS && tl != a) H.left((uint16_t)tl);
+                    const int64_t l = prev_live_h(A, p);
+                    if (l != NONE_POS) {
+                        const uint32_t tl = tok_h(A, l);
+                        if (tl != a) H.left((uint16_t)tl);
+                    }
+                    const int64_t r = next_live_h(A, q);
                     if (r != NONE_POS) {
-                        const bool r_occ = tr == a && r2 != NONE_POS && tr2 == a;
+                        const uint32_t tr = tok_h(A, r);
+                        bool r_occ = false;
+                        if (tr == a) {
+                            const int64_t r2 = next_live_h(A, r);
+                            r_occ = r2 != NONE_POS && tok_h(A, r2) == a;
+                        }
                         if (r_occ) xx++;
                         else H.right((uint16_t)tr);
                     }
