@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "types.hpp"
+#include "wave.hpp"
 
 namespace zbpe {
 // DevState's hot header in one round trip: every word is loaded here at kernel entry, before any
@@ -1933,7 +1934,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             // presence: one atomic per run of hits in one block (the records come in stream order
             // within a tile)
             const uint32_t blk = hit ? pr / PRES_BLK : 0xffffffffu;
-            const uint32_t blk_up = (uint32_t)__shfl_up((int)blk, 1);
+            const uint32_t blk_up = wave_shr1(blk, 0xffffffffu);
             if (hit) {
                 wrec[nbuf + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = pr;
                 if (A.pres && (lane == 0 || blk_up != blk)) pres_set(A, pr);
@@ -2023,17 +2024,15 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
                 const uint32_t P2 = pair_key(A.a, HOLE);
 #pragma unroll
                 for (int u = 0; u < UNROLL; u++) {
-                    const uint32_t nrow = u + 1 < UNROLL ? (uint32_t)__shfl((int)v[u + 1 < UNROLL ? u + 1 : u].x, 0) : e_nx;
-                    const uint32_t dn = (uint32_t)__shfl_down((int)v[u].x, 1);
-                    cand |= (uint64_t)pair_windows8<false>(v[u], lane == 63 ? nrow : dn, P1, P2) << (8 * u);
+                    const uint32_t nrow = u + 1 < UNROLL ? lane_bcast(v[u + 1 < UNROLL ? u + 1 : u].x, 0) : e_nx;
+                    cand |= (uint64_t)pair_windows8<false>(v[u], wave_shl1(v[u].x, nrow), P1, P2) << (8 * u);
                 }
             } else {
                 const uint32_t P2 = pair_key(HOLE, A.b);
 #pragma unroll
                 for (int u = 0; u < UNROLL; u++) {
-                    const uint32_t prow = u > 0 ? (uint32_t)__shfl((int)v[u > 0 ? u - 1 : 0].w, 63) : e_prev;
-                    const uint32_t up = (uint32_t)__shfl_up((int)v[u].w, 1);
-                    cand |= (uint64_t)pair_windows8<true>(v[u], lane == 0 ? prow : up, P1, P2) << (8 * u);
+                    const uint32_t prow = u > 0 ? lane_bcast(v[u > 0 ? u - 1 : 0].w, 63) : e_prev;
+                    cand |= (uint64_t)pair_windows8<true>(v[u], wave_shr1(v[u].w, prow), P1, P2) << (8 * u);
                 }
             }
         } else {
@@ -2045,8 +2044,8 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
         if constexpr (BATCH) {
             if (tile_cand) {
                 const uint32_t cnt = (uint32_t)__popcll(cand);
-                const uint32_t incl = wave_incl_scan(cnt);
-                const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+                const uint32_t incl = wave_incl_scan_dpp(cnt);
+                const uint32_t total = lane_bcast(incl, 63);
                 batched = batch_on && total <= CB_DENSE;  // (ncb <= CB_REC - CB_DENSE here: it fits)
                 if (batched) {
                     uint32_t slot = ncb + incl - cnt;  // this lane's next record
@@ -2054,30 +2053,19 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
                     for (int u = 0; u < UNROLL; u++) {
                         const uint32_t cu = (uint32_t)(cand >> (8 * u)) & 0xffu;
                         if (!__ballot(cu != 0)) continue;
-                        // the window of vector (u, lane) from the lanes' registers
+                        // the window of vector (u, lane) from the lanes' registers: the previous lane's vector (lane 0:
+                        // the previous row's lane 63, or the word before the tile), the word two lanes back, the next
+                        // lane's first two words (lane 63: the next row's lane 0, or the words after the tile)
                         const uint4 vp = u > 0 ? v[u > 0 ? u - 1 : 0] : make_uint4(0, 0, 0, 0);
-                        uint4 pv;
-                        pv.x = (uint32_t)__shfl_up((int)v[u].x, 1);
-                        pv.y = (uint32_t)__shfl_up((int)v[u].y, 1);
-                        pv.z = (uint32_t)__shfl_up((int)v[u].z, 1);
-                        pv.w = (uint32_t)__shfl_up((int)v[u].w, 1);
-                        uint32_t wpp = (uint32_t)__shfl_up((int)v[u].w, 2);
-                        const uint32_t r63x = (uint32_t)__shfl((int)vp.x, 63), r63y = (uint32_t)__shfl((int)vp.y, 63);
-                        const uint32_t r63z = (uint32_t)__shfl((int)vp.z, 63), r63w = (uint32_t)__shfl((int)vp.w, 63);
-                        const uint32_t r62w = (uint32_t)__shfl((int)vp.w, 62);
-                        uint32_t nx = (uint32_t)__shfl_down((int)v[u].x, 1), ny = (uint32_t)__shfl_down((int)v[u].y, 1);
                         const uint4 vn = u + 1 < UNROLL ? v[u + 1 < UNROLL ? u + 1 : u] : make_uint4(0, 0, 0, 0);
-                        const uint32_t n0x = (uint32_t)__shfl((int)vn.x, 0), n0y = (uint32_t)__shfl((int)vn.y, 0);
-                        if (lane == 0) {
-                            pv = u > 0 ? make_uint4(r63x, r63y, r63z, r63w) : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, e_prev);
-                            wpp = u > 0 ? r62w : 0xffffffffu;
-                        } else if (lane == 1) {
-                            wpp = u > 0 ? r63w : e_prev;
-                        }
-                        if (lane == 63) {
-                            nx = u + 1 < UNROLL ? n0x : e_nx;
-                            ny = u + 1 < UNROLL ? n0y : e_ny;
-                        }
+                        uint4 pv;
+                        pv.x = wave_shr1(v[u].x, u > 0 ? lane_bcast(vp.x, 63) : 0xffffffffu);
+                        pv.y = wave_shr1(v[u].y, u > 0 ? lane_bcast(vp.y, 63) : 0xffffffffu);
+                        pv.z = wave_shr1(v[u].z, u > 0 ? lane_bcast(vp.z, 63) : 0xffffffffu);
+                        pv.w = wave_shr1(v[u].w, u > 0 ? lane_bcast(vp.w, 63) : e_prev);
+                        const uint32_t wpp = wave_shr1(pv.w, u > 0 ? lane_bcast(vp.w, 62) : 0xffffffffu);
+                        const uint32_t nx = wave_shl1(v[u].x, u + 1 < UNROLL ? lane_bcast(vn.x, 0) : e_nx);
+                        const uint32_t ny = wave_shl1(v[u].y, u + 1 < UNROLL ? lane_bcast(vn.y, 0) : e_ny);
                         uint32_t c = cu;
                         while (c) {
                             const int k = __builtin_ctz(c);
@@ -2175,8 +2163,8 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
             // phase 2, dense form: the tile's candidates are compacted into a per-wave LDS list and
             // resolved one per lane (a lane-per-vector loop would iterate as often as the busiest lane)
             const uint32_t cnt = (uint32_t)__popcll(cand);
-            const uint32_t incl = wave_incl_scan(cnt);
-            const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+            const uint32_t incl = wave_incl_scan_dpp(cnt);
+            const uint32_t total = lane_bcast(incl, 63);
             const uint64_t tile_blk = (uint64_t)vbase * 8 / PRES_BLK;
             bool tile_hit = false;
             uint32_t *wc = s_cand[wib];
