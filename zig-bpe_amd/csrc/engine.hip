@@ -798,8 +798,8 @@ zbpe_status Engine::set_scan_variant(int v) {
 // Variant 0 by default; its batching twin (variant 7) once the pair is known to be sparse: count_hint
 // (a bound on the pair's count: the top count when the merges were enqueued, which never rises) times
 // SCAN_BATCH_DENSITY below the stream's slots. (Batching resolves a sparse tile's few candidates with
-// those of other tiles, +9..20 % at densities 1e-4..2e-3; variant 7 is ~7 % slower on dense tiles,
-// tools/scan_bands.py, profiles/r03_scan_bands_batch.jsonl.)
+// those of other tiles; since its windows move by DPP it is ahead at every density below 3e-2,
+// tools/scan_bands.py, profiles/r06_scan_bands_dpp.jsonl.)
 static constexpr int kScanBatchVariant = 7;
 zbpe_status Engine::launch_scan(const ScanArgs &A, int grid, uint64_t count_hint) {
     int v = scan_variant;

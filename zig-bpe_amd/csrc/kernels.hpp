@@ -310,6 +310,24 @@ __device__ inline MaxRec wave_max(MaxRec r) {
     }
     return r;
 }
+// The same by DPP (every lane active): a butterfly inside each 16-lane row -- quad_perm [1,0,3,2] and [2,3,0,1],
+// half-row mirror, row mirror; each pairs two disjoint halves, so every record is counted once -- then the four
+// rows' results combined from v_readlane (wave-uniform). The select's argmax reduces on its critical path; six
+// dependent ds_bpermute steps there cost ~0.25 us per reduction.
+template <int CTRL>
+__device__ __attribute__((always_inline)) inline MaxRec max_dpp_step(MaxRec r) {
+    return max_combine(r, MaxRec{dpp_mov<CTRL>(r.cnt), dpp_mov<CTRL>(r.ties), dpp_mov<CTRL>(r.id)});
+}
+__device__ __attribute__((always_inline)) inline MaxRec wave_max_dpp(MaxRec r) {
+    r = max_dpp_step<0xB1>(r);   // quad_perm [1,0,3,2]
+    r = max_dpp_step<0x4E>(r);   // quad_perm [2,3,0,1]
+    r = max_dpp_step<0x141>(r);  // row_half_mirror
+    r = max_dpp_step<0x140>(r);  // row_mirror
+    MaxRec q{lane_bcast(r.cnt, 0), lane_bcast(r.ties, 0), lane_bcast(r.id, 0)};
+#pragma unroll
+    for (int l = 16; l < 64; l += 16) q = max_combine(q, MaxRec{lane_bcast(r.cnt, l), lane_bcast(r.ties, l), lane_bcast(r.id, l)});
+    return q;
+}
 constexpr int ARGMAX_THREADS = 256;
 __global__ void __launch_bounds__(ARGMAX_THREADS) zbpe_argmax_partial(const uint32_t *__restrict__ cnt, uint32_t id_cap,
                                                                       const DevState *st, MaxRec *__restrict__ partial) {
@@ -363,6 +381,8 @@ __global__ void __launch_bounds__(256) zbpe_argmax_final(const MaxRec *__restric
 
 // ------------------------------------------------------------------------------------------
 // Stream helpers (hole skipping). Positions are signed 64-bit; -1 = none.
+// (Slot by slot: a form that crossed holes 8 slots per 16-B load measured 1 % slower over a C4 train -- most runs of
+// holes are one or two slots -- profiles/r06_ab_hole_walk_vector.txt.)
 // ------------------------------------------------------------------------------------------
 __device__ inline int64_t next_live(const uint16_t *tok, int64_t n, int64_t i) {
     for (int64_t k = i + 1; k < n; ++k)
@@ -505,9 +525,10 @@ struct ScanArgs {
     uint32_t *rd_touch, *rd_top, *rd_birth, *rd_jn, *rd_nmax;
 };
 constexpr uint32_t NO_LIST = 0xFFFFFFFFu;
-// batching pays below about one occurrence per 400 slots and costs above it (tools/scan_bands.py:
-// +19 % at 5e-4, -10 % at 5e-3, where most tiles are dense and each one flushes a short batch)
-constexpr uint64_t SCAN_BATCH_DENSITY = 400;
+// batching pays below about one occurrence per 32 slots (tools/scan_bands.py, DPP window moves: +5 % at 5e-4,
+// +11 % at 2e-3, +16 % at 5e-3, +8 % at 1e-2, even at 3e-2, profiles/r06_scan_bands_dpp.jsonl; with shuffles it
+// cost above 1 in 400, where most tiles are dense and each one flushed a short batch)
+constexpr uint64_t SCAN_BATCH_DENSITY = 32;
 // the device-held parts of the arguments: pair (batch mode), halo (batch mode, multi-GPU), record
 // window in the arena
 // (H: the state head, load_head at kernel entry)
@@ -719,7 +740,7 @@ __device__ inline void wave_flush_records(const ScanArgs &A, const uint32_t *rec
         base = atomicAdd(A.rec_ctr, n);
         atomicAdd(A.occ_out, n);
     }
-    base = (uint32_t)__shfl((int)base, 0);
+    base = lane_bcast(base, 0);
     for (uint32_t i = lane; i < n; i += 64)
         if (base + i < A.rec_cap) A.rec[base + i] = rec[i];
     if (lane == 0 && base + n > A.rec_cap) atomicOr(&A.st->error, 8u);
@@ -923,7 +944,7 @@ __device__ inline void lrec_stage(const ScanArgs &A, ScanLds &S, bool hit, uint3
     const int lane = threadIdx.x & 63;
     uint32_t lbase = 0;
     if (lane == 0) lbase = atomicAdd(&S.lrec_n, (uint32_t)__popcll(hm));
-    lbase = (uint32_t)__shfl((int)lbase, 0);
+    lbase = lane_bcast(lbase, 0);
     const uint32_t j = lbase + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));
     if (hit && j < LREC_CAP) S.lrec[j] = pr;
     const uint64_t over = __ballot(hit && j >= LREC_CAP);
@@ -933,7 +954,7 @@ __device__ inline void lrec_stage(const ScanArgs &A, ScanLds &S, bool hit, uint3
         gbase = atomicAdd(A.rec_ctr, (uint32_t)__popcll(over));
         atomicAdd(A.occ_out, (uint32_t)__popcll(over));
     }
-    gbase = (uint32_t)__shfl((int)gbase, 0);
+    gbase = lane_bcast(gbase, 0);
     if (hit && j >= LREC_CAP) {
         const uint32_t jr = gbase + (uint32_t)__popcll(over & ((1ull << lane) - 1ull));
         if (jr < A.rec_cap) A.rec[jr] = pr;
@@ -1613,8 +1634,8 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
             M = hi > lo ? hi - lo : 0u;
         } else {
             c = (uint32_t)__popc(mk);
-            incl = wave_incl_scan(c);
-            M = (uint32_t)__shfl((int)incl, 63);
+            incl = wave_incl_scan_dpp(c);
+            M = lane_bcast(incl, 63);
         }
         for (uint32_t r0 = 0; r0 < M; r0 += 64) {
             const uint32_t j = r0 + lane;
@@ -5099,8 +5120,8 @@ __device__ inline bool block_ticket_last_x(uint32_t *ctr, uint32_t nblocks, uint
     __syncthreads();
     return *s_flag != 0;
 }
-__device__ __attribute__((always_inline)) inline MaxRec block_max(MaxRec r, MaxRec *sm) {
-    r = wave_max(r);
+__device__ __attribute__((always_inline)) inline MaxRec block_max(MaxRec r, MaxRec *sm) {  // (every thread of the block)
+    r = wave_max_dpp(r);
     if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = r;
     __syncthreads();
     MaxRec q = sm[0];

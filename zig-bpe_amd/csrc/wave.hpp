@@ -15,6 +15,11 @@ __device__ __attribute__((always_inline)) inline uint32_t wave_shr1(uint32_t x, 
 __device__ __attribute__((always_inline)) inline uint32_t wave_shl1(uint32_t x, uint32_t fill) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)x, 0x130, 0xF, 0xF, false);
 }
+// a DPP move inside rows (quad_perm, mirrors: every source lane valid)
+template <int CTRL>
+__device__ __attribute__((always_inline)) inline uint32_t dpp_mov(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
 // lane l's x, as a scalar
 __device__ __attribute__((always_inline)) inline uint32_t lane_bcast(uint32_t x, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
