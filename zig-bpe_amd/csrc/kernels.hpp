@@ -135,7 +135,7 @@ __device__ inline uint32_t wave_append(uint32_t *counter, bool flag) {
     const int leader = __ffsll((unsigned long long)m) - 1;
     uint32_t base = 0;
     if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
+    base = lane_bcast(base, leader);  // (the leader lane is active: its flag is in the ballot)
     const uint64_t below = m & ((1ull << lane) - 1ull);
     return flag ? base + (uint32_t)__popcll(below) : ~0u;
 }
@@ -1037,9 +1037,8 @@ __device__ inline void scan_lds_flush_rd(const ScanArgs &A, ScanLds &S, const Ne
         births += e[k] != ~0u && oq[k] == 0 ? 1u : 0u;
         top = e[k] != ~0u ? max(top, oq[k] + vk) : top;
     }
-    births = wave_sum(births);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) top = max(top, (uint32_t)__shfl_xor((int)top, off));
+    births = wave_sum_u32(births);  // (every thread calls it)
+    top = wave_max_u32(top);
     if ((threadIdx.x & 63) == 0) {
         if (births) atomicAdd(&S.rd[0], births);
         if (top) atomicMax(&S.rd[1], top);
@@ -1196,7 +1195,7 @@ __device__ __attribute__((always_inline)) inline void self_list_walk(const ScanA
             else if (q >= 0) H.right((uint16_t)tok[q]);
         }
     }
-    xx = wave_sum(xx);
+    xx = wave_sum_u32(xx);  // (every thread of the block)
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     if (lane == 0 && any) S.any = 1;
     __syncthreads();
@@ -1698,7 +1697,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_filtered(const S
             lrec_stage(A, S, hit, pr, hm);
         }
     }
-    xx = wave_sum(xx);
+    xx = wave_sum_u32(xx);  // (every thread of the block)
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     if (RD && lane == 0 && xx) atomicOr(A.rd_top, RT_XX);
     if (lane == 0 && any) S.any = 1;
@@ -1820,7 +1819,7 @@ __device__ __attribute__((always_inline)) inline void scan_list_body(const ScanA
             lrec_stage(A, S, hit, pr, m);
         }
     }
-    xx = wave_sum(xx);
+    xx = wave_sum_u32(xx);  // (every thread of the block)
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     if (RD && lane == 0 && xx) atomicOr(A.rd_top, RT_XX);
     if (lane == 0 && any) s_any = 1;
@@ -2291,7 +2290,7 @@ __device__ __attribute__((always_inline)) inline void scan_pairs_body(const Scan
         wave_flush_records(A, wrec, nbuf);
     }
     // flush LDS neighbour histograms, the xx count and the streamed-slot count
-    xx = wave_sum(xx);
+    xx = wave_sum_u32(xx);  // (every thread of the block)
     if (lane == 0 && xx) atomicAdd(A.xx_out, xx);
     const bool wave_any = __ballot(any != 0) != 0;  // (a directly recorded occurrence sets it in one lane)
     if (lane == 0 && wave_any) s_any = 1;
@@ -3574,7 +3573,7 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
     }
     if (staged) flush();
     if (threadIdx.x == 0 && occ) atomicAdd(A.occ_out, occ);
-    xx = wave_sum(xx);
+    xx = wave_sum_u32(xx);  // (every thread of the block)
     if ((threadIdx.x & 63) == 0 && xx) atomicAdd(A.xx_out, xx);
     __syncthreads();
     if (occ) {
@@ -3910,6 +3909,35 @@ __device__ inline Summ slot_fold(Summ x, uint32_t k) {
     const int32_t d = (int32_t)k - 1;
     return Summ{x.q + d, max(0, x.m + d)};
 }
+// Ordered scans of carry summaries by DPP (every lane of the wave active). Summ{0, 0} is the identity of
+// summ_cat: every summary has m >= max(q, 0) (summ_slot, slot_fold and summ_cat keep it), so
+// summ_cat({0, 0}, b) = {b.q, max(b.m, b.q)} = b and summ_cat(a, {0, 0}) = {a.q, max(0, a.m)} = a; a DPP lane
+// with no source keeps the 0 it starts from. Inclusive: row_shr:1,2,4,8 inside each 16-lane row, then row 0's
+// total into row 1 and row 2's into row 3 (row_bcast:15), rows 0-1's into rows 2 and 3 (row_bcast:31), each
+// composed on the left. (One VALU op per move; the __shfl forms were six dependent ds_bpermute steps on the tie
+// decision's and the home refresh's paths.)
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline Summ summ_dpp(Summ x) {
+    return Summ{__builtin_amdgcn_update_dpp(0, x.q, CTRL, ROWS, 0xF, false), __builtin_amdgcn_update_dpp(0, x.m, CTRL, ROWS, 0xF, false)};
+}
+__device__ __attribute__((always_inline)) inline Summ summ_scan_dpp(Summ x) {  // lane i: x_0 . x_1 . ... . x_i
+    x = summ_cat(summ_dpp<0x111, 0xF>(x), x);
+    x = summ_cat(summ_dpp<0x112, 0xF>(x), x);
+    x = summ_cat(summ_dpp<0x114, 0xF>(x), x);
+    x = summ_cat(summ_dpp<0x118, 0xF>(x), x);
+    x = summ_cat(summ_dpp<0x142, 0xA>(x), x);
+    x = summ_cat(summ_dpp<0x143, 0xC>(x), x);
+    return x;
+}
+// the exclusive scan from the inclusive one (lane 0: the identity)
+__device__ __attribute__((always_inline)) inline Summ summ_excl_dpp(Summ inc) {
+    return Summ{(int32_t)wave_shr1((uint32_t)inc.q, 0u), (int32_t)wave_shr1((uint32_t)inc.m, 0u)};
+}
+__device__ __attribute__((always_inline)) inline Summ summ_lane(Summ x, int l) {
+    return Summ{(int32_t)lane_bcast((uint32_t)x.q, l), (int32_t)lane_bcast((uint32_t)x.m, l)};
+}
+// ordered reduction over the lanes of one wave (x_0 . x_1 . ... . x_63), wave-uniform (every lane active)
+__device__ inline Summ wave_reduce_summ(Summ x) { return summ_lane(summ_scan_dpp(x), 63); }
 // the summary of 64 consecutive slots (16 words of 4 one-byte home counts): q from byte sums
 // (v_sad_u8, one per word), m by the slot_fold recurrence
 __device__ inline Summ fold64(const uint32_t (&w)[16]) {
@@ -4108,14 +4136,7 @@ __device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslo
             for (int kk = 0; kk < 64; kk++)
                 if (s0 + kk < nslots) x = slot_fold(x, ((w[kk >> 2] >> (8 * (kk & 3))) & 0xffu));
         }
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            Summ y;
-            y.q = __shfl_down(x.q, off);
-            y.m = __shfl_down(x.m, off);
-            if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
-        }
-        return x;
+        return wave_reduce_summ(x);  // (the wave's loop is uniform: every lane active)
     };
     auto put = [&](uint32_t bi, Summ x) {
         const uint32_t blk = sb * SUPER_BLOCKS + bi;
@@ -4145,13 +4166,7 @@ __device__ inline void refresh_super(const Tables &T, uint32_t sb, uint32_t nslo
         const uint32_t bi = lane, blk = sb * SUPER_BLOCKS + bi;
         Summ x{0, 0};
         if (blk < nb) x = ((bits >> bi) & 1) ? s_new[bi] : old;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            Summ y;
-            y.q = __shfl_down(x.q, off);
-            y.m = __shfl_down(x.m, off);
-            if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
-        }
+        x = wave_reduce_summ(x);
         if (lane == 0) {
             if (wt) {
                 __hip_atomic_store(&sup[sb].q, x.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -4241,21 +4256,6 @@ __device__ __attribute__((always_inline)) inline Summ wave_compose_slots(const u
             }
         }
     }
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        Summ y;
-        y.q = __shfl_down(x.q, off);
-        y.m = __shfl_down(x.m, off);
-        if ((lane & (2 * off - 1)) == 0) x = summ_cat(x, y);
-    }
-    Summ r;
-    r.q = __shfl(x.q, 0);
-    r.m = __shfl(x.m, 0);
-    return r;
-}
-// ordered reduction over the lanes of one wave (lane i absorbs lane i + off), result broadcast
-__device__ inline Summ wave_reduce_summ(Summ x) {
-    const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         Summ y;
@@ -4376,24 +4376,13 @@ __device__ __attribute__((always_inline)) inline int64_t wave_first_free(const H
         const bool valid = s < V.C;
         const uint32_t k = valid ? home_at(V.hc, s) : 0u;
         // carry into slot s: composition of the slots [base, s) applied to c (exclusive scan)
-        Summ inc = summ_slot(k);
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            Summ y;
-            y.q = __shfl_up(inc.q, off);
-            y.m = __shfl_up(inc.m, off);
-            if ((int)lane >= off) inc = summ_cat(y, inc);
-        }
-        Summ ex;
-        ex.q = __shfl_up(inc.q, 1);
-        ex.m = __shfl_up(inc.m, 1);
-        if (lane == 0) ex = Summ{0, 0};
+        const Summ inc = summ_scan_dpp(summ_slot(k)), ex = summ_excl_dpp(inc);
         const int32_t cin = max(ex.m, c + ex.q);
         const uint64_t fr = __ballot(valid && cin + (int32_t)k == 0);
         if (fr) return (int64_t)base + __builtin_ctzll(fr);
         if (base + 64 >= V.C) return -1;
-        const int32_t tq = __shfl(inc.q, 63), tm = __shfl(inc.m, 63);
-        c = max(tm, c + tq);
+        const Summ t = summ_lane(inc, 63);
+        c = max(t.m, c + t.q);
     }
     return -1;
 }
@@ -4434,18 +4423,7 @@ __device__ __attribute__((always_inline)) inline int64_t wave_last_free_w(const 
     if (nin == 64) x = fold64(w);
     else if (nin > 0) fold64_split(w, nin, x, unused);
     // exclusive ordered scan over lanes
-    Summ inc = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        Summ y;
-        y.q = __shfl_up(inc.q, off);
-        y.m = __shfl_up(inc.m, off);
-        if ((int)lane >= off) inc = summ_cat(y, inc);
-    }
-    Summ ex;
-    ex.q = __shfl_up(inc.q, 1);
-    ex.m = __shfl_up(inc.m, 1);
-    if (lane == 0) ex = Summ{0, 0};
+    const Summ ex = summ_excl_dpp(summ_scan_dpp(x));
     int32_t c = max(ex.m, carry_in + ex.q);
     int32_t last = -1;
 #pragma unroll
@@ -4459,9 +4437,7 @@ __device__ __attribute__((always_inline)) inline int64_t wave_last_free_w(const 
             c = ok ? max(0, t - 1) : c;
         }
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) last = max(last, __shfl_xor(last, off));
-    return last;
+    return (int32_t)wave_max_u32((uint32_t)(last + 1)) - 1;  // (-1 or a slot below 2^31)
 }
 // sel_prof: add the ticks since *t to st->sel_prof[k] (one thread; fire-and-forget atomic)
 __device__ inline void sel_tick(DevState *st, int k, unsigned long long *t) {
@@ -4523,23 +4499,12 @@ __device__ inline void refresh_prefix(const HomeView &V, uint32_t *cs) {
         const int32_t c = wave_carry_into(V, 0u);
         if (lane == 0) s_c0 = c;
     }
-    Summ inc = S;  // inclusive ordered scan over the wave's super-blocks
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        Summ y;
-        y.q = __shfl_up(inc.q, off);
-        y.m = __shfl_up(inc.m, off);
-        if ((int)lane >= off) inc = summ_cat(y, inc);
-    }
+    const Summ inc = summ_scan_dpp(S);  // inclusive ordered scan over the wave's super-blocks
     if (lane == 63) s_tot[w] = inc;
     __syncthreads();
     Summ pre{0, 0};
     for (uint32_t k = 0; k < w; k++) pre = summ_cat(pre, s_tot[k]);
-    Summ ex;
-    ex.q = __shfl_up(inc.q, 1);
-    ex.m = __shfl_up(inc.m, 1);
-    if (lane == 0) ex = Summ{0, 0};
-    const Summ E = summ_cat(pre, ex);  // super-blocks [0, tid)
+    const Summ E = summ_cat(pre, summ_excl_dpp(inc));  // super-blocks [0, tid)
     const int32_t c0 = s_c0;
     const int32_t cin = max(E.m, c0 + E.q);
     if (tid < V.nsb) st_wt(cs + tid, (uint32_t)cin);
@@ -4631,6 +4596,46 @@ __device__ inline void minK_merge(uint64_t (&a)[K], const uint64_t (&b)[K]) {
 #pragma unroll
     for (int k = 0; k < K; k++) a[k] = r[k];
 }
+// The K smallest of the wave (and the largest home) by DPP, every lane active: a butterfly inside each 16-lane row
+// (quad_perm [1,0,3,2], [2,3,0,1], half-row mirror, row mirror -- each joins two disjoint halves, so no entry is
+// merged twice), then the four rows' lists from v_readlane (wave-uniform results)
+template <int CTRL>
+__device__ __attribute__((always_inline)) inline uint64_t dpp_mov64(uint64_t x) {
+    return (uint64_t)dpp_mov<CTRL>((uint32_t)x) | ((uint64_t)dpp_mov<CTRL>((uint32_t)(x >> 32)) << 32);
+}
+__device__ __attribute__((always_inline)) inline uint64_t lane_bcast64(uint64_t x, int l) {
+    return (uint64_t)lane_bcast((uint32_t)x, l) | ((uint64_t)lane_bcast((uint32_t)(x >> 32), l) << 32);
+}
+template <int K, int CTRL>
+__device__ __attribute__((always_inline)) inline void minK_dpp_step(uint64_t (&m)[K], uint32_t &hmax) {
+    uint64_t b[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) b[k] = dpp_mov64<CTRL>(m[k]);
+    minK_merge<K>(m, b);
+    hmax = max(hmax, dpp_mov<CTRL>(hmax));
+}
+template <int K>
+__device__ __attribute__((always_inline)) inline void wave_minK_reduce_dpp(uint64_t (&m)[K], uint32_t &hmax) {
+    minK_dpp_step<K, 0xB1>(m, hmax);
+    minK_dpp_step<K, 0x4E>(m, hmax);
+    minK_dpp_step<K, 0x141>(m, hmax);
+    minK_dpp_step<K, 0x140>(m, hmax);
+    uint64_t r[K];
+    uint32_t h = lane_bcast(hmax, 0);
+#pragma unroll
+    for (int k = 0; k < K; k++) r[k] = lane_bcast64(m[k], 0);
+#pragma unroll
+    for (int l = 16; l < 64; l += 16) {
+        uint64_t b[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) b[k] = lane_bcast64(m[k], l);
+        minK_merge<K>(r, b);
+        h = max(h, lane_bcast(hmax, l));
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) m[k] = r[k];
+    hmax = h;
+}
 template <int K>
 __device__ inline void wave_minK(const uint64_t *list, uint32_t len, uint64_t (&m)[K], uint32_t &hmax) {
     const uint32_t lane = threadIdx.x & 63;
@@ -4645,14 +4650,7 @@ __device__ inline void wave_minK(const uint64_t *list, uint32_t len, uint64_t (&
         minK_merge<K>(m, b);
         hmax = max(hmax, (uint32_t)(e >> 32));
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        uint64_t b[K];
-#pragma unroll
-        for (int k = 0; k < K; k++) b[k] = __shfl_xor(m[k], off);
-        minK_merge<K>(m, b);
-        hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
-    }
+    wave_minK_reduce_dpp<K>(m, hmax);  // (the caller's whole wave)
 }
 __device__ inline void wave_min3(const uint64_t *list, uint32_t len, uint64_t &m1, uint64_t &m2, uint64_t &m3, uint32_t &hmax) {
     const uint32_t lane = threadIdx.x & 63;
@@ -4663,12 +4661,9 @@ __device__ inline void wave_min3(const uint64_t *list, uint32_t len, uint64_t &m
         min3_merge(m1, m2, m3, e, ~0ull, ~0ull);
         hmax = max(hmax, (uint32_t)(e >> 32));
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint64_t b1 = __shfl_xor(m1, off), b2 = __shfl_xor(m2, off), b3 = __shfl_xor(m3, off);
-        min3_merge(m1, m2, m3, b1, b2, b3);
-        hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
-    }
+    uint64_t q[3] = {m1, m2, m3};  // (minK_merge<3> is min3_merge's rule; the caller's whole wave)
+    wave_minK_reduce_dpp<3>(q, hmax);
+    m1 = q[0]; m2 = q[1]; m3 = q[2];
 }
 // keys whose home lies in the 4096-slot blocks covering [x, y) (0 <= x < y <= C, C >= one super-block):
 // block summaries for the partial super-blocks at the two ends, super-block summaries between (one wave,
@@ -4796,12 +4791,10 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
                 if (e < m1) { m2 = m1; m1 = e; } else if (e < m2) m2 = e;
                 hmax = max(hmax, (uint32_t)(e >> 32));
             }
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                const uint64_t b1 = __shfl_xor(m1, off), b2 = __shfl_xor(m2, off);
-                min2_combine(m1, m2, b1, b2);
-                hmax = max(hmax, (uint32_t)__shfl_xor((int)hmax, off));
-            }
+            uint64_t q[2] = {m1, m2};  // (minK_merge<2> is min2_combine's rule; wave 0 whole)
+            wave_minK_reduce_dpp<2>(q, hmax);
+            m1 = q[0];
+            m2 = q[1];
         }
         if (lane == 0 && !(NT >= 512 && pair_x && m3_w4)) { s_m3 = m3; s_m4 = ~0ull; s_m5 = ~0ull; s_m6 = ~0ull; }
         const uint32_t h1 = (uint32_t)(m1 >> 32);
@@ -4832,8 +4825,10 @@ __device__ __attribute__((always_inline)) inline void decide_body(DevState *st, 
     if (NT >= 256 && plan_on && w == 3 && len) {
         uint64_t m1 = ~0ull;
         for (uint32_t i = lane; i < len; i += 64) m1 = min(m1, list[i]);
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) m1 = min(m1, (uint64_t)__shfl_xor(m1, off));
+        uint64_t q[1] = {m1};
+        uint32_t hx = 0;
+        wave_minK_reduce_dpp<1>(q, hx);  // (wave 3 whole)
+        m1 = q[0];
         if (lane == 0) plan_compute(plan, (uint32_t)m1, s_plan);
     }
     // rplan (a multi-merge round's select): wave 5 finds the next tied keys by home itself and loads their scan
@@ -5501,8 +5496,7 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
             uint32_t L = 0;
 #pragma unroll
             for (uint32_t u = 0; u < UR_U; u++) L = c[u] < Lp && c[u] >= theta && c[u] > L ? c[u] : L;
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) L = max(L, (uint32_t)__shfl_xor((int)L, off));
+            L = wave_max_u32(L);  // (waves 2..7 whole: DPP all-reduces)
             uint32_t m = 0, kk = NO_ID;
 #pragma unroll
             for (uint32_t u = 0; u < UR_U; u++) {
@@ -5511,8 +5505,8 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 kk = eq ? k[u] : kk;
             }
             const uint64_t has = __ballot(m != 0);
-            kk = has ? (uint32_t)__shfl((int)kk, __ffsll((unsigned long long)has) - 1) : NO_ID;
-            m = wave_sum(m);
+            kk = has ? (uint32_t)__builtin_amdgcn_readlane((int)kk, __ffsll((unsigned long long)has) - 1) : NO_ID;
+            m = wave_sum_u32(m);
             if (lane == 0) {
                 s_uw[(w * UR_L + l) * 3 + 0] = L;
                 s_uw[(w * UR_L + l) * 3 + 1] = m;
@@ -5605,12 +5599,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
                 uk[l] = NO_ID;
                 uc[l] = 0;
                 if (!go) continue;
-                uint32_t Lk = L < Lp ? L : 0u;
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) Lk = max(Lk, (uint32_t)__shfl_xor((int)Lk, off));
-                const uint32_t msum = wave_sum(Lk && L == Lk ? M : 0u);
+                const uint32_t Lk = wave_max_u32(L < Lp ? L : 0u);  // (wave 2 whole: DPP all-reduces)
+                const uint32_t msum = wave_sum_u32(Lk && L == Lk ? M : 0u);
                 const uint64_t has = __ballot(Lk && L == Lk);
-                const uint32_t key = has ? (uint32_t)__shfl((int)K, __ffsll((unsigned long long)has) - 1) : NO_ID;
+                const uint32_t key = has ? (uint32_t)__builtin_amdgcn_readlane((int)K, __ffsll((unsigned long long)has) - 1) : NO_ID;
                 // (a count held by several pairs is a tie: the Zig order decides it, so the names end; so does a self pair)
                 go = Lk && msum == 1 && key != NO_ID && (key & 0xFFFF) != (key >> 16);
                 if (go) { uk[l] = key; uc[l] = Lk; nu++; }

@@ -20,6 +20,24 @@ template <int CTRL>
 __device__ __attribute__((always_inline)) inline uint32_t dpp_mov(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
 }
+// all-reduces (every lane active), wave-uniform results: a butterfly inside each 16-lane row (quad_perm [1,0,3,2]
+// and [2,3,0,1], half-row mirror, row mirror: each step joins two disjoint halves), then the four rows by readlane
+__device__ __attribute__((always_inline)) inline uint32_t wave_max_u32(uint32_t x) {
+    x = max(x, dpp_mov<0xB1>(x));
+    x = max(x, dpp_mov<0x4E>(x));
+    x = max(x, dpp_mov<0x141>(x));
+    x = max(x, dpp_mov<0x140>(x));
+    return max(max((uint32_t)__builtin_amdgcn_readlane((int)x, 0), (uint32_t)__builtin_amdgcn_readlane((int)x, 16)),
+               max((uint32_t)__builtin_amdgcn_readlane((int)x, 32), (uint32_t)__builtin_amdgcn_readlane((int)x, 48)));
+}
+__device__ __attribute__((always_inline)) inline uint32_t wave_sum_u32(uint32_t x) {
+    x += dpp_mov<0xB1>(x);
+    x += dpp_mov<0x4E>(x);
+    x += dpp_mov<0x141>(x);
+    x += dpp_mov<0x140>(x);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 0) + (uint32_t)__builtin_amdgcn_readlane((int)x, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)x, 32) + (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+}
 // lane l's x, as a scalar
 __device__ __attribute__((always_inline)) inline uint32_t lane_bcast(uint32_t x, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
