@@ -1,7 +1,8 @@
 // Checks the DPP wave helpers of zig-bpe_amd/csrc/wave.hpp against their definitions on random data:
 // wave_shr1 / wave_shl1 (lane i <- lane i -/+ 1, the edge lane <- fill), lane_bcast, wave_incl_scan_dpp,
 // wave_max_u32, wave_sum_u32, and kernels.hpp's DPP reductions: the ordered carry-summary scan (summ_scan_dpp,
-// summ_excl_dpp, wave_reduce_summ), the argmax's wave_max_dpp and the tie decision's wave_minK_reduce_dpp.
+// summ_excl_dpp, wave_reduce_summ), the argmax's wave_max_dpp, the tie decision's wave_minK_reduce_dpp and the
+// self-pair run-parity block scan (self_block_scan, a 256-thread block).
 //   hipcc -O3 --offload-arch=gfx950 -o tools/dpp_check tools/dpp_check.hip && tools/dpp_check
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -12,7 +13,7 @@
 using namespace zbpe;
 
 constexpr int WAVES = 64;
-constexpr int NOUT = 21;
+constexpr int NOUT = 23;
 
 __global__ void dpp_kernel(const uint32_t *in, uint32_t *out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -40,7 +41,14 @@ __global__ void dpp_kernel(const uint32_t *in, uint32_t *out) {
     wave_minK_reduce_dpp<3>(q, hm);
     for (int k = 0; k < 3; k++) { o[14 + 2 * k] = (uint32_t)q[k]; o[15 + 2 * k] = (uint32_t)(q[k] >> 32); }
     o[20] = hm;
+    __shared__ uint8_t s_wave[SELF_THREADS / 64];
+    uint8_t tot = 0;
+    o[21] = self_block_scan((uint8_t)(x & 3u), s_wave, &tot);
+    o[22] = tot;
 }
+
+// host restatement of self_compose (g after f)
+static uint8_t self_compose_h(uint8_t f, uint8_t g) { return (g & 1) ? (uint8_t)((f & 1) | ((f ^ g) & 2)) : g; }
 
 int main() {
     const int n = WAVES * 64;
@@ -78,6 +86,12 @@ int main() {
             else if (e < k3[2]) k3[2] = e;
         }
         int32_t pq = 0, pm = 0;  // the running inclusive composition
+        // the run-parity functions (bit0: all a, bit1: parity) composed over the block (4 waves) before each thread
+        const int blk0 = (w / 4) * 256;
+        uint8_t bt = 1;
+        for (int t = 0; t < 256; t++) bt = self_compose_h(bt, (uint8_t)(h_in[blk0 + t] & 3u));
+        uint8_t run = 1;
+        for (int t = blk0; t < w * 64; t++) run = self_compose_h(run, (uint8_t)(h_in[t] & 3u));
         for (int l = 0; l < 64; l++) {
             const int i = w * 64 + l;
             const uint32_t *o = h_out + (size_t)i * NOUT, f = o[4];
@@ -88,11 +102,13 @@ int main() {
                 pm = m > pm + q ? m : pm + q;
                 pq += q;
             }
-            const uint32_t e[21] = {l ? h_in[i - 1] : f, l < 63 ? h_in[i + 1] : f, h_in[w * 64 + 63], sum, f, wmax, wsum,
+            const uint8_t ex_self = run;
+            run = self_compose_h(run, (uint8_t)(h_in[i] & 3u));
+            const uint32_t e[23] = {l ? h_in[i - 1] : f, l < 63 ? h_in[i + 1] : f, h_in[w * 64 + 63], sum, f, wmax, wsum,
                                     (uint32_t)pq, (uint32_t)pm, (uint32_t)eq, (uint32_t)em, (uint32_t)tq, (uint32_t)tm, mrec,
                                     (uint32_t)k3[0], (uint32_t)(k3[0] >> 32), (uint32_t)k3[1], (uint32_t)(k3[1] >> 32),
-                                    (uint32_t)k3[2], (uint32_t)(k3[2] >> 32), hm};
-            for (int k = 0; k < 21; k++)
+                                    (uint32_t)k3[2], (uint32_t)(k3[2] >> 32), hm, ex_self, bt};
+            for (int k = 0; k < 23; k++)
                 if (o[k] != e[k] && bad++ < 8) printf("wave %d lane %d op %d: got %08x want %08x\n", w, l, k, o[k], e[k]);
         }
     }

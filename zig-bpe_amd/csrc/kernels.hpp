@@ -3373,16 +3373,22 @@ __device__ inline uint8_t self_walk(const uint32_t (&w)[16], uint32_t a, int x_i
 }
 // exclusive composition of the threads' functions in thread order (wave shuffles, then the waves
 // through LDS); *total: the whole block's function
+// (every thread of the block; the wave scan by DPP: row_shr:1,2,4,8, then row_bcast:15 / :31, a lane with no source
+// composing the identity 1 -- x -> x)
+template <int CTRL, int ROWS>
+__device__ __attribute__((always_inline)) inline uint8_t self_dpp(uint8_t f) {
+    return (uint8_t)__builtin_amdgcn_update_dpp(1, (int)f, CTRL, ROWS, 0xF, false);
+}
 __device__ inline uint8_t self_block_scan(uint8_t f, uint8_t *s_wave, uint8_t *total) {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t inc = f;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint8_t y = (uint8_t)__shfl_up((int)inc, off);
-        if ((int)lane >= off) inc = self_compose(y, inc);
-    }
-    uint8_t ex = (uint8_t)__shfl_up((int)inc, 1);
-    if (lane == 0) ex = 1;  // identity
+    inc = self_compose(self_dpp<0x111, 0xF>(inc), inc);
+    inc = self_compose(self_dpp<0x112, 0xF>(inc), inc);
+    inc = self_compose(self_dpp<0x114, 0xF>(inc), inc);
+    inc = self_compose(self_dpp<0x118, 0xF>(inc), inc);
+    inc = self_compose(self_dpp<0x142, 0xA>(inc), inc);
+    inc = self_compose(self_dpp<0x143, 0xC>(inc), inc);
+    const uint8_t ex = (uint8_t)wave_shr1(inc, 1u);  // (lane 0: the identity)
     if (lane == 63) s_wave[wv] = inc;
     __syncthreads();
     uint8_t pre = 1;
@@ -3561,7 +3567,7 @@ __global__ void __launch_bounds__(SELF_THREADS) zbpe_scan_self(ScanArgs A0, cons
             if (hm) {
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(&s_nrec, (uint32_t)__popcll(hm));
-                base = (uint32_t)__shfl((int)base, 0);
+                base = lane_bcast(base, 0);
                 if (hit) s_rec[base + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint32_t)p;
             }
         }
@@ -5682,10 +5688,10 @@ __global__ void __launch_bounds__(NEXT_THREADS, 4) zbpe_select_next(DevState *st
             const uint32_t c = t ? s_pt[b] : 0u;
             const uint64_t m = __ballot(t);
             const uint32_t below = (uint32_t)__popcll(m & ((1ull << tid) - 1ull));
-            const uint32_t inc = wave_incl_scan(c);
+            const uint32_t inc = wave_incl_scan_dpp(c);  // (wave 0 whole, a uniform trip count)
             if (t) { s_tb[k + below] = b; s_to[k + below] = o + inc - c; }
             k += (uint32_t)__popcll(m);
-            o += (uint32_t)__shfl((int)inc, 63);
+            o += lane_bcast(inc, 63);
         }
         if (tid == 0) { s_ntb = k; s_to[k] = o; }
     }
