@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "zig-bpe_amd"))
 
 # tools/pmc_traffic.py output: this round's PMC passes when present, else the last round's
-PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", f"r0{r}_c4_pmc_traffic.json") for r in (5, 4, 3, 2))
+PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", f"r0{r}_c4_pmc_traffic.json") for r in (6, 5, 4, 3, 2))
                     if os.path.exists(p)), os.path.join(ROOT, "profiles", "r02_c4_pmc_traffic.json"))
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured copy)
 C4_SEED = 0x5EED0004

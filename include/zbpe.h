@@ -182,7 +182,10 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * launch triple while no pair the merged members made reaches the next member's count; rounds in every list streak), "lp_lazy" (0/1,
  * default 1: the stream's last pair is looked up only for a tie whose Zig capacity depends on it),
  * "refresh_wgs" (home refresh workgroups of a select), "self_batch" (0/1, default 1: a self pair (a, a) whose
- * list the host path would walk runs inside a batch instead of halting it). */
+ * list the host path would walk runs inside a batch instead of halting it), "round_streak" (0/1, default 1: rounds
+ * only in list streaks; 0: also in batches with stream-form scans when the arena holds their records), "handover"
+ * (1-3, default 2: sharded ranks replicate once top count * list_start * world^handover < live tokens),
+ * "scan_batch" (0-2, default 1: stream scans batch sparse tiles' candidates when count * 32 < slots; 2: always). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* printTimeStats (src/utils/time_statistics.zig:36-60): the reference's "Time statistics" text for
