@@ -156,7 +156,7 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * holes > slots/den), "scan_blocks_per_cu", "scan_variant" (0..7: unroll, load kind, phase-2 form;
  * see engine.hip kScanVariants), "dense_hist" (0/1: the full pair histogram of a byte stream counts every byte pair in a fixed 16-bit LDS bin),
  * "scan_batch" (stream form, variants with cross-tile candidate batching:
- * 0 off, 1 for sparse pairs, 2 always), "hot_target" (ids kept by the argmax hot list),
+ * 0 off, 1 for sparse pairs -- count * 32 < slots --, 2 always), "hot_target" (ids kept by the argmax hot list),
  * "block_skip" (0/1: stream only the 8192-slot blocks that hold the pair's rarer token),
  * "trace" (0/1: record per-merge timings, see zbpe_trace), "merge_batch" (merges enqueued per host
  * sync, 1 = synchronous loop), "merge_timing" (HIP events around every N-th merge of a batch; 0 =
@@ -184,8 +184,7 @@ zbpe_status zbpe_tokens(zbpe_ctx *ctx, uint16_t *out, size_t cap, size_t *n_toke
  * "refresh_wgs" (home refresh workgroups of a select), "self_batch" (0/1, default 1: a self pair (a, a) whose
  * list the host path would walk runs inside a batch instead of halting it), "round_streak" (0/1, default 1: rounds
  * only in list streaks; 0: also in batches with stream-form scans when the arena holds their records), "handover"
- * (1-3, default 2: sharded ranks replicate once top count * list_start * world^handover < live tokens),
- * "scan_batch" (0-2, default 1: stream scans batch sparse tiles' candidates when count * 32 < slots; 2: always). */
+ * (1-3, default 2: sharded ranks replicate once top count * list_start * world^handover < live tokens). */
 zbpe_status zbpe_set_option(zbpe_ctx *ctx, const char *name, int64_t value);
 
 /* printTimeStats (src/utils/time_statistics.zig:36-60): the reference's "Time statistics" text for
