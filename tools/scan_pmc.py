@@ -19,6 +19,7 @@ def main():
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--n-bytes", type=int, default=1 << 30)
     p.add_argument("--summarise", default="")
+    p.add_argument("--variant", type=int, default=-1, help="option scan_variant (7: the batched form)")
     a = p.parse_args()
     if a.summarise:
         tot, launches = defaultdict(float), set()
@@ -34,6 +35,8 @@ def main():
     x, y = (int(v) for v in a.pair.split(","))
     e = zbpe.Engine(0)
     e.upload(zbpe.synth_corpus("words_utf8", 0x5EED0004, a.n_bytes, threads=16))
+    if a.variant >= 0:
+        e.set_option("scan_variant", a.variant)
     ms, gbps = e.bench_scan(x, y, a.reps)
     print(json.dumps({"pair": [x, y], "ms": ms, "GBps": gbps}))
     e.close()

@@ -5904,9 +5904,8 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist(const uint16_t *__r
         for (int u = 0; u < PH_U; u++) {
             const int64_t vi = tile + u * 64 + lane;
             // the next vector's first token: the next lane's, or (lane 63) the next row's lane 0 / the tile's end
-            uint32_t nx = (uint32_t)__shfl_down((int)(v[u].x & 0xFFFFu), 1);
-            const uint32_t row0 = u + 1 < PH_U ? (uint32_t)__shfl((int)(v[u + 1 < PH_U ? u + 1 : u].x & 0xFFFFu), 0) : after_tile;
-            if (lane == 63) nx = row0;
+            // (DPP: the next lane's first token; lane 63 the next row's lane 0, or the token after the tile)
+            uint32_t nx = wave_shl1(v[u].x & 0xFFFFu, u + 1 < PH_U ? lane_bcast(v[u + 1 < PH_U ? u + 1 : u].x & 0xFFFFu, 0) : after_tile);
             const int64_t p8 = vi * 8 + 8;
             if (p8 >= n) nx = p8 == n && next_tok >= 0 ? (uint32_t)next_tok : PH_EMPTY;
             if (vi >= nvec) continue;
@@ -6029,9 +6028,8 @@ __global__ void __launch_bounds__(PH_THREADS) zbpe_pair_hist_bytes(const uint16_
 #pragma unroll
         for (int u = 0; u < PH_U; u++) {
             const int64_t vi = tile + u * 64 + lane;
-            uint32_t nx = (uint32_t)__shfl_down((int)v[u].x, 1);
-            const uint32_t row0 = u + 1 < PH_U ? (uint32_t)__shfl((int)v[u + 1 < PH_U ? u + 1 : u].x, 0) : after_tile;
-            if (lane == 63) nx = row0;
+            // (DPP: the next lane's first word; lane 63 the next row's lane 0, or the word after the tile)
+            const uint32_t nx = wave_shl1(v[u].x, u + 1 < PH_U ? lane_bcast(v[u + 1 < PH_U ? u + 1 : u].x, 0) : after_tile);
             if (vi >= nfull) continue;
             // ab = a << 8 | b by one byte permute per pair: a pair inside a word (t0, t1) takes bytes {2, 0}
             // of it, a pair across words (t1 of w, t0 of the next) bytes {4, 2} of (next : w)
